@@ -1,0 +1,605 @@
+// GroupNorm (+ fused per-(n,c) bias before the norm, + fused SiLU after) for gfx950.
+//
+// Replaces the nn.GroupNorm -> act chains of the NCSN++ / DDPM++ residual blocks
+// (models/layerspp.py:242-274, :200-209; models/ncsnpp.py:371-377) and folds in the
+// time-embedding bias `h += Dense_0(act(temb))[:, :, None, None]` that sits right
+// before GroupNorm_1 (layerspp.py:263-265).
+//
+// NCHW makes every (sample, group) a contiguous slab of S = (C/G)*HW floats, so:
+//  * resident path (S <= 64K floats): one workgroup per slab, the slab is loaded
+//    ONCE into registers with 16-byte loads, mean and variance are exact two-pass
+//    reductions over the registers, and the normalized output is written once:
+//    1 read + 1 write of HBM per element (the algorithmic minimum).
+//  * split path (larger slabs): per-chunk (count, mean, M2) partials combined with
+//    Chan's formula in a fixed order (deterministic), then a normalize pass.
+// Backward mirrors this (resident: x and dy read once; dgamma/dbeta emitted as
+// per-(n,c) partial sums that the host reduces over n).
+#include "bpk_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int kWave = 64;
+
+template <int T>
+__device__ inline float block_sum(float v, float* sbuf) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  const int wid = threadIdx.x / kWave;
+  const int lane = threadIdx.x % kWave;
+  __syncthreads();
+  if (lane == 0) sbuf[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < T / kWave; ++i) r += sbuf[i];
+  return r;
+}
+
+__device__ inline float act_fwd(float z, int act) {
+  return act == 1 ? z / (1.f + expf(-z)) : z;
+}
+// d act / dz
+__device__ inline float act_bwd(float z, int act) {
+  if (act != 1) return 1.f;
+  const float s = 1.f / (1.f + expf(-z));
+  return s * (1.f + z * (1.f - s));
+}
+
+// Element access for a slab: W = 4 (float4 path) or 1 (scalar path).
+template <int W>
+struct Vec;
+template <>
+struct Vec<4> {
+  static __device__ inline void load(const float* p, float* v) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  static __device__ inline void store(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <>
+struct Vec<1> {
+  static __device__ inline void load(const float* p, float* v) { v[0] = *p; }
+  static __device__ inline void store(float* p, const float* v) { *p = v[0]; }
+};
+
+// ---------------------------------------------------------------- forward
+
+template <int T, int VPT, int W>
+__global__ __launch_bounds__(T) void gn_fwd_resident(const float* __restrict__ x,
+                                                     const float* __restrict__ bias_nc,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     float* __restrict__ y, float* mean_out,
+                                                     float* rstd_out, int C, int HW, int G,
+                                                     float eps, int act) {
+  __shared__ float sbuf[T / kWave];
+  const int ng = blockIdx.x;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int S = cpg * HW;
+  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const int tid = threadIdx.x;
+
+  float v[VPT][W];
+  float lsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = (k * T + tid) * W;
+    if (e < S) {
+      Vec<W>::load(x + base + e, v[k]);
+      if (bias_nc) {
+        const float b = bias_nc[(int64_t)n * C + g * cpg + e / HW];
+#pragma unroll
+        for (int q = 0; q < W; ++q) v[k][q] += b;
+      }
+#pragma unroll
+      for (int q = 0; q < W; ++q) lsum += v[k][q];
+    }
+  }
+  const float mean = block_sum<T>(lsum, sbuf) / (float)S;
+  float lm2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = (k * T + tid) * W;
+    if (e < S) {
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const float d = v[k][q] - mean;
+        lm2 += d * d;
+      }
+    }
+  }
+  const float var = block_sum<T>(lm2, sbuf) / (float)S;
+  const float rstd = 1.f / sqrtf(var + eps);
+  if (tid == 0) {
+    if (mean_out) mean_out[ng] = mean;
+    if (rstd_out) rstd_out[ng] = rstd;
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = (k * T + tid) * W;
+    if (e < S) {
+      const int c = g * cpg + e / HW;
+      const float ga = gamma ? gamma[c] : 1.f;
+      const float be = beta ? beta[c] : 0.f;
+      float o[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) o[q] = act_fwd((v[k][q] - mean) * rstd * ga + be, act);
+      Vec<W>::store(y + base + e, o);
+    }
+  }
+}
+
+// split path, stage 1: per-chunk (mean, M2) of CHUNK = T*VPT*W elements
+template <int T, int VPT, int W>
+__global__ __launch_bounds__(T) void gn_fwd_partial(const float* __restrict__ x,
+                                                    const float* __restrict__ bias_nc,
+                                                    float* __restrict__ part, int C, int HW,
+                                                    int G, int splits) {
+  __shared__ float sbuf[T / kWave];
+  const int split = blockIdx.x;
+  const int ng = blockIdx.y;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int S = cpg * HW;
+  constexpr int CHUNK = T * VPT * W;
+  const int e0 = split * CHUNK;
+  const int cnt = min(CHUNK, S - e0);
+  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const int tid = threadIdx.x;
+  float v[VPT][W];
+  float lsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = e0 + (k * T + tid) * W;
+    if (e < S) {
+      Vec<W>::load(x + base + e, v[k]);
+      if (bias_nc) {
+        const float b = bias_nc[(int64_t)n * C + g * cpg + e / HW];
+#pragma unroll
+        for (int q = 0; q < W; ++q) v[k][q] += b;
+      }
+#pragma unroll
+      for (int q = 0; q < W; ++q) lsum += v[k][q];
+    }
+  }
+  const float m = block_sum<T>(lsum, sbuf) / (float)cnt;
+  float lm2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = e0 + (k * T + tid) * W;
+    if (e < S) {
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const float d = v[k][q] - m;
+        lm2 += d * d;
+      }
+    }
+  }
+  const float m2 = block_sum<T>(lm2, sbuf);
+  if (tid == 0) {
+    float* p = part + ((int64_t)ng * splits + split) * 3;
+    p[0] = (float)cnt;
+    p[1] = m;
+    p[2] = m2;
+  }
+}
+
+// Chan et al. parallel combination, fixed order -> deterministic
+__device__ inline void combine_partials(const float* p, int splits, float& mean, float& m2,
+                                        float& count) {
+  count = p[0];
+  mean = p[1];
+  m2 = p[2];
+  for (int s = 1; s < splits; ++s) {
+    const float nb = p[3 * s];
+    const float mb = p[3 * s + 1];
+    const float m2b = p[3 * s + 2];
+    const float nn = count + nb;
+    const float d = mb - mean;
+    mean += d * (nb / nn);
+    m2 += m2b + d * d * (count * nb / nn);
+    count = nn;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void gn_fwd_apply(const float* __restrict__ x,
+                                                    const float* __restrict__ bias_nc,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta,
+                                                    const float* __restrict__ part,
+                                                    float* __restrict__ y, float* mean_out,
+                                                    float* rstd_out, int C, int HW, int G,
+                                                    int splits, int chunk, float eps, int act) {
+  __shared__ float s_stat[2];
+  const int split = blockIdx.x;
+  const int ng = blockIdx.y;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int S = cpg * HW;
+  if (threadIdx.x == 0) {
+    float mean, m2, count;
+    combine_partials(part + (int64_t)ng * splits * 3, splits, mean, m2, count);
+    const float rstd = 1.f / sqrtf(m2 / count + eps);
+    s_stat[0] = mean;
+    s_stat[1] = rstd;
+    if (split == 0) {
+      if (mean_out) mean_out[ng] = mean;
+      if (rstd_out) rstd_out[ng] = rstd;
+    }
+  }
+  __syncthreads();
+  const float mean = s_stat[0];
+  const float rstd = s_stat[1];
+  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const int e_end = min(S, (split + 1) * chunk);
+  for (int e = split * chunk + threadIdx.x * W; e < e_end; e += 256 * W) {
+    float v[W];
+    Vec<W>::load(x + base + e, v);
+    const int c = g * cpg + e / HW;
+    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+    const float ga = gamma ? gamma[c] : 1.f;
+    const float be = beta ? beta[c] : 0.f;
+    float o[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) o[q] = act_fwd((v[q] + b - mean) * rstd * ga + be, act);
+    Vec<W>::store(y + base + e, o);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+
+template <int T, int VPT, int W>
+__global__ __launch_bounds__(T) void gn_bwd_resident(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, float* __restrict__ dx,
+    float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C, int HW, int G, int act) {
+  extern __shared__ float sdyn[];  // [T/64] reduce buffer + 2*cpg channel partials
+  float* sbuf = sdyn;
+  float* s_dg = sdyn + T / kWave;
+  const int ng = blockIdx.x;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int S = cpg * HW;
+  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const int tid = threadIdx.x;
+  const float mean = mean_in[ng];
+  const float rstd = rstd_in[ng];
+  for (int i = tid; i < 2 * cpg; i += T) s_dg[i] = 0.f;
+  __syncthreads();
+
+  float xh[VPT][W], dxh[VPT][W];
+  float la = 0.f, lb = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = (k * T + tid) * W;
+    if (e < S) {
+      const int cl = e / HW;
+      const int c = g * cpg + cl;
+      const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+      const float ga = gamma ? gamma[c] : 1.f;
+      const float be = beta ? beta[c] : 0.f;
+      float xv[W], gv[W];
+      Vec<W>::load(x + base + e, xv);
+      Vec<W>::load(dy + base + e, gv);
+      float pg = 0.f, pb = 0.f;
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const float xhat = (xv[q] + b - mean) * rstd;
+        const float dz = gv[q] * act_bwd(xhat * ga + be, act);
+        pg += dz * xhat;
+        pb += dz;
+        xh[k][q] = xhat;
+        dxh[k][q] = dz * ga;
+        la += dxh[k][q];
+        lb += dxh[k][q] * xhat;
+      }
+      if (dgamma_nc || dbeta_nc) {
+        atomicAdd(&s_dg[cl], pg);
+        atomicAdd(&s_dg[cpg + cl], pb);
+      }
+    }
+  }
+  const float A = block_sum<T>(la, sbuf) / (float)S;
+  const float Bm = block_sum<T>(lb, sbuf) / (float)S;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int e = (k * T + tid) * W;
+    if (e < S) {
+      float o[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) o[q] = rstd * (dxh[k][q] - A - xh[k][q] * Bm);
+      Vec<W>::store(dx + base + e, o);
+    }
+  }
+  // block_sum's barriers ordered every LDS atomic before this read
+  for (int i = tid; i < cpg; i += T) {
+    if (dgamma_nc) dgamma_nc[(int64_t)n * C + g * cpg + i] = s_dg[i];
+    if (dbeta_nc) dbeta_nc[(int64_t)n * C + g * cpg + i] = s_dg[cpg + i];
+  }
+}
+
+// split backward stage 1: chunk sums of dxhat and dxhat*xhat; dgamma/dbeta via global atomics
+template <int W>
+__global__ __launch_bounds__(256) void gn_bwd_partial(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    float* __restrict__ part, float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C,
+    int HW, int G, int splits, int chunk, int act) {
+  __shared__ float sbuf[256 / kWave];
+  const int split = blockIdx.x;
+  const int ng = blockIdx.y;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int S = cpg * HW;
+  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const float mean = mean_in[ng];
+  const float rstd = rstd_in[ng];
+  float la = 0.f, lb = 0.f;
+  const int e_end = min(S, (split + 1) * chunk);
+  int cur_c = -1;
+  float pg = 0.f, pb = 0.f;
+  for (int e = split * chunk + threadIdx.x * W; e < e_end; e += 256 * W) {
+    const int c = g * cpg + e / HW;
+    if (c != cur_c) {
+      if (cur_c >= 0) {
+        if (dgamma_nc) atomicAdd(&dgamma_nc[(int64_t)n * C + cur_c], pg);
+        if (dbeta_nc) atomicAdd(&dbeta_nc[(int64_t)n * C + cur_c], pb);
+      }
+      cur_c = c;
+      pg = 0.f;
+      pb = 0.f;
+    }
+    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+    const float ga = gamma ? gamma[c] : 1.f;
+    const float be = beta ? beta[c] : 0.f;
+    float xv[W], gv[W];
+    Vec<W>::load(x + base + e, xv);
+    Vec<W>::load(dy + base + e, gv);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const float xhat = (xv[q] + b - mean) * rstd;
+      const float dz = gv[q] * act_bwd(xhat * ga + be, act);
+      pg += dz * xhat;
+      pb += dz;
+      la += dz * ga;
+      lb += dz * ga * xhat;
+    }
+  }
+  if (cur_c >= 0) {
+    if (dgamma_nc) atomicAdd(&dgamma_nc[(int64_t)n * C + cur_c], pg);
+    if (dbeta_nc) atomicAdd(&dbeta_nc[(int64_t)n * C + cur_c], pb);
+  }
+  const float A = block_sum<256>(la, sbuf);
+  const float B = block_sum<256>(lb, sbuf);
+  if (threadIdx.x == 0) {
+    part[((int64_t)ng * splits + split) * 2] = A;
+    part[((int64_t)ng * splits + split) * 2 + 1] = B;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void gn_bwd_apply(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const float* __restrict__ part, float* __restrict__ dx, int C, int HW, int G, int splits,
+    int chunk, int act) {
+  const int split = blockIdx.x;
+  const int ng = blockIdx.y;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int S = cpg * HW;
+  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const float mean = mean_in[ng];
+  const float rstd = rstd_in[ng];
+  float A = 0.f, B = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    A += part[((int64_t)ng * splits + s) * 2];
+    B += part[((int64_t)ng * splits + s) * 2 + 1];
+  }
+  A /= (float)S;
+  B /= (float)S;
+  const int e_end = min(S, (split + 1) * chunk);
+  for (int e = split * chunk + threadIdx.x * W; e < e_end; e += 256 * W) {
+    const int c = g * cpg + e / HW;
+    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+    const float ga = gamma ? gamma[c] : 1.f;
+    const float be = beta ? beta[c] : 0.f;
+    float xv[W], gv[W], o[W];
+    Vec<W>::load(x + base + e, xv);
+    Vec<W>::load(dy + base + e, gv);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const float xhat = (xv[q] + b - mean) * rstd;
+      const float dxhat = gv[q] * act_bwd(xhat * ga + be, act) * ga;
+      o[q] = rstd * (dxhat - A - xhat * B);
+    }
+    Vec<W>::store(dx + base + e, o);
+  }
+}
+
+// ---------------------------------------------------------------- dispatch
+
+constexpr int kSplitChunk = 256 * 16 * 4;  // floats per split-path chunk (W = 4)
+
+struct Plan {
+  bool resident;
+  int W;
+  int splits;
+  int chunk;
+};
+
+Plan make_plan(int64_t S, int64_t HW, bool aligned, int64_t resident_max) {
+  Plan p{};
+  p.W = (HW % 4 == 0 && aligned) ? 4 : 1;
+  p.resident = S <= resident_max;
+  p.chunk = kSplitChunk / (4 / p.W);
+  p.splits = (int)bpk::ceil_div(S, p.chunk);
+  return p;
+}
+
+template <int W>
+int fwd_resident_dispatch(int64_t S, const float* x, const float* bias, const float* gamma,
+                          const float* beta, float* y, float* mean, float* rstd, int N, int C,
+                          int HW, int G, float eps, int act, hipStream_t st) {
+  const int64_t units = bpk::ceil_div(S, W);
+  dim3 grid(N * G);
+#define GN_FWD(T_, V_)                                                                         \
+  if (units <= (int64_t)(T_) * (V_)) {                                                         \
+    hipLaunchKernelGGL((gn_fwd_resident<T_, V_, W>), grid, dim3(T_), 0, st, x, bias, gamma,   \
+                       beta, y, mean, rstd, C, HW, G, eps, act);                               \
+    BPK_LAUNCH_CHECK("group_norm_fwd_resident");                                              \
+    return BPK_OK;                                                                             \
+  }
+  GN_FWD(256, 1)
+  GN_FWD(256, 2)
+  GN_FWD(256, 4)
+  GN_FWD(256, 8)
+  GN_FWD(512, 8)
+  GN_FWD(1024, 8)
+  GN_FWD(1024, 16)
+#undef GN_FWD
+  bpk::set_error("group_norm: slab too large for resident path");
+  return BPK_ERR_ARG;
+}
+
+template <int W>
+int bwd_resident_dispatch(int64_t S, const float* dy, const float* x, const float* bias,
+                          const float* gamma, const float* beta, const float* mean,
+                          const float* rstd, float* dx, float* dg, float* db, int N, int C, int HW,
+                          int G, int act, hipStream_t st) {
+  const int64_t units = bpk::ceil_div(S, W);
+  const int cpg = C / G;
+  dim3 grid(N * G);
+#define GN_BWD(T_, V_)                                                                         \
+  if (units <= (int64_t)(T_) * (V_)) {                                                         \
+    const size_t sh = sizeof(float) * ((T_) / kWave + 2 * cpg);                                \
+    hipLaunchKernelGGL((gn_bwd_resident<T_, V_, W>), grid, dim3(T_), sh, st, dy, x, bias,     \
+                       gamma, beta, mean, rstd, dx, dg, db, C, HW, G, act);                    \
+    BPK_LAUNCH_CHECK("group_norm_bwd_resident");                                              \
+    return BPK_OK;                                                                             \
+  }
+  GN_BWD(256, 1)
+  GN_BWD(256, 2)
+  GN_BWD(256, 4)
+  GN_BWD(256, 8)
+  GN_BWD(512, 8)
+  GN_BWD(1024, 8)
+#undef GN_BWD
+  bpk::set_error("group_norm: slab too large for resident backward");
+  return BPK_ERR_ARG;
+}
+
+constexpr int64_t kFwdResidentMax = 1024 * 16 * 4;
+constexpr int64_t kBwdResidentMax = 1024 * 8 * 4;
+
+bool is_aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int64_t bpk_group_norm_workspace_bytes(int N, int C, int64_t HW, int G) {
+  if (N <= 0 || G <= 0 || C % G != 0) return 0;
+  const int64_t S = (int64_t)(C / G) * HW;
+  const int64_t splits = bpk::ceil_div(S, kSplitChunk / 4);  // worst case W = 1
+  return (int64_t)N * G * splits * 3 * (int64_t)sizeof(float);
+}
+
+extern "C" int bpk_group_norm_fwd_f32(const float* x, const float* bias_nc, const float* gamma,
+                                      const float* beta, float* y, float* mean, float* rstd,
+                                      void* workspace, int N, int C, int64_t HW, int G, float eps,
+                                      int act, void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && G > 0, "group_norm: bad shape");
+  BPK_REQUIRE(C % G == 0, "group_norm: C (%d) not divisible by G (%d)", C, G);
+  BPK_REQUIRE(act == 0 || act == 1, "group_norm: act must be 0 (none) or 1 (silu)");
+  BPK_REQUIRE(HW < (1ll << 31) / 64, "group_norm: plane too large");
+  if (N == 0) return BPK_OK;
+  const int64_t S = (int64_t)(C / G) * HW;
+  BPK_REQUIRE(S < (1ll << 31), "group_norm: slab too large");
+  hipStream_t st = bpk::as_stream(stream);
+  const Plan p = make_plan(S, HW, is_aligned16(x) && is_aligned16(y), kFwdResidentMax);
+  if (p.resident) {
+    if (p.W == 4)
+      return fwd_resident_dispatch<4>(S, x, bias_nc, gamma, beta, y, mean, rstd, N, C, (int)HW, G,
+                                      eps, act, st);
+    return fwd_resident_dispatch<1>(S, x, bias_nc, gamma, beta, y, mean, rstd, N, C, (int)HW, G,
+                                    eps, act, st);
+  }
+  BPK_REQUIRE(workspace != nullptr, "group_norm: split path needs a workspace");
+  float* part = static_cast<float*>(workspace);
+  dim3 grid(p.splits, N * G);
+  if (p.W == 4) {
+    hipLaunchKernelGGL((gn_fwd_partial<256, 16, 4>), grid, dim3(256), 0, st, x, bias_nc, part, C,
+                       (int)HW, G, p.splits);
+    BPK_LAUNCH_CHECK("group_norm_fwd_partial");
+    hipLaunchKernelGGL((gn_fwd_apply<4>), grid, dim3(256), 0, st, x, bias_nc, gamma, beta, part, y,
+                       mean, rstd, C, (int)HW, G, p.splits, p.chunk, eps, act);
+  } else {
+    hipLaunchKernelGGL((gn_fwd_partial<256, 16, 1>), grid, dim3(256), 0, st, x, bias_nc, part, C,
+                       (int)HW, G, p.splits);
+    BPK_LAUNCH_CHECK("group_norm_fwd_partial");
+    hipLaunchKernelGGL((gn_fwd_apply<1>), grid, dim3(256), 0, st, x, bias_nc, gamma, beta, part, y,
+                       mean, rstd, C, (int)HW, G, p.splits, p.chunk, eps, act);
+  }
+  BPK_LAUNCH_CHECK("group_norm_fwd_apply");
+  return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
+                                      const float* gamma, const float* beta, const float* mean,
+                                      const float* rstd, float* dx, float* dgamma_nc,
+                                      float* dbeta_nc, void* workspace, int N, int C, int64_t HW,
+                                      int G, int act, void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && G > 0, "group_norm_bwd: bad shape");
+  BPK_REQUIRE(C % G == 0, "group_norm_bwd: C (%d) not divisible by G (%d)", C, G);
+  BPK_REQUIRE(act == 0 || act == 1, "group_norm_bwd: act must be 0 or 1");
+  BPK_REQUIRE(mean && rstd, "group_norm_bwd: mean/rstd required");
+  if (N == 0) return BPK_OK;
+  const int64_t S = (int64_t)(C / G) * HW;
+  BPK_REQUIRE(S < (1ll << 31), "group_norm_bwd: slab too large");
+  hipStream_t st = bpk::as_stream(stream);
+  const bool al = is_aligned16(x) && is_aligned16(dy) && is_aligned16(dx);
+  const Plan p = make_plan(S, HW, al, kBwdResidentMax);
+  if (p.resident) {
+    if (p.W == 4)
+      return bwd_resident_dispatch<4>(S, dy, x, bias_nc, gamma, beta, mean, rstd, dx, dgamma_nc,
+                                      dbeta_nc, N, C, (int)HW, G, act, st);
+    return bwd_resident_dispatch<1>(S, dy, x, bias_nc, gamma, beta, mean, rstd, dx, dgamma_nc,
+                                    dbeta_nc, N, C, (int)HW, G, act, st);
+  }
+  BPK_REQUIRE(workspace != nullptr, "group_norm_bwd: split path needs a workspace");
+  float* part = static_cast<float*>(workspace);
+  if (dgamma_nc) (void)hipMemsetAsync(dgamma_nc, 0, sizeof(float) * (size_t)N * C, st);
+  if (dbeta_nc) (void)hipMemsetAsync(dbeta_nc, 0, sizeof(float) * (size_t)N * C, st);
+  dim3 grid(p.splits, N * G);
+  if (p.W == 4) {
+    hipLaunchKernelGGL(gn_bwd_partial<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
+                       mean, rstd, part, dgamma_nc, dbeta_nc, C, (int)HW, G, p.splits, p.chunk,
+                       act);
+    BPK_LAUNCH_CHECK("group_norm_bwd_partial");
+    hipLaunchKernelGGL(gn_bwd_apply<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta, mean,
+                       rstd, part, dx, C, (int)HW, G, p.splits, p.chunk, act);
+  } else {
+    hipLaunchKernelGGL(gn_bwd_partial<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
+                       mean, rstd, part, dgamma_nc, dbeta_nc, C, (int)HW, G, p.splits, p.chunk,
+                       act);
+    BPK_LAUNCH_CHECK("group_norm_bwd_partial");
+    hipLaunchKernelGGL(gn_bwd_apply<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta, mean,
+                       rstd, part, dx, C, (int)HW, G, p.splits, p.chunk, act);
+  }
+  BPK_LAUNCH_CHECK("group_norm_bwd_apply");
+  return BPK_OK;
+}

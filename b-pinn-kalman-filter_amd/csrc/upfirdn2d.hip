@@ -1,0 +1,214 @@
+// upfirdn2d for gfx950: zero-insert upsample -> pad/crop -> FIR (true convolution)
+// -> decimate, on [major, H, W, minor] planes.
+//
+// Semantics follow the reference's CPU oracle `upfirdn2d_native`
+// (op/upfirdn2d.py:159-200) and its CUDA op (op/upfirdn2d_kernel.cu:50-207):
+//   out[p, oy, ox, m] = sum_{i<kh, j<kw} U[oy*dy + i - py0, ox*dx + j - px0, m]
+//                                         * k[kh-1-i, kw-1-j]
+//   U[a, b] = x[a/uy, b/ux] when a % uy == 0, b % ux == 0 and in range, else 0.
+//
+// Design (MI355X-first, HBM-bound op):
+//  * minor == 1 (NCHW planes, every NCSN++ call site) goes to an LDS-tiled
+//    kernel: a workgroup owns a TH x TW output tile of one plane, stages the
+//    input window (with the zero halo) into LDS with coalesced row loads, and
+//    each of the 256 threads produces 4 outputs from LDS.  Tile width adapts to
+//    the plane width (16/32/64) so 16x16 and 32x32 planes do not idle lanes.
+//    The taps are read once into registers (flipped, zero-extended to KxK).
+//  * anything else (minor > 1, factors > 2, kernels > 4x4) uses a grid-stride
+//    direct kernel; L1/L2 absorb the tap overlap.
+#include "bpk_common.h"
+
+namespace {
+
+template <typename T, int UP, int DOWN, int K, int TH, int TW>
+__global__ __launch_bounds__(256) void upfirdn2d_tiled(const T* __restrict__ x,
+                                                        const T* __restrict__ kern,
+                                                        T* __restrict__ out, int in_h, int in_w,
+                                                        int kh, int kw, int px0, int py0,
+                                                        int out_h, int out_w, int tiles_x,
+                                                        int tiles_y) {
+  // input window that covers the output tile (upper bound incl. one slack row/col)
+  constexpr int TIH = ((TH - 1) * DOWN + K - 1) / UP + 2;
+  constexpr int TIW = ((TW - 1) * DOWN + K - 1) / UP + 2;
+  __shared__ T sx[TIH * TIW];
+
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  const int tx_i = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty_i = bid % tiles_y;
+  const int plane = bid / tiles_y;
+
+  const int oy0 = ty_i * TH;
+  const int ox0 = tx_i * TW;
+  // U-space origin of the window and its input-space origin
+  const int ay0 = oy0 * DOWN - py0;
+  const int ax0 = ox0 * DOWN - px0;
+  const int iy0 = bpk::floordiv(ay0, UP);
+  const int ix0 = bpk::floordiv(ax0, UP);
+
+  const T* xp = x + (int64_t)plane * in_h * in_w;
+  for (int e = tid; e < TIH * TIW; e += 256) {
+    const int r = e / TIW;
+    const int c = e - r * TIW;
+    const int iy = iy0 + r;
+    const int ix = ix0 + c;
+    T v = T(0);
+    if (iy >= 0 && iy < in_h && ix >= 0 && ix < in_w) v = xp[(int64_t)iy * in_w + ix];
+    sx[e] = v;
+  }
+
+  // flipped taps, zero-extended to K x K
+  T w[K][K];
+#pragma unroll
+  for (int i = 0; i < K; ++i)
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      w[i][j] = (i < kh && j < kw) ? kern[(kh - 1 - i) * kw + (kw - 1 - j)] : T(0);
+
+  __syncthreads();
+
+  constexpr int ROWS_PER_PASS = 256 / TW;
+  const int tx = tid % TW;
+  const int ox = ox0 + tx;
+#pragma unroll
+  for (int pass = 0; pass < TH / ROWS_PER_PASS; ++pass) {
+    const int ty = pass * ROWS_PER_PASS + tid / TW;
+    const int oy = oy0 + ty;
+    T acc = T(0);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int a = oy * DOWN + i - py0;  // U-space row
+      const int r = bpk::floordiv(a, UP) - iy0;
+      const bool row_ok = (UP == 1) || (bpk::floormod(a, UP) == 0);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int b = ox * DOWN + j - px0;
+        const int c = bpk::floordiv(b, UP) - ix0;
+        const bool ok = row_ok && ((UP == 1) || (bpk::floormod(b, UP) == 0));
+        acc += sx[r * TIW + c] * (ok ? w[i][j] : T(0));
+      }
+    }
+    if (oy < out_h && ox < out_w)
+      out[((int64_t)plane * out_h + oy) * out_w + ox] = acc;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void upfirdn2d_direct(
+    const T* __restrict__ x, const T* __restrict__ kern, T* __restrict__ out, int in_h, int in_w,
+    int minor, int kh, int kw, int ux, int uy, int dx, int dy, int px0, int py0, int out_h,
+    int out_w, int64_t total) {
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = idx;
+    const int m = (int)(t % minor);
+    t /= minor;
+    const int ox = (int)(t % out_w);
+    t /= out_w;
+    const int oy = (int)(t % out_h);
+    const int64_t p = t / out_h;
+    const T* xp = x + p * in_h * in_w * minor + m;
+    T acc = T(0);
+    for (int i = 0; i < kh; ++i) {
+      const int a = oy * dy + i - py0;
+      if (a < 0 || (a % uy) != 0) continue;
+      const int iy = a / uy;
+      if (iy >= in_h) continue;
+      for (int j = 0; j < kw; ++j) {
+        const int b = ox * dx + j - px0;
+        if (b < 0 || (b % ux) != 0) continue;
+        const int ix = b / ux;
+        if (ix >= in_w) continue;
+        acc += xp[((int64_t)iy * in_w + ix) * minor] * kern[(kh - 1 - i) * kw + (kw - 1 - j)];
+      }
+    }
+    out[idx] = acc;
+  }
+}
+
+template <typename T, int UP, int DOWN, int K, int TW>
+int launch_tiled(const T* x, const T* k, T* out, int major, int in_h, int in_w, int kh, int kw,
+                 int px0, int py0, int out_h, int out_w, hipStream_t st) {
+  constexpr int TH = 1024 / TW;  // 4 outputs per thread
+  const int tiles_x = (int)bpk::ceil_div(out_w, TW);
+  const int tiles_y = (int)bpk::ceil_div(out_h, TH);
+  const int64_t blocks = (int64_t)major * tiles_x * tiles_y;
+  if (blocks <= 0) return BPK_OK;
+  BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large (%lld blocks)",
+              (long long)blocks);
+  hipLaunchKernelGGL((upfirdn2d_tiled<T, UP, DOWN, K, TH, TW>), dim3((unsigned)blocks), dim3(256),
+                     0, st, x, k, out, in_h, in_w, kh, kw, px0, py0, out_h, out_w, tiles_x,
+                     tiles_y);
+  BPK_LAUNCH_CHECK("upfirdn2d_tiled");
+  return BPK_OK;
+}
+
+template <typename T, int UP, int DOWN>
+int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w, int kh, int kw,
+                   int px0, int py0, int out_h, int out_w, hipStream_t st) {
+  if (out_w <= 16)
+    return launch_tiled<T, UP, DOWN, 4, 16>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h,
+                                            out_w, st);
+  if (out_w <= 32)
+    return launch_tiled<T, UP, DOWN, 4, 32>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h,
+                                            out_w, st);
+  return launch_tiled<T, UP, DOWN, 4, 64>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h,
+                                          out_w, st);
+}
+
+template <typename T>
+int upfirdn2d_impl(const T* x, const T* k, T* out, int major, int in_h, int in_w, int minor,
+                   int kh, int kw, int ux, int uy, int dx, int dy, int px0, int px1, int py0,
+                   int py1, int out_h, int out_w, void* stream) {
+  BPK_REQUIRE(major >= 0 && in_h > 0 && in_w > 0 && minor > 0, "upfirdn2d: bad input shape");
+  BPK_REQUIRE(kh > 0 && kw > 0, "upfirdn2d: empty kernel");
+  BPK_REQUIRE(ux > 0 && uy > 0 && dx > 0 && dy > 0, "upfirdn2d: factors must be positive");
+  const int exp_h = (in_h * uy + py0 + py1 - kh) / dy + 1;
+  const int exp_w = (in_w * ux + px0 + px1 - kw) / dx + 1;
+  BPK_REQUIRE(out_h == exp_h && out_w == exp_w,
+              "upfirdn2d: out shape (%d,%d) != expected (%d,%d)", out_h, out_w, exp_h, exp_w);
+  BPK_REQUIRE(out_h > 0 && out_w > 0, "upfirdn2d: empty output");
+  if (major == 0) return BPK_OK;
+  hipStream_t st = bpk::as_stream(stream);
+  const bool tiled = minor == 1 && ux == uy && dx == dy && kh <= 4 && kw <= 4 &&
+                     ((ux == 1 && dx == 1) || (ux == 2 && dx == 1) || (ux == 1 && dx == 2));
+  if (tiled) {
+    if (ux == 2)
+      return launch_tiled_w<T, 2, 1>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h, out_w,
+                                     st);
+    if (dx == 2)
+      return launch_tiled_w<T, 1, 2>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h, out_w,
+                                     st);
+    return launch_tiled_w<T, 1, 1>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h, out_w,
+                                   st);
+  }
+  const int64_t total = (int64_t)major * out_h * out_w * minor;
+  const int64_t blocks = std::min<int64_t>(bpk::ceil_div(total, 256), 256 * 32);
+  hipLaunchKernelGGL(upfirdn2d_direct<T>, dim3((unsigned)blocks), dim3(256), 0, st, x, k, out,
+                     in_h, in_w, minor, kh, kw, ux, uy, dx, dy, px0, py0, out_h, out_w, total);
+  BPK_LAUNCH_CHECK("upfirdn2d_direct");
+  return BPK_OK;
+}
+
+}  // namespace
+
+extern "C" int bpk_upfirdn2d_f32(const float* x, const float* kernel, float* out, int major,
+                                 int in_h, int in_w, int minor, int kernel_h, int kernel_w,
+                                 int up_x, int up_y, int down_x, int down_y, int pad_x0,
+                                 int pad_x1, int pad_y0, int pad_y1, int out_h, int out_w,
+                                 void* stream) {
+  return upfirdn2d_impl<float>(x, kernel, out, major, in_h, in_w, minor, kernel_h, kernel_w, up_x,
+                               up_y, down_x, down_y, pad_x0, pad_x1, pad_y0, pad_y1, out_h, out_w,
+                               stream);
+}
+
+extern "C" int bpk_upfirdn2d_f64(const double* x, const double* kernel, double* out, int major,
+                                 int in_h, int in_w, int minor, int kernel_h, int kernel_w,
+                                 int up_x, int up_y, int down_x, int down_y, int pad_x0,
+                                 int pad_x1, int pad_y0, int pad_y1, int out_h, int out_w,
+                                 void* stream) {
+  return upfirdn2d_impl<double>(x, kernel, out, major, in_h, in_w, minor, kernel_h, kernel_w, up_x,
+                                up_y, down_x, down_y, pad_x0, pad_x1, pad_y0, pad_y1, out_h, out_w,
+                                stream);
+}

@@ -1,0 +1,221 @@
+"""Shared score-network layers on the gfx950 path (reference: models/layers.py).
+
+Parameter names and initialisation follow the reference so that state dicts
+(and therefore reference checkpoints) load unchanged; the arithmetic runs on
+the fused HIP ops of `op.norm_act` (GroupNorm + bias + SiLU, residual rescale).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from op.norm_act import ACT_NONE, ACT_SILU, group_norm_act, residual_rescale
+
+
+def get_act(config):
+    """Activation module from config.model.nonlinearity (reference layers.py:29-41)."""
+    name = config.model.nonlinearity.lower()
+    table = {"elu": nn.ELU, "relu": nn.ReLU, "swish": nn.SiLU}
+    if name == "lrelu":
+        return nn.LeakyReLU(negative_slope=0.2)
+    if name not in table:
+        raise NotImplementedError("activation function does not exist!")
+    return table[name]()
+
+
+def gn_act(x, gn: nn.GroupNorm, act=None, bias_nc=None):
+    """act(GroupNorm(x + bias_nc)); SiLU (and no activation) fuse into one HIP launch."""
+    if act is None:
+        return group_norm_act(x, gn, ACT_NONE, bias_nc)
+    if isinstance(act, nn.SiLU):
+        return group_norm_act(x, gn, ACT_SILU, bias_nc)
+    return act(group_norm_act(x, gn, ACT_NONE, bias_nc))
+
+
+def variance_scaling(scale, mode, distribution, in_axis=1, out_axis=0, dtype=torch.float32,
+                     device="cpu"):
+    """JAX-style variance-scaling initializer (reference layers.py:54-80)."""
+
+    def init(shape, dtype=dtype, device=device):
+        receptive = np.prod(shape) / shape[in_axis] / shape[out_axis]
+        fan_in = shape[in_axis] * receptive
+        fan_out = shape[out_axis] * receptive
+        denom = {"fan_in": fan_in, "fan_out": fan_out, "fan_avg": (fan_in + fan_out) / 2}.get(mode)
+        if denom is None:
+            raise ValueError(f"invalid mode for variance scaling initializer: {mode}")
+        variance = scale / denom
+        if distribution == "normal":
+            return torch.randn(*shape, dtype=dtype, device=device) * np.sqrt(variance)
+        if distribution == "uniform":
+            return (torch.rand(*shape, dtype=dtype, device=device) * 2. - 1.) * np.sqrt(3 * variance)
+        raise ValueError("invalid distribution for variance scaling initializer")
+
+    return init
+
+
+def default_init(scale=1.):
+    """DDPM initialisation (reference layers.py:83-86)."""
+    return variance_scaling(1e-10 if scale == 0 else scale, "fan_avg", "uniform")
+
+
+def ddpm_conv1x1(in_planes, out_planes, stride=1, bias=True, init_scale=1., padding=0):
+    conv = nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, padding=padding, bias=bias)
+    conv.weight.data = default_init(init_scale)(conv.weight.data.shape)
+    if bias:
+        nn.init.zeros_(conv.bias)
+    return conv
+
+
+def ddpm_conv3x3(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=1):
+    conv = nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=padding,
+                     dilation=dilation, bias=bias)
+    conv.weight.data = default_init(init_scale)(conv.weight.data.shape)
+    if bias:
+        nn.init.zeros_(conv.bias)
+    return conv
+
+
+def conv_nobias(x, conv: nn.Conv2d):
+    """Run a Conv2d module without its bias (the bias is folded into a later fused op)."""
+    return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def get_timestep_embedding(timesteps, embedding_dim, max_positions=10000):
+    """Sinusoidal embedding (reference layers.py:500-514)."""
+    assert timesteps.ndim == 1
+    half = embedding_dim // 2
+    rate = math.log(max_positions) / (half - 1)
+    freqs = torch.exp(torch.arange(half, dtype=torch.float32, device=timesteps.device) * -rate)
+    arg = timesteps.float()[:, None] * freqs[None, :]
+    emb = torch.cat([torch.sin(arg), torch.cos(arg)], dim=1)
+    if embedding_dim % 2 == 1:
+        emb = F.pad(emb, (0, 1), mode="constant")
+    return emb
+
+
+def get_spatial_embedding(x, y, omega, s=1.0):
+    """Spatial embedding of the PINN nets (reference layers.py:517-521)."""
+    e1 = torch.sin(omega * torch.sqrt(x ** 2 + y ** 2))
+    e2 = torch.sin(omega * torch.sqrt((x.max() - x) ** 2 + (y.max() - y) ** 2))
+    return (e1 + e2) / s
+
+
+class NIN(nn.Module):
+    """Per-pixel dense layer: y[b, :, h, w] = x[b, :, h, w] @ W + b (reference layers.py:537-546)."""
+
+    def __init__(self, in_dim, num_units, init_scale=0.1):
+        super().__init__()
+        self.W = nn.Parameter(default_init(scale=init_scale)((in_dim, num_units)), requires_grad=True)
+        self.b = nn.Parameter(torch.zeros(num_units), requires_grad=True)
+
+    def forward(self, x):
+        # 1x1 convolution with weight W^T: one GEMM on MFMA via the BLAS library
+        w = self.W.t()[:, :, None, None]
+        return F.conv2d(x, w, self.b)
+
+
+def _attention(h, nin_q, nin_k, nin_v):
+    """softmax(q^T k / sqrt(C)) over the H*W positions, returns [B, C, H, W]."""
+    B, C, H, W = h.shape
+    q = nin_q(h).reshape(B, C, H * W)
+    k = nin_k(h).reshape(B, C, H * W)
+    v = nin_v(h).reshape(B, C, H * W)
+    w = torch.bmm(q.transpose(1, 2), k) * (int(C) ** (-0.5))  # [B, HW(q), HW(k)]
+    w = torch.softmax(w, dim=-1)
+    out = torch.bmm(v, w.transpose(1, 2))  # [B, C, HW(q)]
+    return out.reshape(B, C, H, W)
+
+
+class AttnBlock(nn.Module):
+    """DDPM channel attention block (reference layers.py:549-573)."""
+
+    def __init__(self, channels, num_groups=32):
+        super().__init__()
+        self.GroupNorm_0 = nn.GroupNorm(num_groups=num_groups, num_channels=channels, eps=1e-6)
+        self.NIN_0 = NIN(channels, channels)
+        self.NIN_1 = NIN(channels, channels)
+        self.NIN_2 = NIN(channels, channels)
+        self.NIN_3 = NIN(channels, channels, init_scale=0.)
+
+    def forward(self, x):
+        h = gn_act(x, self.GroupNorm_0, None)
+        h = self.NIN_3(_attention(h, self.NIN_0, self.NIN_1, self.NIN_2))
+        return residual_rescale(x, h, None, 1.0)
+
+
+class Upsample(nn.Module):
+    """Nearest x2 (+ conv3x3) (reference layers.py:576-590)."""
+
+    def __init__(self, channels, with_conv=False):
+        super().__init__()
+        if with_conv:
+            self.Conv_0 = ddpm_conv3x3(channels, channels)
+        self.with_conv = with_conv
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        h = F.interpolate(x, (H * 2, W * 2), mode="nearest")
+        return self.Conv_0(h) if self.with_conv else h
+
+
+class Downsample(nn.Module):
+    """'SAME'-padded strided conv or 2x2 average pool (reference layers.py:593-608)."""
+
+    def __init__(self, channels, with_conv=False):
+        super().__init__()
+        if with_conv:
+            self.Conv_0 = ddpm_conv3x3(channels, channels, stride=2, padding=0)
+        self.with_conv = with_conv
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        if self.with_conv:
+            x = self.Conv_0(F.pad(x, (0, 1, 0, 1)))
+        else:
+            x = F.avg_pool2d(x, kernel_size=2, stride=2, padding=0)
+        assert x.shape == (B, C, H // 2, W // 2)
+        return x
+
+
+class ResnetBlockDDPM(nn.Module):
+    """DDPM residual block (reference layers.py:611-655), fused GN+SiLU(+temb bias)."""
+
+    def __init__(self, act, in_ch, out_ch=None, temb_dim=None, conv_shortcut=False, dropout=0.1):
+        super().__init__()
+        out_ch = out_ch or in_ch
+        self.GroupNorm_0 = nn.GroupNorm(num_groups=32, num_channels=in_ch, eps=1e-6)
+        self.act = act
+        self.Conv_0 = ddpm_conv3x3(in_ch, out_ch)
+        if temb_dim is not None:
+            self.Dense_0 = nn.Linear(temb_dim, out_ch)
+            self.Dense_0.weight.data = default_init()(self.Dense_0.weight.data.shape)
+            nn.init.zeros_(self.Dense_0.bias)
+        self.GroupNorm_1 = nn.GroupNorm(num_groups=32, num_channels=out_ch, eps=1e-6)
+        self.Dropout_0 = nn.Dropout(dropout)
+        self.Conv_1 = ddpm_conv3x3(out_ch, out_ch, init_scale=0.)
+        if in_ch != out_ch:
+            if conv_shortcut:
+                self.Conv_2 = ddpm_conv3x3(in_ch, out_ch)
+            else:
+                self.NIN_0 = NIN(in_ch, out_ch)
+        self.out_ch = out_ch
+        self.in_ch = in_ch
+        self.conv_shortcut = conv_shortcut
+
+    def forward(self, x, temb=None):
+        assert x.shape[1] == self.in_ch
+        h = gn_act(x, self.GroupNorm_0, self.act)
+        h = conv_nobias(h, self.Conv_0)
+        bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
+        if temb is not None:
+            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        h = self.Dropout_0(h)
+        h = conv_nobias(h, self.Conv_1)
+        if self.in_ch != self.out_ch:
+            x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
+        return residual_rescale(x, h, self.Conv_1.bias, 1.0)

@@ -1,0 +1,226 @@
+"""NCSN++ layers on the gfx950 path (reference: models/layerspp.py).
+
+Module / parameter names are the reference's (GroupNorm_0, Conv_0, Dense_0,
+GroupNorm_1, Conv_1, Conv_2, NIN_*, Conv2d_0, W) so reference state dicts load.
+Per block the arithmetic is re-scheduled for the GPU:
+  GroupNorm_0+SiLU                  -> 1 fused launch
+  FIR up/down of h and x            -> upfirdn2d HIP kernel
+  Conv_0 (no bias)                  -> conv
+  + Conv_0.bias + Dense_0(SiLU(temb)), GroupNorm_1, SiLU -> 1 fused launch
+  Conv_1 (no bias), + Conv_1.bias + skip, / sqrt(2)      -> conv + 1 fused launch
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from op.norm_act import residual_rescale
+
+from . import layers, up_or_down_sampling
+
+conv1x1 = layers.ddpm_conv1x1
+conv3x3 = layers.ddpm_conv3x3
+NIN = layers.NIN
+default_init = layers.default_init
+gn_act = layers.gn_act
+conv_nobias = layers.conv_nobias
+
+
+class GaussianFourierProjection(nn.Module):
+    """Random Fourier features of log-sigma (reference :32-41)."""
+
+    def __init__(self, embedding_size=256, scale=1.0):
+        super().__init__()
+        self.W = nn.Parameter(torch.randn(embedding_size) * scale, requires_grad=False)
+
+    def forward(self, x):
+        proj = x[:, None] * self.W[None, :] * 2 * np.pi
+        return torch.cat([torch.sin(proj), torch.cos(proj)], dim=-1)
+
+
+class Combine(nn.Module):
+    """1x1 conv of x then concat/sum with y (reference :44-59)."""
+
+    def __init__(self, dim1, dim2, method="cat"):
+        super().__init__()
+        self.Conv_0 = conv1x1(dim1, dim2)
+        self.method = method
+
+    def forward(self, x, y):
+        h = self.Conv_0(x)
+        if self.method == "cat":
+            return torch.cat([h, y], dim=1)
+        if self.method == "sum":
+            return h + y
+        raise ValueError(f"Method {self.method} not recognized.")
+
+
+class AttnBlockpp(nn.Module):
+    """Channel self-attention over H*W positions (reference :62-91)."""
+
+    def __init__(self, channels, skip_rescale=False, init_scale=0.):
+        super().__init__()
+        self.GroupNorm_0 = nn.GroupNorm(num_groups=min(channels // 4, 32), num_channels=channels,
+                                        eps=1e-6)
+        self.NIN_0 = NIN(channels, channels)
+        self.NIN_1 = NIN(channels, channels)
+        self.NIN_2 = NIN(channels, channels)
+        self.NIN_3 = NIN(channels, channels, init_scale=init_scale)
+        self.skip_rescale = skip_rescale
+
+    def forward(self, x):
+        h = gn_act(x, self.GroupNorm_0, None)
+        h = self.NIN_3(layers._attention(h, self.NIN_0, self.NIN_1, self.NIN_2))
+        return residual_rescale(x, h, None, np.sqrt(2.) if self.skip_rescale else 1.0)
+
+
+class Upsample(nn.Module):
+    """x2 upsampling: nearest(+conv) or FIR(+fused conv) (reference :94-126)."""
+
+    def __init__(self, in_ch=None, out_ch=None, with_conv=False, fir=False,
+                 fir_kernel=(1, 3, 3, 1)):
+        super().__init__()
+        out_ch = out_ch if out_ch else in_ch
+        if not fir:
+            if with_conv:
+                self.Conv_0 = conv3x3(in_ch, out_ch)
+        elif with_conv:
+            self.Conv2d_0 = up_or_down_sampling.Conv2d(in_ch, out_ch, kernel=3, up=True,
+                                                       resample_kernel=fir_kernel, use_bias=True,
+                                                       kernel_init=default_init())
+        self.fir, self.with_conv = fir, with_conv
+        self.fir_kernel = fir_kernel
+        self.out_ch = out_ch
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        if not self.fir:
+            # the reference passes 'nearest' positionally as scale_factor (layerspp.py:117),
+            # which raises; the intended nearest-neighbour upsample is used here
+            h = F.interpolate(x, (H * 2, W * 2), mode="nearest")
+            return self.Conv_0(h) if self.with_conv else h
+        if not self.with_conv:
+            return up_or_down_sampling.upsample_2d(x, self.fir_kernel, factor=2)
+        return self.Conv2d_0(x)
+
+
+class Downsample(nn.Module):
+    """/2 downsampling: strided conv / avg-pool or FIR(+fused conv) (reference :129-163)."""
+
+    def __init__(self, in_ch=None, out_ch=None, with_conv=False, fir=False,
+                 fir_kernel=(1, 3, 3, 1)):
+        super().__init__()
+        out_ch = out_ch if out_ch else in_ch
+        if not fir:
+            if with_conv:
+                self.Conv_0 = conv3x3(in_ch, out_ch, stride=2, padding=0)
+        elif with_conv:
+            self.Conv2d_0 = up_or_down_sampling.Conv2d(in_ch, out_ch, kernel=3, down=True,
+                                                       resample_kernel=fir_kernel, use_bias=True,
+                                                       kernel_init=default_init())
+        self.fir, self.with_conv = fir, with_conv
+        self.fir_kernel = fir_kernel
+        self.out_ch = out_ch
+
+    def forward(self, x):
+        if not self.fir:
+            if self.with_conv:
+                return self.Conv_0(F.pad(x, (0, 1, 0, 1)))
+            return F.avg_pool2d(x, 2, stride=2)
+        if not self.with_conv:
+            return up_or_down_sampling.downsample_2d(x, self.fir_kernel, factor=2)
+        return self.Conv2d_0(x)
+
+
+class ResnetBlockDDPMpp(nn.Module):
+    """DDPM++ residual block (reference :166-209)."""
+
+    def __init__(self, act, in_ch, out_ch=None, temb_dim=None, conv_shortcut=False,
+                 dropout=0.1, skip_rescale=False, init_scale=0.):
+        super().__init__()
+        out_ch = out_ch if out_ch else in_ch
+        self.GroupNorm_0 = nn.GroupNorm(num_groups=min(in_ch // 4, 32), num_channels=in_ch, eps=1e-6)
+        self.Conv_0 = conv3x3(in_ch, out_ch)
+        if temb_dim is not None:
+            self.Dense_0 = nn.Linear(temb_dim, out_ch)
+            self.Dense_0.weight.data = default_init()(self.Dense_0.weight.data.shape)
+            nn.init.zeros_(self.Dense_0.bias)
+        self.GroupNorm_1 = nn.GroupNorm(num_groups=min(out_ch // 4, 32), num_channels=out_ch,
+                                        eps=1e-6)
+        self.Dropout_0 = nn.Dropout(dropout)
+        self.Conv_1 = conv3x3(out_ch, out_ch, init_scale=init_scale)
+        if in_ch != out_ch:
+            if conv_shortcut:
+                self.Conv_2 = conv3x3(in_ch, out_ch)
+            else:
+                self.NIN_0 = NIN(in_ch, out_ch)
+        self.skip_rescale = skip_rescale
+        self.act = act
+        self.out_ch = out_ch
+        self.conv_shortcut = conv_shortcut
+
+    def forward(self, x, temb=None):
+        h = gn_act(x, self.GroupNorm_0, self.act)
+        h = conv_nobias(h, self.Conv_0)
+        bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
+        if temb is not None:
+            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        h = self.Dropout_0(h)
+        h = conv_nobias(h, self.Conv_1)
+        if x.shape[1] != self.out_ch:
+            x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
+        return residual_rescale(x, h, self.Conv_1.bias, np.sqrt(2.) if self.skip_rescale else 1.0)
+
+
+class ResnetBlockBigGANpp(nn.Module):
+    """BigGAN residual block with optional FIR up/down (reference :212-274)."""
+
+    def __init__(self, act, in_ch, out_ch=None, temb_dim=None, up=False, down=False,
+                 dropout=0.1, fir=False, fir_kernel=(1, 3, 3, 1), skip_rescale=True,
+                 init_scale=0.):
+        super().__init__()
+        out_ch = out_ch if out_ch else in_ch
+        self.GroupNorm_0 = nn.GroupNorm(num_groups=min(in_ch // 4, 32), num_channels=in_ch, eps=1e-6)
+        self.up, self.down = up, down
+        self.fir, self.fir_kernel = fir, fir_kernel
+        self.Conv_0 = conv3x3(in_ch, out_ch)
+        if temb_dim is not None:
+            self.Dense_0 = nn.Linear(temb_dim, out_ch)
+            self.Dense_0.weight.data = default_init()(self.Dense_0.weight.shape)
+            nn.init.zeros_(self.Dense_0.bias)
+        self.GroupNorm_1 = nn.GroupNorm(num_groups=min(out_ch // 4, 32), num_channels=out_ch,
+                                        eps=1e-6)
+        self.Dropout_0 = nn.Dropout(dropout)
+        self.Conv_1 = conv3x3(out_ch, out_ch, init_scale=init_scale)
+        if in_ch != out_ch or up or down:
+            self.Conv_2 = conv1x1(in_ch, out_ch)
+        self.skip_rescale = skip_rescale
+        self.act = act
+        self.in_ch, self.out_ch = in_ch, out_ch
+
+    def _resample(self, t):
+        if self.up:
+            return (up_or_down_sampling.upsample_2d(t, self.fir_kernel, factor=2) if self.fir
+                    else up_or_down_sampling.naive_upsample_2d(t, factor=2))
+        if self.down:
+            return (up_or_down_sampling.downsample_2d(t, self.fir_kernel, factor=2) if self.fir
+                    else up_or_down_sampling.naive_downsample_2d(t, factor=2))
+        return t
+
+    def forward(self, x, temb=None):
+        h = gn_act(x, self.GroupNorm_0, self.act)
+        h = self._resample(h)
+        x = self._resample(x)
+        h = conv_nobias(h, self.Conv_0)
+        bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
+        if temb is not None:
+            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        h = self.Dropout_0(h)
+        h = conv_nobias(h, self.Conv_1)
+        if self.in_ch != self.out_ch or self.up or self.down:
+            x = self.Conv_2(x)
+        return residual_rescale(x, h, self.Conv_1.bias, np.sqrt(2.) if self.skip_rescale else 1.0)

@@ -1,0 +1,113 @@
+"""Fused GroupNorm(+bias)(+SiLU) and the skip-rescale residual, with autograd.
+
+These are the build's fusions of the NCSN++/DDPM++ block arithmetic
+(models/layerspp.py:242-274 and :200-209):
+  * `group_norm_act(x, gn, act, bias_nc)`  = act(GroupNorm(x + bias_nc[:, :, None, None]))
+    -- one HIP launch (csrc/group_norm.hip) instead of add + group_norm + silu;
+  * `residual_rescale(x, h, bias, div)`    = (x + (h + bias[c])) / div
+    -- folds Conv_1's bias and the skip connection into one pass.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+from ._lib import check, lib, require_hip, stream_ptr
+
+ACT_NONE, ACT_SILU = 0, 1
+
+
+def _ws(N, C, HW, G, device):
+    nb = lib.bpk_group_norm_workspace_bytes(N, C, HW, G)
+    return torch.empty(max(nb // 4, 1), device=device, dtype=torch.float32) if nb > 0 else None
+
+
+class _GroupNormAct(Function):
+    @staticmethod
+    def forward(ctx, x, bias_nc, weight, bias, num_groups, eps, act):
+        require_hip(x, what="group_norm_act")
+        if x.dtype != torch.float32:
+            raise RuntimeError(f"group_norm_act: float32 required, got {x.dtype}")
+        x = x.contiguous()
+        N, C = x.shape[:2]
+        HW = x.numel() // max(N * C, 1)
+        y = torch.empty_like(x)
+        mean = torch.empty((N, num_groups), device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        bnc = bias_nc.contiguous() if bias_nc is not None else None
+        ws = _ws(N, C, HW, num_groups, x.device)
+        check(lib.bpk_group_norm_fwd_f32(
+            x.data_ptr(), bnc.data_ptr() if bnc is not None else None,
+            weight.data_ptr() if weight is not None else None,
+            bias.data_ptr() if bias is not None else None, y.data_ptr(), mean.data_ptr(),
+            rstd.data_ptr(), ws.data_ptr() if ws is not None else None, N, C, HW, num_groups,
+            float(eps), act, stream_ptr(x.device)), "group_norm_act")
+        ctx.save_for_backward(x, bnc, weight, bias, mean, rstd)
+        ctx.num_groups, ctx.act = num_groups, act
+        ctx.has_bnc = bnc is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, bnc, weight, bias, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, C = x.shape[:2]
+        HW = x.numel() // max(N * C, 1)
+        G = ctx.num_groups
+        dx = torch.empty_like(x)
+        need_affine = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dg = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
+        db = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
+        ws = _ws(N, C, HW, G, x.device)
+        check(lib.bpk_group_norm_bwd_f32(
+            dy.data_ptr(), x.data_ptr(), bnc.data_ptr() if bnc is not None else None,
+            weight.data_ptr() if weight is not None else None,
+            bias.data_ptr() if bias is not None else None, mean.data_ptr(), rstd.data_ptr(),
+            dx.data_ptr(), dg.data_ptr() if dg is not None else None,
+            db.data_ptr() if db is not None else None, ws.data_ptr() if ws is not None else None,
+            N, C, HW, G, ctx.act, stream_ptr(x.device)), "group_norm_act_bwd")
+        d_bnc = dx.reshape(N, C, -1).sum(-1) if (ctx.has_bnc and ctx.needs_input_grad[1]) else None
+        dw = dg.sum(0) if dg is not None and ctx.needs_input_grad[2] else None
+        dbeta = db.sum(0) if db is not None and ctx.needs_input_grad[3] else None
+        return dx, d_bnc, dw, dbeta, None, None, None
+
+
+def group_norm_act(x, gn: torch.nn.GroupNorm, act: int = ACT_SILU, bias_nc=None):
+    """act(GroupNorm(x + bias_nc)) using the parameters of an nn.GroupNorm module."""
+    w = gn.weight if gn.affine else None
+    b = gn.bias if gn.affine else None
+    return _GroupNormAct.apply(x, bias_nc, w, b, gn.num_groups, gn.eps, act)
+
+
+def group_norm_act_f(x, num_groups, weight, bias, eps, act=ACT_SILU, bias_nc=None):
+    return _GroupNormAct.apply(x, bias_nc, weight, bias, num_groups, eps, act)
+
+
+class _Residual(Function):
+    @staticmethod
+    def forward(ctx, x, h, bias, div):
+        require_hip(x, h, what="residual_rescale")
+        x, h = x.contiguous(), h.contiguous()
+        if x.shape != h.shape:
+            raise RuntimeError(f"residual_rescale: shape mismatch {x.shape} vs {h.shape}")
+        N, C = x.shape[:2]
+        HW = x.numel() // max(N * C, 1)
+        out = torch.empty_like(x)
+        check(lib.bpk_residual_rescale_f32(x.data_ptr(), h.data_ptr(),
+                                           bias.data_ptr() if bias is not None else None,
+                                           out.data_ptr(), N, C, HW, float(div),
+                                           stream_ptr(x.device)), "residual_rescale")
+        ctx.div = div
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gd = g / ctx.div
+        gb = gd.sum(dim=[0] + list(range(2, g.ndim))) if ctx.has_bias and ctx.needs_input_grad[2] \
+            else None
+        return gd, gd, gb, None
+
+
+def residual_rescale(x, h, bias=None, div=2 ** 0.5):
+    return _Residual.apply(x, h, bias, div)

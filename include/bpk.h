@@ -1,0 +1,258 @@
+/*
+ * bpk.h -- C ABI of the MI355X-native (gfx950) hot-path library `libbpk.so`.
+ *
+ * This is the drop-in boundary for the hot path of XDzzzzzZyq/b-pinn-kalman-filter
+ * (score-SDE training / PC sampling + PINN / Navier-Stokes stencil).  Each entry
+ * point replaces one native op of the reference's `op/` package; the citation on
+ * each block names the reference interface it replaces (paths relative to the
+ * reference repository root).
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers, element counts / sizes, and a `hipStream_t` passed as
+ *     `void* stream` (the caller's current stream; 0 = legacy default stream);
+ *   - all ops are out-of-place and asynchronous on `stream`; nothing allocates;
+ *     where scratch memory is needed the caller passes it (size queried with the
+ *     matching `*_workspace_bytes` function) -- so every call is graph-capturable;
+ *   - return BPK_OK (0) on success; otherwise an error code, and
+ *     bpk_last_error() returns a thread-local human-readable message.  The
+ *     reference raised c10::Error -> Python RuntimeError from TORCH_CHECK
+ *     (op/upfirdn2d.cpp:8,15-16); the Python host maps a nonzero status to
+ *     RuntimeError the same way.
+ *   - tensors are dense row-major (C-contiguous) unless a stride argument says
+ *     otherwise.
+ */
+#ifndef BPK_H_
+#define BPK_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BPK_OK 0
+#define BPK_ERR_ARG 1
+#define BPK_ERR_LAUNCH 2
+#define BPK_ERR_UNSUPPORTED 3
+
+#define BPK_ABI_VERSION 1
+
+/* Thread-local message of the last failed call on this thread. */
+const char* bpk_last_error(void);
+/* Returns BPK_ABI_VERSION. */
+int bpk_abi_version(void);
+
+/* ------------------------------------------------------------------------- *
+ * upfirdn2d: zero-insert upsample by (up_x, up_y), pad (negative = crop),
+ * true 2-D convolution with `kernel` [kernel_h, kernel_w] (i.e. correlation with
+ * the flipped taps), then keep every (down_x, down_y)-th sample.
+ *   x   : [major, in_h, in_w, minor]
+ *   out : [major, out_h, out_w, minor],
+ *         out_h = (in_h*up_y + pad_y0 + pad_y1 - kernel_h) / down_y + 1 (same for w)
+ * Replaces `upfirdn2d_op.upfirdn2d(input, kernel, up_x, up_y, down_x, down_y,
+ * pad_x0, pad_x1, pad_y0, pad_y1)` -- op/upfirdn2d.cpp:12-22 and its CUDA host
+ * op/upfirdn2d_kernel.cu:209-369.  The adjoint (backward) is the same entry
+ * with up<->down, the flipped kernel and the g_pad of op/upfirdn2d.py:111-116.
+ * ------------------------------------------------------------------------- */
+int bpk_upfirdn2d_f32(const float* x, const float* kernel, float* out, int major, int in_h,
+                      int in_w, int minor, int kernel_h, int kernel_w, int up_x, int up_y,
+                      int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
+                      int out_h, int out_w, void* stream);
+int bpk_upfirdn2d_f64(const double* x, const double* kernel, double* out, int major, int in_h,
+                      int in_w, int minor, int kernel_h, int kernel_w, int up_x, int up_y,
+                      int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
+                      int out_h, int out_w, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * fused_bias_act: out = scale * act(x + bias[(i / step_b) % size_b]), act in
+ * {1: linear, 3: leaky-relu(alpha)}; grad = 1 selects the derivative mask from
+ * `refer` (out > 0 ? 1 : alpha); grad = 2 writes zeros.  `bias` / `refer` may be
+ * NULL (numel 0 in the reference).  Replaces `fused.fused_bias_act(input, bias,
+ * refer, act, grad, alpha, scale)` -- op/fused_bias_act.cpp:11-20,
+ * op/fused_bias_act_kernel.cu:18-98.
+ * ------------------------------------------------------------------------- */
+int bpk_fused_bias_act_f32(const float* x, const float* bias, const float* refer, float* out,
+                           int64_t n, int64_t step_b, int64_t size_b, int act, int grad,
+                           float alpha, float scale, void* stream);
+int bpk_fused_bias_act_f64(const double* x, const double* bias, const double* refer, double* out,
+                           int64_t n, int64_t step_b, int64_t size_b, int act, int grad,
+                           double alpha, double scale, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * grid_sample 2-D, bilinear, padding_mode 0 = zeros / 1 = border.
+ *   input [N, C, H_in, W_in], grid [N, H_out, W_out, 2], out [N, C, H_out, W_out]
+ * fwd/bwd replace the ATen calls of op/grid_sample.py:39-60; grad2 replaces
+ * `gridsample_grad2.grad2_2d(...)` -- op/grid_sample.cpp:26-57,
+ * op/grid_sample_kernel.cu:27-210 and 536-599.
+ * bwd: grad_input (may be NULL) must be zero-filled by the caller (atomics);
+ *      grad_grid (may be NULL) is overwritten.
+ * grad2: outputs grad_grad_output (overwritten), grad_input (zero-filled by the
+ *      caller, atomics), grad_grid (overwritten).
+ * ------------------------------------------------------------------------- */
+int bpk_grid_sample2d_fwd_f32(const float* input, const float* grid, float* out, int N, int C,
+                              int H_in, int W_in, int H_out, int W_out, int padding_mode,
+                              int align_corners, void* stream);
+int bpk_grid_sample2d_bwd_f32(const float* grad_out, const float* input, const float* grid,
+                              float* grad_input, float* grad_grid, int N, int C, int H_in,
+                              int W_in, int H_out, int W_out, int padding_mode, int align_corners,
+                              void* stream);
+int bpk_grid_sample2d_grad2_f32(const float* g2_input, const float* g2_grid,
+                                const float* grad_out, const float* input, const float* grid,
+                                float* grad_grad_out, float* grad_input, float* grad_grid, int N,
+                                int C, int H_in, int W_in, int H_out, int W_out, int padding_mode,
+                                int align_corners, void* stream);
+int bpk_grid_sample2d_fwd_f64(const double* input, const double* grid, double* out, int N, int C,
+                              int H_in, int W_in, int H_out, int W_out, int padding_mode,
+                              int align_corners, void* stream);
+int bpk_grid_sample2d_bwd_f64(const double* grad_out, const double* input, const double* grid,
+                              double* grad_input, double* grad_grid, int N, int C, int H_in,
+                              int W_in, int H_out, int W_out, int padding_mode, int align_corners,
+                              void* stream);
+int bpk_grid_sample2d_grad2_f64(const double* g2_input, const double* g2_grid,
+                                const double* grad_out, const double* input, const double* grid,
+                                double* grad_grad_out, double* grad_input, double* grad_grid, int N,
+                                int C, int H_in, int W_in, int H_out, int W_out, int padding_mode,
+                                int align_corners, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * ns_step: explicit 2-D incompressible-flow step on B planes.
+ * Memory convention follows the reference exactly (op/ns_step_kernel.cu:30-37):
+ * a plane is addressed as field[y * nx + x] with nx = tensor.size(2) (the
+ * contiguous axis) and ny = tensor.size(3); scalar fields [B,1,.,.] have plane
+ * stride nx*ny, velocity [B,2,.,.] has its u / v planes at (2b) / (2b+1).
+ * Arithmetic mirrors op/ns_step_kernel.cu:50-234 operation for operation
+ * (including the double-precision promotions of its `2.0`, `3.0`, `0.25`,
+ * `8.0` literals), compiled without FMA contraction, so it is bit-identical to
+ * the C oracle restatement (oracle/ns_step_ref.c).
+ *
+ * Low-level kernels (replace the device kernels of op/ns_step_kernel.cu):
+ *   gradient  : fx, fy <- central differences of f          (:97-112)
+ *   cip_advect: out <- CIP advection of f by vel            (:115-158)
+ *   advect    : out <- f - dt (u fx + v fy)                 (:161-178)
+ *   vel_update: vel_n <- vel - dt grad(p)                   (:181-202)
+ *   pres_update: pres_n <- Jacobi-like pressure update      (:205-234)
+ * `f_plane_stride` is the element distance between consecutive batch planes of f.
+ *
+ * High-level ops (replace ns_step_forward.update_{density,velocity,pressure},
+ * op/ns_step.cpp:45-102).  update_velocity with compat = 1 reproduces the
+ * reference's unbind-stride quirk (op/ns_step.cpp:70: the u / v views of vel_n
+ * are read with batch stride nx*ny instead of 2*nx*ny); compat = 0 reads the
+ * intended planes.  Scratch: bpk_ns_workspace_bytes(op, B, nx, ny) bytes
+ * (op: 0 = density, 1 = velocity, 2 = pressure).
+ * ------------------------------------------------------------------------- */
+int bpk_ns_gradient_f32(const float* f, int64_t f_plane_stride, float* fx, float* fy, int B, int nx,
+                        int ny, float dx, void* stream);
+int bpk_ns_cip_advect_f32(const float* f, int64_t f_plane_stride, const float* fx, const float* fy,
+                          const float* vel, float* out, int B, int nx, int ny, float dt, float dx,
+                          void* stream);
+int bpk_ns_advect_f32(const float* f, int64_t f_plane_stride, const float* fx, const float* fy,
+                      const float* vel, float* out, int B, int nx, int ny, float dt, void* stream);
+int bpk_ns_vel_update_f32(const float* vel, const float* px, const float* py, float* vel_n, int B,
+                          int nx, int ny, float dt, void* stream);
+int bpk_ns_pres_update_f32(const float* pres, const float* vel, float* pres_n, int B, int nx, int ny,
+                           float dt, float dx, void* stream);
+int64_t bpk_ns_workspace_bytes(int op, int B, int nx, int ny);
+int bpk_ns_update_density_f32(const float* dens, const float* vel, float* out, void* workspace,
+                              int B, int nx, int ny, float dt, float dx, void* stream);
+int bpk_ns_update_velocity_f32(const float* vel, const float* pres, float* out, void* workspace,
+                               int B, int nx, int ny, float dt, float dx, int compat, void* stream);
+int bpk_ns_update_pressure_f32(const float* pres, const float* vel, float* out, int B, int nx,
+                               int ny, float dt, float dx, void* stream);
+/* One whole simulator step (pinn_kalman/simulator.py:55-57): vel' =
+ * update_velocity(vel, pres); pres' = update_pressure(pres, vel'); dens' =
+ * update_density(dens, vel'), fused into LDS-tiled kernels.  Results equal the
+ * three calls above bit for bit. */
+int64_t bpk_ns_full_step_workspace_bytes(int B, int nx, int ny);
+int bpk_ns_full_step_f32(const float* dens, const float* vel, const float* pres, float* dens_out,
+                         float* vel_out, float* pres_out, void* workspace, int B, int nx, int ny,
+                         float dt, float dx, int compat, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * GroupNorm (+ optional fused per-(n,c) bias before the norm and SiLU after).
+ * The build's fusion of nn.GroupNorm + act + `h += Dense(temb)[:, :, None, None]`
+ * of models/layerspp.py:242-274 (ResnetBlockBigGANpp) and :200-209.
+ *   x [N, C, HW] (NCHW), bias_nc [N, C] or NULL, gamma/beta [C] or NULL,
+ *   y [N, C, HW]; mean/rstd [N, G] (may be NULL in fwd).  act: 0 none, 1 silu.
+ * bwd: dx [N,C,HW]; dgamma_nc / dbeta_nc [N, C] per-sample partial sums
+ * (reduce over N on the host); may be NULL.
+ * ------------------------------------------------------------------------- */
+int64_t bpk_group_norm_workspace_bytes(int N, int C, int64_t HW, int G);
+int bpk_group_norm_fwd_f32(const float* x, const float* bias_nc, const float* gamma,
+                           const float* beta, float* y, float* mean, float* rstd, void* workspace,
+                           int N, int C, int64_t HW, int G, float eps, int act, void* stream);
+int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
+                           const float* gamma, const float* beta, const float* mean,
+                           const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,
+                           void* workspace, int N, int C, int64_t HW, int G, int act,
+                           void* stream);
+
+/* out[n,c,:] = (x + (h + bias[c])) / div -- the skip_rescale residual of the
+ * BigGAN / DDPM++ blocks with Conv_1's bias folded in (models/layerspp.py:266-274,
+ * :200-209).  bias may be NULL.  x, h, out: [N, C, HW]. */
+int bpk_residual_rescale_f32(const float* x, const float* h, const float* bias, float* out, int N,
+                             int C, int64_t HW, float div, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Score-SDE PC-sampler update kernels (sampling.py:176-282) and the counter-
+ * based noise source.  Per-step scalars live in a device table `coef`
+ * [n_steps, BPK_COEF_STRIDE] built on the host with the reference's float32
+ * algorithm; the step index is read from device memory `step_ptr` so a whole
+ * PC step can be captured once in a hipGraph and replayed.  Noise: when
+ * `noise` is NULL the kernel draws N(0,1) from Philox4x32-10 keyed by `seed`,
+ * counter = (global element index / 4, step, draw); global element index =
+ * (sample_offset + b) * D + e, so draws are identical however the batch is
+ * sharded over ranks.  A non-NULL `noise` [B, D] injects explicit noise (parity
+ * hook).  x_mean may alias nothing; x_out may alias x.
+ * ------------------------------------------------------------------------- */
+#define BPK_COEF_STRIDE 8
+/* coef layout per step (float32):
+ *  [0] score_div   (std used to turn model output into a score; see score_mode)
+ *  [1] drift_coef  (EM: -0.5 beta(t), VE: 0)        / ancestral & RD: beta or sigma^2 - adj^2
+ *  [2] diffusion   (EM: g(t))                        / ancestral: sqrt(1-beta) ...
+ *  [3] dt          (EM: -1/N as float32)
+ *  [4] sqrt_mdt    (EM: float32(sqrt(-dt)))
+ *  [5] alpha       (Langevin: alphas[timestep] or 1)
+ *  [6], [7] spare
+ */
+enum {
+  BPK_PRED_EULER_MARUYAMA = 0,
+  BPK_PRED_REVERSE_DIFFUSION = 1,
+  BPK_PRED_ANCESTRAL_VP = 2,
+  BPK_PRED_ANCESTRAL_VE = 3,
+};
+/* score_mode 0: score = (-m) / coef[0]  (VP / subVP);  1: score = m (VE). */
+int bpk_philox_normal_f32(float* out, int B, int64_t D, int64_t sample_offset, uint64_t seed,
+                          const int* step_ptr, int draw, void* stream);
+int bpk_pc_predictor_f32(int kind, const float* x, const float* model_out, const float* noise,
+                         float* x_out, float* x_mean, int B, int64_t D, int64_t sample_offset,
+                         const float* coef, int coef_bdim, const int* step_ptr, int score_mode,
+                         int drift_mul_x, uint64_t seed, int draw, void* stream);
+/* Langevin corrector, split in three launches so a 2-float all-reduce can sit
+ * between (2) and (3) for batch-sharded runs:
+ *   (1) partial: per (sample, chunk) sums of squares of score and noise
+ *   (2) reduce : red[0] = sum_b ||score_b||, red[1] = sum_b ||noise_b|| (local batch)
+ *   (3) update : step = (snr * (red[1]/B_global) / (red[0]/B_global))^2 * 2 * alpha;
+ *                x_mean = x + step*score; x = x_mean + sqrt(2 step) * noise
+ * mode 0 = Langevin (sampling.py:253-282), 1 = annealed Langevin dynamics
+ * (sampling.py:285-319: step = (snr * std)^2 * 2 * alpha, std = coef[6]).  */
+int64_t bpk_langevin_workspace_bytes(int B, int64_t D);
+int bpk_langevin_partial_f32(const float* model_out, const float* noise, void* workspace, int B,
+                             int64_t D, int64_t sample_offset, const float* coef, int coef_bdim,
+                             const int* step_ptr, int score_mode, uint64_t seed, int draw,
+                             void* stream);
+int bpk_langevin_reduce_f32(void* workspace, float* red, int B, int64_t D, void* stream);
+int bpk_langevin_update_f32(int mode, const float* x, const float* model_out, const float* noise,
+                            const float* red, float* x_out, float* x_mean, int B, int64_t D,
+                            int B_global, int64_t sample_offset, const float* coef,
+                            int coef_bdim, const int* step_ptr, int score_mode, float snr,
+                            uint64_t seed, int draw, void* stream);
+/* step_ptr[0] += 1 (device-side step counter for graph replay) */
+int bpk_step_increment(int* step_ptr, void* stream);
+/* labels[b] = table[*step_ptr] for b < B (time conditioning for the score net) */
+int bpk_fill_step_scalar_f32(float* labels, int B, const float* table, const int* step_ptr,
+                             void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPK_H_ */
