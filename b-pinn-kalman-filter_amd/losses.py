@@ -1,0 +1,156 @@
+"""Training losses and the one-step train/eval function (reference: losses.py:29-224).
+
+Same factories and state contract: `get_optimizer(config, params)`,
+`optimization_manager(config)` (linear warm-up, grad-norm clipping),
+`get_sde_loss_fn` (denoising score matching), `get_smld_loss_fn`,
+`get_ddpm_loss_fn`, and `get_step_fn(sde, train, optimize_fn, reduce_mean,
+continuous, likelihood_weighting)` -> `step_fn(state, batch)` with
+state = {'optimizer', 'model', 'ema', 'step'}.
+
+MI355X notes: the model runs on the fused HIP block ops; Adam uses the
+multi-tensor (foreach) implementation; for batch-sharded data parallelism wrap
+the model in torch DistributedDataParallel (RCCL all-reduce of the gradient
+buckets, overlapped with backward) -- each rank's loss is the mean over its
+shard, so the averaged gradient equals the single-process full-batch gradient.
+The PINN step functions live in pinn_kalman/.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.optim as optim
+
+from models import utils as mutils
+from sde_lib import VESDE, VPSDE
+
+
+def get_optimizer(config, params, lr_mul=1.0, is_bpinn=False):
+    lr = config.optim.bpinn_lr if is_bpinn else config.optim.lr
+    decay = config.optim.bpinn_weight_decay if is_bpinn else config.optim.weight_decay
+    if config.optim.optimizer != "Adam":
+        raise NotImplementedError(f"Optimizer {config.optim.optimizer} not supported yet!")
+    return optim.Adam(params, lr=lr * lr_mul, betas=(config.optim.beta1, 0.999),
+                      eps=config.optim.eps, weight_decay=decay, foreach=True)
+
+
+def optimization_manager(config, is_bpinn=False):
+    base_lr = config.optim.bpinn_lr if is_bpinn else config.optim.lr
+
+    def optimize_fn(optimizer, params, step, lr=base_lr, warmup=config.optim.warmup,
+                    grad_clip=config.optim.grad_clip):
+        if warmup > 0:
+            for g in optimizer.param_groups:
+                g["lr"] = lr * np.minimum(step / warmup, 1.0)
+        if grad_clip >= 0:
+            torch.nn.utils.clip_grad_norm_(params, max_norm=grad_clip, foreach=True)
+        optimizer.step()
+
+    return optimize_fn
+
+
+def _reducer(reduce_mean):
+    if reduce_mean:
+        return torch.mean
+    return lambda *a, **k: 0.5 * torch.sum(*a, **k)
+
+
+def get_sde_loss_fn(sde, train, reduce_mean=True, continuous=True, likelihood_weighting=True,
+                    eps=1e-5):
+    """Denoising score matching over t ~ U(eps, T) (reference losses.py:69-115)."""
+    reduce_op = _reducer(reduce_mean)
+
+    def loss_fn(model, batch):
+        score_fn = mutils.get_score_fn(sde, model, train=train, continuous=continuous)
+        t = torch.rand(batch.shape[0], device=batch.device) * (sde.T - eps) + eps
+        z = torch.randn_like(batch)
+        mean, std = sde.marginal_prob(batch, t)
+        perturbed = mean + std[:, None, None, None] * z
+        score = score_fn(perturbed, t)
+        if not likelihood_weighting:
+            losses = torch.square(score * std[:, None, None, None] + z)
+            losses = reduce_op(losses.reshape(losses.shape[0], -1), dim=-1)
+        else:
+            g2 = sde.sde(torch.zeros_like(batch), t)[1] ** 2
+            losses = torch.square(score + z / std[:, None, None, None])
+            losses = reduce_op(losses.reshape(losses.shape[0], -1), dim=-1) * g2
+        return torch.mean(losses)
+
+    return loss_fn
+
+
+def get_smld_loss_fn(vesde, train, reduce_mean=False):
+    """Legacy NCSN loss (reference losses.py:118-139)."""
+    assert isinstance(vesde, VESDE), "SMLD training only works for VESDEs."
+    sigmas_desc = torch.flip(vesde.discrete_sigmas, dims=(0,))
+    reduce_op = _reducer(reduce_mean)
+
+    def loss_fn(model, batch):
+        model_fn = mutils.get_model_fn(model, train=train)
+        labels = torch.randint(0, vesde.N, (batch.shape[0],), device=batch.device)
+        sig = sigmas_desc.to(batch.device)[labels]
+        noise = torch.randn_like(batch) * sig[:, None, None, None]
+        score = model_fn(noise + batch, labels)
+        target = -noise / (sig ** 2)[:, None, None, None]
+        losses = torch.square(score - target)
+        losses = reduce_op(losses.reshape(losses.shape[0], -1), dim=-1) * sig ** 2
+        return torch.mean(losses)
+
+    return loss_fn
+
+
+def get_ddpm_loss_fn(vpsde, train, reduce_mean=True):
+    """Legacy DDPM loss (reference losses.py:142-162)."""
+    assert isinstance(vpsde, VPSDE), "DDPM training only works for VPSDEs."
+    reduce_op = _reducer(reduce_mean)
+
+    def loss_fn(model, batch):
+        model_fn = mutils.get_model_fn(model, train=train)
+        labels = torch.randint(0, vpsde.N, (batch.shape[0],), device=batch.device)
+        sa = vpsde.sqrt_alphas_cumprod.to(batch.device)
+        s1 = vpsde.sqrt_1m_alphas_cumprod.to(batch.device)
+        noise = torch.randn_like(batch)
+        perturbed = sa[labels, None, None, None] * batch + s1[labels, None, None, None] * noise
+        out = model_fn(perturbed, labels)
+        losses = torch.square(out - noise)
+        losses = reduce_op(losses.reshape(losses.shape[0], -1), dim=-1)
+        return torch.mean(losses)
+
+    return loss_fn
+
+
+def get_step_fn(sde, train, optimize_fn=None, reduce_mean=False, continuous=True,
+                likelihood_weighting=False):
+    """One optimisation / evaluation step (reference losses.py:165-224)."""
+    if continuous:
+        loss_fn = get_sde_loss_fn(sde, train, reduce_mean=reduce_mean, continuous=True,
+                                  likelihood_weighting=likelihood_weighting)
+    else:
+        assert not likelihood_weighting, \
+            "Likelihood weighting is not supported for original SMLD/DDPM training."
+        if isinstance(sde, VESDE):
+            loss_fn = get_smld_loss_fn(sde, train, reduce_mean=reduce_mean)
+        elif isinstance(sde, VPSDE):
+            loss_fn = get_ddpm_loss_fn(sde, train, reduce_mean=reduce_mean)
+        else:
+            raise ValueError(f"Discrete training for {sde.__class__.__name__} is not recommended.")
+
+    def step_fn(state, batch):
+        model = state["model"]
+        if train:
+            optimizer = state["optimizer"]
+            optimizer.zero_grad(set_to_none=True)
+            loss = loss_fn(model, batch)
+            loss.backward()
+            optimize_fn(optimizer, model.parameters(), step=state["step"])
+            state["step"] += 1
+            state["ema"].update(model.parameters())
+        else:
+            with torch.no_grad():
+                ema = state["ema"]
+                ema.store(model.parameters())
+                ema.copy_to(model.parameters())
+                loss = loss_fn(model, batch)
+                ema.restore(model.parameters())
+        return loss
+
+    return step_fn

@@ -513,32 +513,47 @@ class PCEngine:
         return x, x.clone()
 
     @torch.no_grad()
-    def run(self, model, x_init=None, n_iters=None, progress=None):
-        """Run n_iters (default N) PC steps from the prior; returns (x, x_mean)."""
+    def reset(self, model, x_init=None):
+        """Draw / load the prior, (re)capture the step graph if needed, zero the step counter."""
         x, x_mean = self.init_state(x_init)
-        x0 = x.clone()
-        n_iters = self.sde.N if n_iters is None else n_iters
         self.step.zero_()
         if self.use_graph:
             key = (self.seed, id(model))
             if self.graph is None or self._graph_key != key:
                 self._capture(model, x, x_mean)
                 self._graph_key = key
-            x.copy_(x0)
-            x_mean.copy_(x0)
-            self.step.zero_()
+        if self.use_graph:
             self._gx.copy_(x)
-            self._gxm.copy_(x_mean)
-            for k in range(n_iters):
+            self._gxm.copy_(x)
+            self.step.zero_()
+            self._x, self._xm = self._gx, self._gxm
+        else:
+            self._x, self._xm = x, x_mean
+        self._model = model
+        self._done = 0
+
+    @torch.no_grad()
+    def advance(self, n, progress=None):
+        """Run n more PC steps on the current state (no host sync)."""
+        if self._done + n > self.sde.N:
+            raise ValueError(f"only {self.sde.N - self._done} steps left on the time grid")
+        for k in range(n):
+            if self.use_graph:
                 self.graph.replay()
-                if progress is not None:
-                    progress(k)
-            return self._gx.clone(), self._gxm.clone()
-        for k in range(n_iters):
-            self._pc_step(model, x, x_mean, i=k if self.noise_fn is not None else None)
+            else:
+                i = self._done if self.noise_fn is not None else None
+                self._pc_step(self._model, self._x, self._xm, i=i)
+            self._done += 1
             if progress is not None:
-                progress(k)
-        return x, x_mean
+                progress(self._done)
+        return self._x, self._xm
+
+    @torch.no_grad()
+    def run(self, model, x_init=None, n_iters=None, progress=None):
+        """Run n_iters (default N) PC steps from the prior; returns (x, x_mean)."""
+        self.reset(model, x_init)
+        x, xm = self.advance(self.sde.N if n_iters is None else n_iters, progress)
+        return x.clone(), xm.clone()
 
     def _capture(self, model, x, x_mean):
         # static buffers owned by the graph

@@ -1,0 +1,245 @@
+"""Benchmark: PC-sampler score-net evals/s (+ DSM train steps/s), NCSN++ 128x128x1.
+
+BASELINE.json metric "PC-sampler score-net evals/s + train steps/s, NCSN++ 128^2 @1/2/4/8
+MI355X", workload configs[2] (SURVEY.md 8d cfg #3): NCSN++ hyper-parameters of
+configs/vp/cifar10_ncsnpp_continuous.py at 128x128x1, continuous VP-SDE N = 1000,
+Euler-Maruyama predictor + Langevin corrector (snr 0.075, 1 corrector step), batch 64 per
+GPU (weak scaling).  A "step" = one PC step over the batch = 2 score-net evaluations per
+sample (corrector + predictor), fused update kernels, the whole step replayed from a
+hipGraph.  Synthetic data: prior noise + random-init weights (no checkpoints offline).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  value = score-net evals/s of the whole job.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+NCSNPP_GFLOP_PER_EVAL = 333.25     # SURVEY.md 8(d), FlopCounterMode, fwd, 128x128x1
+NCSNPP_GFLOP_PER_TRAIN_SAMPLE = 999.10
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md (f32-input MFMA = f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--train-steps", type=int, default=6)
+    ap.add_argument("--train-warmup", type=int, default=2)
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-samples", type=int, default=4)
+    return ap.parse_args()
+
+
+def build_model(dev, seed=0):
+    import models  # noqa: F401
+    from configs.vp import nc_ncsnpp_128
+    from models import utils as mutils
+    c = nc_ncsnpp_128.get_config()
+    c.device = dev
+    torch.manual_seed(seed)
+    model = mutils.create_model(c, wrap=False)
+    with torch.no_grad():  # random init everywhere (Conv_1 / NIN_3 are zero-init)
+        for p in model.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    return c, model
+
+
+def time_kernel(fn, stream, reps=10):
+    """Average duration (s) of fn() measured with HIP events on `stream`."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            fn()
+        s.record(stream)
+        for _ in range(reps):
+            fn()
+        e.record(stream)
+    e.synchronize()
+    return s.elapsed_time(e) / 1e3 / reps
+
+
+def conv_roofline(dev, batch):
+    """Dominant kernel of the score net: the 3x3 conv 128->128 @128^2 (13 per forward,
+    19% of the FLOPs).  fp32, MFMA-bound."""
+    import torch.nn.functional as F
+    x = torch.randn(batch, 128, 128, 128, device=dev)
+    w = torch.randn(128, 128, 3, 3, device=dev) * 0.02
+    st = torch.cuda.Stream(dev)
+    t = time_kernel(lambda: F.conv2d(x, w, padding=1), st)
+    flops = 2.0 * batch * 128 * 128 * 9 * 128 * 128
+    ach = flops / t / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": "conv3x3 128->128 @128x128 fp32 (MIOpen)", "ms_per_launch": round(t * 1e3, 4),
+            "flop_per_launch": flops}
+
+
+def upfirdn_roofline(dev, batch):
+    """HBM roofline of upfirdn2d on the NCSN++ down2 shape [B,128,128,128] -> [B,128,64,64]."""
+    from op import upfirdn2d
+    k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32, device=dev)
+    x = torch.randn(batch, 128, 128, 128, device=dev)
+    st = torch.cuda.Stream(dev)
+    with torch.cuda.stream(st):
+        t = time_kernel(lambda: upfirdn2d(x, k, down=2, pad=(1, 1)), st)
+    nbytes = 4.0 * (x.numel() + x.numel() // 4)
+    ach = nbytes / t / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "upfirdn2d down2 k4 [B,128,128,128]", "ms_per_launch": round(t * 1e3, 4),
+            "bytes_per_launch": nbytes}
+
+
+def cpu_baseline(n_samples):
+    """The oracle (torch-CPU restatement of the reference path) on the host cores: one warm-up
+    PC step on 1 sample, then 1 PC step (EM + Langevin = 2 evals/sample) on n_samples."""
+    from configs.vp import nc_ncsnpp_128
+    from oracle import nets_ref, score_sde_ref
+    import models  # noqa: F401
+    from models import utils as mutils
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    c = nc_ncsnpp_128.get_config()
+    c.device = "cpu"
+    torch.manual_seed(0)
+    params = nets_ref.init_params(mutils.create_model(c, wrap=False).state_dict())
+    sde = score_sde_ref.SDESpec("vp", N=1000)
+    mf = lambda x, t: nets_ref.forward(params, c, x, t)
+    score_sde_ref.pc_sample(mf, sde, torch.randn(1, 1, 128, 128), "euler_maruyama", "langevin",
+                            0.075, 1, True, n_iters=1)
+    t0 = time.perf_counter()
+    score_sde_ref.pc_sample(mf, sde, torch.randn(n_samples, 1, 128, 128), "euler_maruyama",
+                            "langevin", 0.075, 1, True, n_iters=1)
+    dt = time.perf_counter() - t0
+    return {"value": round(2 * n_samples / dt, 4), "unit": "score-net evals/s", "cores": cores,
+            "kind": "port",
+            "sample": f"oracle/nets_ref + score_sde_ref: 1 PC step (EM+Langevin) on {n_samples} "
+                      f"samples of 128x128x1, {dt:.1f}s, cpu={platform.processor() or 'x86_64'}"}
+
+
+def main():
+    args = parse()
+    import dist
+    import sampling
+    import sde_lib
+    ctx = dist.init_from_env()
+    dev = torch.device("cuda", ctx.local_rank)
+    torch.cuda.set_device(dev)
+    world = ctx.world_size
+    B = args.batch
+    c, model = build_model(dev)
+    model.eval()
+
+    # ---------------------------------------------------------------- PC sampler
+    sde = sde_lib.VPSDE(c.model.beta_min, c.model.beta_max, c.model.num_scales)
+    eng = sampling.PCEngine(sde, (B, 1, 128, 128), sampling.EulerMaruyamaPredictor,
+                            sampling.LangevinCorrector, c.sampling.snr, c.sampling.n_steps_each,
+                            continuous=True, device=dev, seed=1234 + ctx.rank * 0,
+                            use_graph=not args.no_graph, dist_ctx=ctx if world > 1 else None)
+    eng.reset(model)
+    eng.advance(args.warmup)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    eng.advance(args.steps)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
+    x = eng._xm
+    finite = bool(torch.isfinite(x).all().item())
+    evals = 2 * B * world * args.steps  # (1 corrector + 1 predictor) score evals per sample/step
+    evals_per_s = evals / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    # ---------------------------------------------------------------- DSM train step
+    train = None
+    if not args.no_train:
+        import losses
+        from models.ema import ExponentialMovingAverage
+        c.model.dropout = 0.0
+        tmodel = model
+        tmodel.train()
+        if world > 1:
+            tmodel = torch.nn.parallel.DistributedDataParallel(model, device_ids=[ctx.local_rank],
+                                                               bucket_cap_mb=100)
+        opt = losses.get_optimizer(c, tmodel.parameters())
+        ema = ExponentialMovingAverage(tmodel.parameters(), decay=c.model.ema_rate)
+        state = dict(optimizer=opt, model=tmodel, ema=ema, step=0)
+        step_fn = losses.get_step_fn(sde, train=True, optimize_fn=losses.optimization_manager(c),
+                                     reduce_mean=True, continuous=True)
+        batch = torch.rand(B, 1, 128, 128, device=dev)
+        for _ in range(args.train_warmup):
+            step_fn(state, batch)
+        torch.cuda.synchronize(dev)
+        ctx.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.train_steps):
+            loss = step_fn(state, batch)
+        torch.cuda.synchronize(dev)
+        ctx.barrier()
+        torch.cuda.synchronize(dev)
+        tdt = ctx.all_reduce_max(time.perf_counter() - t1, dev)
+        train = {"train_steps_per_s": round(args.train_steps / tdt, 4),
+                 "train_ms_per_step": round(tdt / args.train_steps * 1e3, 2),
+                 "train_global_batch": B * world, "train_loss": round(float(loss.item()), 5),
+                 "train_tflops": round(args.train_steps * B * world * NCSNPP_GFLOP_PER_TRAIN_SAMPLE
+                                       / tdt / 1e3, 2)}
+
+    result = None
+    if ctx.rank == 0:
+        roof = conv_roofline(dev, B)
+        up_roof = upfirdn_roofline(dev, B)
+        model_tflops = evals_per_s * NCSNPP_GFLOP_PER_EVAL / 1e3
+        result = {
+            "metric": "PC-sampler score-net evals/s (NCSN++ 128x128x1, EM + Langevin)",
+            "value": round(evals_per_s, 3), "unit": "score-net evals/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (prior noise, random-init weights)",
+            "config": {"workload": "configs[2]: NCSN++ 128x128x1 PC sampler, VP-SDE N=1000, "
+                                   "euler_maruyama + langevin (snr 0.075), batch 64/GPU",
+                       "model": "ncsnpp (62.69M params)", "global_batch": B * world,
+                       "seq_len": None, "parallelism": f"dp{world} (batch-sharded, RCCL)",
+                       "hip_graph": eng.graph is not None},
+            "score_net_tflops": round(model_tflops, 2),
+            "score_net_mfma_frac": round(model_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+            "samples_finite": finite,
+            "roofline": roof,
+            "roofline_upfirdn2d": up_roof,
+        }
+        if train:
+            result.update(train)
+    if world == 1 and not args.no_cpu_baseline and ctx.rank == 0:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_samples)
+        result["speedup_vs_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+    if ctx.rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

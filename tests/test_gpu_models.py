@@ -1,0 +1,192 @@
+"""GPU parity of the score networks, PC sampler and train step against the reference
+fixtures (tests/golden) and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, net_fixture, product_config
+from oracle import nets_ref, score_sde_ref
+
+pytestmark = pytest.mark.gpu
+
+# fp32 tolerance for whole networks: MIOpen / hipBLASLt accumulate in a different order
+# than the CPU reference (same dtype, different summation order)
+NET_RTOL = 1e-4
+
+
+def _model(name, hip):
+    import models  # noqa: F401
+    from models import utils as mutils
+    cfg, sd, x, labels, y = net_fixture(name)
+    model = mutils.create_model(product_config(cfg, hip), wrap=False)
+    model.load_state_dict({k: torch.tensor(v) for k, v in sd.items()}, strict=True)
+    model.eval()
+    return cfg, model, x, labels, y
+
+
+def _close(a, b, rtol):
+    scale = max(1.0, float(np.abs(b).max()))
+    err = float(np.abs(a - b).max())
+    assert err <= rtol * scale, f"max err {err:.3e} > {rtol:.1e} * {scale:.3e}"
+
+
+@pytest.mark.parametrize("name", ["ncsnpp_a", "ncsnpp_b", "ncsnpp_c", "ddpm_a"])
+def test_networks_match_reference_fixture(hip, name):
+    cfg, model, x, labels, y = _model(name, hip)
+    with torch.no_grad():
+        out = model(torch.tensor(x, device=hip), torch.tensor(labels, device=hip))
+    _close(out.cpu().numpy(), y, NET_RTOL)
+
+
+def test_ncsnpp_128_full_size_matches_cpu_oracle(hip):
+    """The benchmark network (62.7M params, 128x128x1) against the oracle on CPU."""
+    import models  # noqa: F401
+    from configs.vp import nc_ncsnpp_128
+    from models import utils as mutils
+    torch.manual_seed(0)
+    c = nc_ncsnpp_128.get_config()
+    c.device = hip
+    model = mutils.create_model(c, wrap=False).eval()
+    with torch.no_grad():  # non-zero init everywhere (Conv_1 / NIN_3 start at zero)
+        for p in model.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    x = torch.rand(2, 1, 128, 128)
+    t = torch.tensor([0.3, 0.9]) * 999
+    with torch.no_grad():
+        out = model(x.to(hip), t.to(hip)).cpu().numpy()
+    params = nets_ref.init_params(model.state_dict())
+    ref = nets_ref.forward(params, c, x, t).numpy()
+    _close(out, ref, NET_RTOL)
+
+
+@pytest.mark.parametrize("name", ["em_langevin", "rd_ald", "anc_none", "em_none"])
+def test_pc_sampler_matches_reference_with_injected_noise(hip, name):
+    """Fused PC engine, fed the reference's own noise draws, reproduces its samples."""
+    import sampling
+    import sde_lib
+    from op import sde_kernels as K
+    d = load_golden(f"pc_{name}.npz")
+    cfg, model, *_ = _model(str(d["net"]), hip)
+    sde = sde_lib.VPSDE(0.1, 20., int(d["N"]))
+    draws = [torch.tensor(z) for z in d["draws"]]
+    n_steps = int(d["n_steps"])
+    pred, corr = str(d["predictor"]), str(d["corrector"])
+    # map the reference's sequential draw order onto (step, draw-id) of the engine
+    per_step = (n_steps if corr != "none" else 0) + (1 if pred != "none" else 0)
+    order = [1 + j for j in range(n_steps if corr != "none" else 0)] + ([0] if pred != "none" else [])
+    table = {}
+    for i in range(int(d["N"])):
+        for k, draw_id in enumerate(order):
+            table[(i, draw_id)] = draws[i * per_step + k]
+    eng = sampling.PCEngine(sde, tuple(d["prior"].shape), sampling.get_predictor(pred),
+                            sampling.get_corrector(corr), float(d["snr"]), n_steps,
+                            continuous=bool(d["continuous"]), device=hip,
+                            noise_fn=lambda i, draw: table[(i, draw)])
+    out, nfe = eng(model, x_init=torch.tensor(d["prior"]))
+    assert nfe == int(d["nfe"])
+    _close(out.cpu().numpy(), d["out"], 2e-3)
+
+
+def test_pc_engine_graph_replay_equals_eager_and_is_shard_invariant(hip):
+    import sampling
+    import sde_lib
+    cfg, model, *_ = _model("ncsnpp_a", hip)
+    sde = sde_lib.VPSDE(0.1, 20., 25)
+    prior = torch.randn(4, 1, 32, 32)
+    mk = lambda graph, shape: sampling.PCEngine(sde, shape, sampling.EulerMaruyamaPredictor,
+                                                sampling.LangevinCorrector, 0.075, 1,
+                                                continuous=True, device=hip, seed=1234,
+                                                use_graph=graph)
+    eager = mk(False, (4, 1, 32, 32))
+    graph = mk(True, (4, 1, 32, 32))
+    xe, _ = eager.run(model, prior)
+    xg, _ = graph.run(model, prior)
+    assert graph.graph is not None, getattr(graph, "capture_error", "")
+    assert torch.equal(xe, xg)
+
+
+def test_fused_update_kernels_bit_exact_vs_cpu_formula(hip):
+    """Same model output + same noise -> the fused EM / Langevin kernels reproduce the
+    reference's float32 expressions bit for bit (FMA contraction is off in sampler.hip)."""
+    import sampling
+    import sde_lib
+    from op import sde_kernels as K
+    sde = sde_lib.VPSDE(0.1, 20., 1000)
+    torch.manual_seed(0)
+    B = 3
+    x = torch.randn(B, 1, 8, 8)
+    m = torch.randn(B, 1, 8, 8)
+    z = torch.randn(B, 1, 8, 8)
+    t = torch.ones(B) * 0.4567
+    rows = sampling.coef_rows(sde, t, True, K.PRED_EM)
+    # reference expression order (sampling.py:181-187, sde_lib.py:103-110, models/utils.py:159)
+    std = sde.marginal_coef(t)[1]
+    score = -m / std[:, None, None, None]
+    dc, g = sde.coefficient(t)
+    drift = dc[:, None, None, None] * x - g[:, None, None, None] ** 2 * score * 1.
+    x_mean = x + drift * (-1. / sde.N)
+    x_new = x_mean + g[:, None, None, None] * np.sqrt(1. / sde.N) * z
+    xo, xm = torch.empty_like(x).to(hip), torch.empty_like(x).to(hip)
+    K.predictor(K.PRED_EM, x.to(hip), m.to(hip), rows[None].to(hip),
+                torch.zeros(1, dtype=torch.int32, device=hip), x_out=xo, x_mean=xm,
+                noise=z.to(hip))
+    assert torch.equal(xm.cpu(), x_mean) and torch.equal(xo.cpu(), x_new)
+
+
+def test_philox_noise_is_standard_normal_and_shard_invariant(hip):
+    from op import sde_kernels as K
+    step = torch.tensor([7], dtype=torch.int32, device=hip)
+    full = K.philox_normal((8, 4096), 99, step, 1, device=hip)
+    half = K.philox_normal((4, 4096), 99, step, 1, sample_offset=4, device=hip)
+    assert torch.equal(full[4:], half)
+    v = full.double()
+    assert abs(v.mean().item()) < 0.02 and abs(v.std().item() - 1) < 0.02
+
+
+@pytest.mark.parametrize("name", ["dsm_ncsnpp", "dsm_fourier", "ddpm_discrete"])
+def test_train_step_matches_reference(hip, name, monkeypatch):
+    """One optimisation step (loss, grads, Adam update, EMA) with the reference's random draws."""
+    import losses
+    import sde_lib
+    from models.ema import ExponentialMovingAverage
+    d = load_golden(f"train_{name}.npz")
+    cfg, model, *_ = _model(str(d["net"]), hip)
+    c = product_config(net_fixture(str(d["net"]))[0], hip)
+    model.train()
+    rng = [(k.split("_", 1)[1], torch.tensor(d[k])) for k in sorted(
+        (k for k in d.files if k.startswith("rng")), key=lambda s: int(s[3:].split("_")[0]))]
+    it = iter(rng)
+
+    def replay(kind):
+        def f(*a, **kw):
+            k, v = next(it)
+            assert k == kind, (k, kind)
+            return v.to(hip)
+        return f
+
+    monkeypatch.setattr(torch, "rand", replay("rand"))
+    monkeypatch.setattr(torch, "randn_like", replay("randn_like"))
+    monkeypatch.setattr(torch, "randint", replay("randint"))
+    sde = sde_lib.VPSDE(c.model.beta_min, c.model.beta_max, c.model.num_scales)
+    opt = losses.get_optimizer(c, model.parameters())
+    ema = ExponentialMovingAverage(model.parameters(), decay=c.model.ema_rate)
+    state = dict(optimizer=opt, model=model, ema=ema, step=int(d["step0"]))
+    grads = {}
+    real_step = opt.step
+
+    def capture(*a, **kw):
+        for k, p in model.named_parameters():
+            if p.grad is not None:
+                grads[k] = p.grad.detach().cpu().numpy()
+        return real_step(*a, **kw)
+
+    opt.step = capture
+    step_fn = losses.get_step_fn(sde, train=True, optimize_fn=losses.optimization_manager(c),
+                                 reduce_mean=c.training.reduce_mean,
+                                 continuous=bool(d["continuous"]))
+    loss = step_fn(state, torch.tensor(d["batch"], device=hip))
+    assert abs(loss.item() - float(d["loss"])) <= 1e-4 * max(1.0, abs(float(d["loss"])))
+    for k in grads:
+        _close(grads[k], d["g:" + k], 2e-3)
+    for k, p in model.named_parameters():
+        _close(p.detach().cpu().numpy(), d["p1:" + k], 1e-4)

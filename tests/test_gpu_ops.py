@@ -1,0 +1,210 @@
+"""GPU parity of the native ops (HIP kernels via the C ABI) against the oracle / fixtures."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import load_golden
+from oracle import fused_act_ref, grid_sample_ref, ns_step_ref
+from oracle.upfirdn2d_ref import upfirdn2d_np
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ upfirdn2d
+def _golden_cases():
+    d = load_golden("upfirdn2d.npz")
+    out = []
+    for c in range(int(d["n_cases"])):
+        p = d[f"c{c}_params"]
+        out.append((d[f"c{c}_x"], d[f"c{c}_k"], (int(p[0]), int(p[1])), (int(p[2]), int(p[3])),
+                    tuple(int(v) for v in p[4:]), d[f"c{c}_y"], d[f"c{c}_g"], d[f"c{c}_gx"]))
+    return out
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_upfirdn2d_matches_reference_fixture_fwd_and_bwd(hip, case):
+    from op.upfirdn2d import upfirdn2d_xy
+    x, k, up, down, pad, y, g, gx = _golden_cases()[case]
+    xt = torch.tensor(x, device=hip, requires_grad=True)
+    out = upfirdn2d_xy(xt, torch.tensor(k, device=hip), up, down, pad)
+    tol = 2e-6 * max(1.0, float(np.abs(y).max()))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), y, rtol=0, atol=tol)
+    (gin,) = torch.autograd.grad(out, xt, torch.tensor(g, device=hip))
+    np.testing.assert_allclose(gin.cpu().numpy(), gx, rtol=0,
+                               atol=2e-6 * max(1.0, float(np.abs(gx).max())))
+
+
+@pytest.mark.parametrize("shape,up,down,pad,gain", [
+    ((4, 64, 64, 64), 1, 2, (1, 1), 1), ((4, 64, 32, 32), 2, 1, (2, 1), 4),
+    ((4, 32, 64, 64), 1, 1, (2, 2), 1), ((2, 16, 16, 16), 2, 1, (2, 1), 4),
+    ((2, 16, 32, 32), 1, 2, (1, 1), 1), ((3, 5, 37, 23), 1, 2, (1, 1), 1)])
+def test_upfirdn2d_ncsnpp_modes_vs_oracle(hip, shape, up, down, pad, gain):
+    from op import upfirdn2d
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(shape).astype(np.float32)
+    k = np.outer([1, 3, 3, 1], [1, 3, 3, 1]).astype(np.float32) / 64 * gain
+    y = upfirdn2d(torch.tensor(x, device=hip), torch.tensor(k, device=hip), up=up, down=down,
+                  pad=pad).cpu().numpy()
+    ref = upfirdn2d_np(x.astype(np.float64), k, (up, up), (down, down),
+                       (pad[0], pad[1], pad[0], pad[1]))
+    np.testing.assert_allclose(y, ref, rtol=0, atol=2e-6)
+
+
+def test_upfirdn2d_second_order_gradcheck_f64(hip):
+    from op import upfirdn2d
+    k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, device=hip)
+    x = torch.randn(1, 2, 6, 6, dtype=torch.float64, device=hip, requires_grad=True)
+    for up, down, pad in [(1, 2, (1, 1)), (2, 1, (2, 1))]:
+        f = lambda t: upfirdn2d(t, k * (4 if up == 2 else 1), up=up, down=down, pad=pad)
+        assert torch.autograd.gradcheck(f, (x,))
+        assert torch.autograd.gradgradcheck(f, (x,))
+
+
+def test_upfirdn2d_large_plane_count_and_empty_batch(hip):
+    from op import upfirdn2d
+    k = torch.ones(4, 4, device=hip) / 16
+    x = torch.randn(70000, 1, 4, 4, device=hip)  # > 65535 planes: 1-D grid mapping
+    y = upfirdn2d(x, k, down=2, pad=(1, 1))
+    ref = upfirdn2d_np(x[:5].cpu().numpy(), k.cpu().numpy(), (1, 1), (2, 2), (1, 1, 1, 1))
+    np.testing.assert_allclose(y[:5].cpu().numpy(), ref, atol=1e-6)
+    assert upfirdn2d(torch.zeros(0, 3, 8, 8, device=hip), k, down=2, pad=(1, 1)).shape == (0, 3, 4, 4)
+
+
+# ------------------------------------------------------------------ fused_bias_act
+def test_fused_leaky_relu_matches_fixture_and_oracle(hip):
+    from op import fused_leaky_relu
+    d = load_golden("fused_lrelu.npz")
+    y = fused_leaky_relu(torch.tensor(d["x"], device=hip), torch.tensor(d["b"], device=hip))
+    np.testing.assert_allclose(y.cpu().numpy(), d["y"], rtol=1e-6, atol=1e-6)
+    x = np.random.default_rng(3).standard_normal((2, 6, 5, 5)).astype(np.float32)
+    b = np.random.default_rng(4).standard_normal(6).astype(np.float32)
+    y = fused_leaky_relu(torch.tensor(x, device=hip), torch.tensor(b, device=hip), 0.1, 1.7)
+    np.testing.assert_allclose(y.cpu().numpy(), fused_act_ref.fused_bias_act(x, b, None, 3, 0, 0.1, 1.7),
+                               rtol=1e-6, atol=1e-6)
+
+
+def test_fused_leaky_relu_grads_f64(hip):
+    from op import fused_leaky_relu
+    x = torch.randn(2, 3, 4, 4, dtype=torch.float64, device=hip, requires_grad=True)
+    b = torch.randn(3, dtype=torch.float64, device=hip, requires_grad=True)
+    f = lambda a, c: fused_leaky_relu(a, c, 0.2, 2 ** 0.5)
+    assert torch.autograd.gradcheck(f, (x, b))
+    assert torch.autograd.gradgradcheck(f, (x, b))
+
+
+# ------------------------------------------------------------------ GroupNorm + SiLU
+@pytest.mark.parametrize("N,C,H,G", [(2, 64, 16, 16), (3, 128, 32, 32), (2, 256, 64, 32),
+                                      (2, 384, 64, 32), (1, 8, 5, 2), (2, 32, 128, 8)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_group_norm_act_fwd_bwd_vs_torch(hip, N, C, H, G, act):
+    from op.norm_act import group_norm_act_f
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, H) * 2 + 0.5
+    bnc = torch.randn(N, C)
+    w = torch.randn(C)
+    b = torch.randn(C)
+    dy = torch.randn(N, C, H, H)
+    xs = [t.clone().requires_grad_(True) for t in (x, bnc, w, b)]
+    ref = F.group_norm(xs[0] + xs[1][:, :, None, None], G, xs[2], xs[3], eps=1e-6)
+    if act:
+        ref = F.silu(ref)
+    ref.backward(dy)
+    xg = [t.to(hip).requires_grad_(True) for t in (x, bnc, w, b)]
+    out = group_norm_act_f(xg[0], G, xg[2], xg[3], 1e-6, act, xg[1])
+    out.backward(dy.to(hip))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=0, atol=2e-5)
+    for a, r, tol in zip(xg, xs, (5e-5, 2e-3, 2e-3, 2e-3)):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-4,
+                                   atol=tol * max(1.0, r.grad.abs().max().item()))
+
+
+def test_residual_rescale(hip):
+    from op.norm_act import residual_rescale
+    x, h = torch.randn(2, 6, 5, 7), torch.randn(2, 6, 5, 7)
+    b = torch.randn(6)
+    out = residual_rescale(x.to(hip), h.to(hip), b.to(hip), np.sqrt(2.)).cpu()
+    assert torch.equal(out, (x + (h + b[None, :, None, None])) / np.sqrt(2.))
+
+
+# ------------------------------------------------------------------ ns_step
+def _ns_fields(B, nx, ny, seed=0):
+    rng = np.random.default_rng(seed)
+    f = rng.uniform(0.1, 1.0, (B, 1, nx, ny)).astype(np.float32)
+    p = rng.normal(0, 0.01, (B, 1, nx, ny)).astype(np.float32)
+    v = (rng.uniform(0.05, 0.5, (B, 2, nx, ny)) * rng.choice([-1, 1], (B, 2, nx, ny))).astype(np.float32)
+    return f, v, p
+
+
+@pytest.mark.parametrize("B,nx,ny", [(1, 16, 16), (3, 32, 32), (4, 24, 40), (1100, 8, 8),
+                                      (2, 192, 192)])
+@pytest.mark.parametrize("compat", [True, False])
+def test_ns_step_bit_exact_vs_c_oracle(hip, B, nx, ny, compat):
+    from op import ns_step
+    dt, dx = 0.0025, 0.005
+    f, v, p = _ns_fields(B, nx, ny)
+    ft, vt, pt = (torch.tensor(a, device=hip) for a in (f, v, p))
+    v1 = ns_step.update_velocity(vt, pt, dt, dx, compat=compat).cpu().numpy()
+    np.testing.assert_array_equal(v1, ns_step_ref.update_velocity(v, p, dt, dx, compat))
+    p1 = ns_step.update_pressure(pt, vt, dt, dx).cpu().numpy()
+    np.testing.assert_array_equal(p1, ns_step_ref.update_pressure(p, v, dt, dx))
+    f1 = ns_step.update_density(ft, vt, dt, dx).cpu().numpy()
+    np.testing.assert_array_equal(f1, ns_step_ref.update_density(f, v, dt, dx))
+    # fused whole step == the three reference calls, bit for bit
+    d2, v2, p2 = (t.cpu().numpy() for t in ns_step.full_step(ft, vt, pt, dt, dx, compat=compat))
+    rd, rv, rp = ns_step_ref.full_step(f, v, p, dt, dx, compat)
+    np.testing.assert_array_equal(v2, rv)
+    np.testing.assert_array_equal(p2, rp)
+    np.testing.assert_array_equal(d2, rd)
+
+
+def test_ns_step_nan_quirk_on_zero_velocity(hip):
+    from op import ns_step
+    f = torch.rand(1, 1, 8, 8, device=hip)
+    assert torch.isnan(ns_step.update_density(f, torch.zeros(1, 2, 8, 8, device=hip), 0.1, 0.1)).any()
+
+
+# ------------------------------------------------------------------ grid_sample
+@pytest.mark.parametrize("pm", ["zeros", "border"])
+@pytest.mark.parametrize("ac", [True, False])
+def test_grid_sample_fwd_bwd_vs_aten_cpu(hip, pm, ac):
+    from op.grid_sample import grid_sample_2d
+    torch.manual_seed(1)
+    inp = torch.randn(3, 5, 9, 11)
+    grid = torch.rand(3, 7, 6, 2) * 2.4 - 1.2
+    gout = torch.randn(3, 5, 7, 6)
+    ri, rg = inp.clone().requires_grad_(True), grid.clone().requires_grad_(True)
+    ref = F.grid_sample(ri, rg, mode="bilinear", padding_mode=pm, align_corners=ac)
+    ref.backward(gout)
+    gi, gg = inp.to(hip).requires_grad_(True), grid.to(hip).requires_grad_(True)
+    out = grid_sample_2d(gi, gg, pm, ac)
+    out.backward(gout.to(hip))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), atol=1e-5)
+    np.testing.assert_allclose(gi.grad.cpu().numpy(), ri.grad.numpy(), atol=1e-5)
+    np.testing.assert_allclose(gg.grad.cpu().numpy(), rg.grad.numpy(), atol=1e-4)
+
+
+@pytest.mark.parametrize("pm", [0, 1])
+def test_grid_sample_grad2_vs_oracle(hip, pm):
+    from op.grid_sample import grid_sample2d_grad2_raw
+    torch.manual_seed(2)
+    N, C, H, W, Ho, Wo = 2, 4, 7, 8, 5, 6
+    inp = torch.randn(N, C, H, W, dtype=torch.float64)
+    grid = torch.rand(N, Ho, Wo, 2, dtype=torch.float64) * 2.4 - 1.2
+    gout = torch.randn(N, C, Ho, Wo, dtype=torch.float64)
+    g2i, g2g = torch.randn_like(inp), torch.randn_like(grid)
+    ref = grid_sample_ref.grad2(g2i, g2g, gout, inp, grid, pm, True)
+    got = grid_sample2d_grad2_raw(*(t.to(hip) for t in (g2i, g2g, gout, inp, grid)), pm, True)
+    for a, r in zip(got, ref):
+        np.testing.assert_allclose(a.cpu().numpy(), r.numpy(), rtol=1e-10, atol=1e-10)
+
+
+def test_grid_sample_double_backward_gradgradcheck(hip):
+    """Second derivatives through grid_sample, as the PINN residual needs (pinn.py:89-92)."""
+    from op.grid_sample import grid_sample_2d
+    torch.manual_seed(3)
+    inp = torch.randn(1, 2, 5, 5, dtype=torch.float64, device=hip, requires_grad=True)
+    grid = (torch.rand(1, 3, 4, 2, dtype=torch.float64, device=hip) * 1.6 - 0.8).requires_grad_(True)
+    f = lambda a, g: grid_sample_2d(a, g, "border", True)
+    assert torch.autograd.gradcheck(f, (inp, grid))
+    assert torch.autograd.gradgradcheck(f, (inp, grid))

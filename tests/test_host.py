@@ -1,0 +1,128 @@
+"""CPU: host-side logic of the product (no kernel launches)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import load_golden, net_fixture, product_config
+
+
+@pytest.mark.parametrize("name", ["ncsnpp_a", "ncsnpp_b", "ncsnpp_c", "ddpm_a"])
+def test_state_dict_layout_matches_reference(name):
+    """Reference checkpoints load unchanged: same keys and shapes (`all_modules.{i}...`)."""
+    from models import utils as mutils
+    import models  # noqa: F401
+    cfg, sd, *_ = net_fixture(name)
+    model = mutils.create_model(product_config(cfg, "cpu"), wrap=False)
+    ours = model.state_dict()
+    assert set(ours) == set(sd)
+    for k, v in sd.items():
+        assert tuple(ours[k].shape) == v.shape, k
+    model.load_state_dict({k: torch.tensor(v) for k, v in sd.items()}, strict=True)
+    wrapped = mutils.create_model(product_config(cfg, "cpu"))
+    assert all(k.startswith("module.") for k in wrapped.state_dict())
+
+
+def test_benchmark_config_is_the_62_7M_ncsnpp():
+    from configs.vp import nc_ncsnpp_128
+    from models import utils as mutils
+    import models  # noqa: F401
+    c = nc_ncsnpp_128.get_config()
+    c.device = "cpu"
+    n = sum(p.numel() for p in mutils.create_model(c, wrap=False).parameters())
+    assert n == 62_686_337
+
+
+def test_sde_lib_matches_reference_tables_bit_exactly():
+    import sde_lib
+    d = load_golden("sde_tables.npz")
+    for N in (1000, 2000):
+        vp = sde_lib.VPSDE(0.1, 20., N)
+        for key in ("discrete_betas", "alphas", "alphas_cumprod", "sqrt_alphas_cumprod",
+                    "sqrt_1m_alphas_cumprod"):
+            np.testing.assert_array_equal(getattr(vp, key).numpy(), d[f"vp{N}_{key}"])
+        ts = torch.tensor(d[f"vp{N}_timesteps"])
+        dc, g = vp.coefficient(ts)
+        np.testing.assert_array_equal(dc.numpy(), d[f"vp{N}_drift_coef"])
+        np.testing.assert_array_equal(g.numpy(), d[f"vp{N}_diffusion"])
+        m, s = vp.marginal_coef(ts)
+        np.testing.assert_array_equal(s.numpy(), d[f"vp{N}_marginal_std"])
+        np.testing.assert_array_equal(vp.timestep_index(ts).numpy(), d[f"vp{N}_index"])
+    ve = sde_lib.VESDE(0.01, 50., 1000)
+    np.testing.assert_array_equal(ve.discrete_sigmas.numpy(), d["ve1000_discrete_sigmas"])
+    tv = torch.tensor(d["ve_t"])
+    np.testing.assert_array_equal(ve.coefficient(tv)[1].numpy(), d["ve_coef_diffusion"])
+    np.testing.assert_array_equal(ve.marginal_prob(torch.zeros(37, 1, 1, 1), tv)[1].numpy(),
+                                  d["ve_marginal_std"])
+    np.testing.assert_array_equal(ve.discretize(torch.zeros(37, 1, 1, 1), tv)[1].numpy(),
+                                  d["ve_discretize_G"])
+    sv = sde_lib.subVPSDE(0.1, 20., 1000)
+    np.testing.assert_array_equal(sv.coefficient(tv)[1].numpy(), d["subvp_diffusion"])
+    np.testing.assert_array_equal(sv.marginal_coef(tv)[1].numpy(), d["subvp_std"])
+
+
+def test_pc_engine_step_tables_are_the_reference_float32_values():
+    """Per-step scalars precomputed on the host equal the reference's per-step values."""
+    import sampling
+    import sde_lib
+    from op import sde_kernels as K
+    d = load_golden("sde_tables.npz")
+    sde = sde_lib.VPSDE(0.1, 20., 1000)
+    eng = sampling.PCEngine(sde, (2, 1, 8, 8), sampling.EulerMaruyamaPredictor,
+                            sampling.LangevinCorrector, 0.075, 1, continuous=True, device="cpu")
+    coef = eng.coef[:, 0]
+    np.testing.assert_array_equal(coef[:, K.C_DRIFT].numpy(), d["vp1000_drift_coef"])
+    np.testing.assert_array_equal(coef[:, K.C_DIFF].numpy(), d["vp1000_diffusion"])
+    np.testing.assert_array_equal(coef[:, K.C_SDIV].numpy(), d["vp1000_marginal_std"])
+    np.testing.assert_array_equal(coef[:, K.C_ALPHA].numpy(),
+                                  d["vp1000_alphas"][d["vp1000_index"]])
+    np.testing.assert_array_equal(eng.label_table.numpy(), d["vp1000_labels999"])
+    assert coef[0, K.C_DT].item() == np.float32(-1e-3)
+
+
+def test_engine_supports_reference_pairs():
+    import sampling
+    import sde_lib
+    vp = sde_lib.VPSDE()
+    S = sampling
+    assert S.PCEngine.supports(vp, S.EulerMaruyamaPredictor, S.LangevinCorrector, False)
+    assert S.PCEngine.supports(vp, S.AncestralSamplingPredictor, S.NoneCorrector, False)
+    assert not S.PCEngine.supports(vp, S.EulerMaruyamaPredictor, S.LangevinCorrector, True)
+    assert not S.PCEngine.supports(S.sde_lib.subVPSDE(), S.ReverseDiffusionPredictor,
+                                   S.NoneCorrector, False)
+    assert set(S._PREDICTORS) >= {"euler_maruyama", "reverse_diffusion", "ancestral_sampling",
+                                  "none"}
+    assert set(S._CORRECTORS) >= {"langevin", "ald", "none"}
+
+
+def _gloo_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path[:0] = [os.path.join(os.path.dirname(__file__), "..", "b-pinn-kalman-filter_amd")]
+    import dist
+    ctx = dist.init_from_env(backend="gloo")
+    off, n = dist.shard(8, ctx)
+    red = torch.tensor([float(rank + 1), 10.0 * (rank + 1)])
+    ctx.all_reduce_sum_(red)
+    g = ctx.all_gather_cat(torch.full((n, 2), float(rank)))
+    ctx.barrier()
+    q.put((rank, off, n, red.tolist(), g[:, 0].tolist()))
+    torch.distributed.destroy_process_group()
+
+
+def test_dist_context_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0][1:3] == (0, 4) and res[1][1:3] == (4, 4)
+    assert res[0][3] == [3.0, 30.0] == res[1][3]
+    assert res[0][4] == [0.0] * 4 + [1.0] * 4
