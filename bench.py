@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=4)
+    ap.add_argument("--miopen-find", type=int, default=1,
+                    help="1: MIOpen exhaustive find (cudnn.benchmark) for every conv shape")
     return ap.parse_args()
 
 
@@ -143,6 +145,7 @@ def main():
     import sampling
     import sde_lib
     ctx = dist.init_from_env()
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     dev = torch.device("cuda", ctx.local_rank)
     torch.cuda.set_device(dev)
     world = ctx.world_size
