@@ -10,27 +10,36 @@
 // Design (MI355X-first, HBM-bound op):
 //  * minor == 1 (NCHW planes, every NCSN++ call site) goes to an LDS-tiled
 //    kernel: a workgroup owns a TH x TW output tile of one plane, stages the
-//    input window (with the zero halo) into LDS with coalesced row loads, and
-//    each of the 256 threads produces 4 outputs from LDS.  Tile width adapts to
-//    the plane width (16/32/64) so 16x16 and 32x32 planes do not idle lanes.
-//    The taps are read once into registers (flipped, zero-extended to KxK).
+//    input window (with the zero halo) into LDS with 16-byte row loads from an
+//    aligned origin, and each of the 256 threads produces 4-wide output strips
+//    written with 16-byte stores.  Tile width adapts to the plane width
+//    (16/32/64) so 16x16 and 32x32 planes do not idle lanes.  The taps are read
+//    once into registers (flipped, zero-extended to KxK).
 //  * anything else (minor > 1, factors > 2, kernels > 4x4) uses a grid-stride
 //    direct kernel; L1/L2 absorb the tap overlap.
 #include "bpk_common.h"
 
+#include <type_traits>
+
 namespace {
 
-template <typename T, int UP, int DOWN, int K, int TH, int TW>
+// LDS-tiled kernel.  A workgroup produces a TH x TW output tile of one plane: it stages the
+// input window (zero halo included) into LDS -- 16-byte loads from an aligned origin when
+// VEC -- then each thread produces 4-wide output strips (one 16-byte store each when VEC).
+template <typename T, int UP, int DOWN, int K, int TH, int TW, bool VEC_>
 __global__ __launch_bounds__(256) void upfirdn2d_tiled(const T* __restrict__ x,
                                                         const T* __restrict__ kern,
                                                         T* __restrict__ out, int in_h, int in_w,
                                                         int kh, int kw, int px0, int py0,
                                                         int out_h, int out_w, int tiles_x,
                                                         int tiles_y) {
-  // input window that covers the output tile (upper bound incl. one slack row/col)
+  constexpr bool VEC = VEC_ && std::is_same<T, float>::value;
   constexpr int TIH = ((TH - 1) * DOWN + K - 1) / UP + 2;
-  constexpr int TIW = ((TW - 1) * DOWN + K - 1) / UP + 2;
-  __shared__ T sx[TIH * TIW];
+  constexpr int TIW_RAW = ((TW - 1) * DOWN + K - 1) / UP + 2;
+  constexpr int TIW = (TIW_RAW + 3 + 3) / 4 * 4;  // + room for the 0..3 alignment shift
+  constexpr int LD = TIW + 4;                     // row pitch (16-byte multiple, skews banks)
+  constexpr int QW = TIW / 4;
+  __shared__ __attribute__((aligned(16))) T sx[TIH * LD];
 
   const int tid = threadIdx.x;
   int bid = blockIdx.x;
@@ -41,21 +50,38 @@ __global__ __launch_bounds__(256) void upfirdn2d_tiled(const T* __restrict__ x,
 
   const int oy0 = ty_i * TH;
   const int ox0 = tx_i * TW;
-  // U-space origin of the window and its input-space origin
-  const int ay0 = oy0 * DOWN - py0;
-  const int ax0 = ox0 * DOWN - px0;
-  const int iy0 = bpk::floordiv(ay0, UP);
-  const int ix0 = bpk::floordiv(ax0, UP);
+  const int iy0 = bpk::floordiv(oy0 * DOWN - py0, UP);
+  const int ix0 = bpk::floordiv(ox0 * DOWN - px0, UP);
+  const int ixa = VEC ? bpk::floordiv(ix0, 4) * 4 : ix0;  // aligned load origin
+  const int shift = ix0 - ixa;
 
   const T* xp = x + (int64_t)plane * in_h * in_w;
-  for (int e = tid; e < TIH * TIW; e += 256) {
-    const int r = e / TIW;
-    const int c = e - r * TIW;
+  for (int e = tid; e < TIH * QW; e += 256) {
+    const int r = e / QW;
+    const int q = e - r * QW;
     const int iy = iy0 + r;
-    const int ix = ix0 + c;
-    T v = T(0);
-    if (iy >= 0 && iy < in_h && ix >= 0 && ix < in_w) v = xp[(int64_t)iy * in_w + ix];
-    sx[e] = v;
+    const int ix = ixa + 4 * q;
+    T v[4];
+    const bool row_ok = iy >= 0 && iy < in_h;
+    bool loaded = false;
+    if constexpr (VEC) {
+      if (row_ok && ix >= 0 && ix + 3 < in_w) {
+        const float4 f = *reinterpret_cast<const float4*>(xp + (int64_t)iy * in_w + ix);
+        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+        loaded = true;
+      }
+    }
+    if (!loaded) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[j] = (row_ok && ix + j >= 0 && ix + j < in_w) ? xp[(int64_t)iy * in_w + ix + j] : T(0);
+    }
+    if constexpr (VEC) {
+      *reinterpret_cast<float4*>(&sx[r * LD + 4 * q]) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sx[r * LD + 4 * q + j] = v[j];
+    }
   }
 
   // flipped taps, zero-extended to K x K
@@ -68,29 +94,48 @@ __global__ __launch_bounds__(256) void upfirdn2d_tiled(const T* __restrict__ x,
 
   __syncthreads();
 
-  constexpr int ROWS_PER_PASS = 256 / TW;
-  const int tx = tid % TW;
-  const int ox = ox0 + tx;
+  constexpr int SPR = TW / 4;           // strips per output row
+  constexpr int ROWS_PER_PASS = 256 / SPR;
+  const int sx0 = (tid % SPR) * 4;
 #pragma unroll
   for (int pass = 0; pass < TH / ROWS_PER_PASS; ++pass) {
-    const int ty = pass * ROWS_PER_PASS + tid / TW;
+    const int ty = pass * ROWS_PER_PASS + tid / SPR;
     const int oy = oy0 + ty;
-    T acc = T(0);
+    T acc[4] = {T(0), T(0), T(0), T(0)};
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const int a = oy * DOWN + i - py0;  // U-space row
+      const int a = oy * DOWN + i - py0;
       const int r = bpk::floordiv(a, UP) - iy0;
       const bool row_ok = (UP == 1) || (bpk::floormod(a, UP) == 0);
+      const T* srow = sx + r * LD + shift;
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int b = ox * DOWN + j - px0;
-        const int c = bpk::floordiv(b, UP) - ix0;
-        const bool ok = row_ok && ((UP == 1) || (bpk::floormod(b, UP) == 0));
-        acc += sx[r * TIW + c] * (ok ? w[i][j] : T(0));
+      for (int s = 0; s < 4; ++s) {
+        const int ox = ox0 + sx0 + s;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int b = ox * DOWN + j - px0;
+          const int c = bpk::floordiv(b, UP) - ix0;
+          const bool ok = row_ok && ((UP == 1) || (bpk::floormod(b, UP) == 0));
+          acc[s] += srow[c] * (ok ? w[i][j] : T(0));
+        }
       }
     }
-    if (oy < out_h && ox < out_w)
-      out[((int64_t)plane * out_h + oy) * out_w + ox] = acc;
+    const int ox = ox0 + sx0;
+    if (oy < out_h) {
+      T* op = out + ((int64_t)plane * out_h + oy) * out_w + ox;
+      bool stored = false;
+      if constexpr (VEC) {
+        if (ox + 3 < out_w) {
+          *reinterpret_cast<float4*>(op) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+          stored = true;
+        }
+      }
+      if (!stored) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (ox + s < out_w) op[s] = acc[s];
+      }
+    }
   }
 }
 
@@ -127,34 +172,41 @@ __global__ __launch_bounds__(256) void upfirdn2d_direct(
   }
 }
 
-template <typename T, int UP, int DOWN, int K, int TW>
+template <typename T, int UP, int DOWN, int K, int TH, int TW>
 int launch_tiled(const T* x, const T* k, T* out, int major, int in_h, int in_w, int kh, int kw,
                  int px0, int py0, int out_h, int out_w, hipStream_t st) {
-  constexpr int TH = 1024 / TW;  // 4 outputs per thread
   const int tiles_x = (int)bpk::ceil_div(out_w, TW);
   const int tiles_y = (int)bpk::ceil_div(out_h, TH);
   const int64_t blocks = (int64_t)major * tiles_x * tiles_y;
   if (blocks <= 0) return BPK_OK;
   BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large (%lld blocks)",
               (long long)blocks);
-  hipLaunchKernelGGL((upfirdn2d_tiled<T, UP, DOWN, K, TH, TW>), dim3((unsigned)blocks), dim3(256),
-                     0, st, x, k, out, in_h, in_w, kh, kw, px0, py0, out_h, out_w, tiles_x,
-                     tiles_y);
+  const bool vec = std::is_same<T, float>::value && in_w % 4 == 0 && out_w % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL((upfirdn2d_tiled<T, UP, DOWN, K, TH, TW, true>), dim3((unsigned)blocks),
+                       dim3(256), 0, st, x, k, out, in_h, in_w, kh, kw, px0, py0, out_h, out_w,
+                       tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL((upfirdn2d_tiled<T, UP, DOWN, K, TH, TW, false>), dim3((unsigned)blocks),
+                       dim3(256), 0, st, x, k, out, in_h, in_w, kh, kw, px0, py0, out_h, out_w,
+                       tiles_x, tiles_y);
   BPK_LAUNCH_CHECK("upfirdn2d_tiled");
   return BPK_OK;
 }
 
+// tile shapes (TH x TW outputs, 4..8 per thread) by plane width
 template <typename T, int UP, int DOWN>
 int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w, int kh, int kw,
                    int px0, int py0, int out_h, int out_w, hipStream_t st) {
   if (out_w <= 16)
-    return launch_tiled<T, UP, DOWN, 4, 16>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h,
-                                            out_w, st);
+    return launch_tiled<T, UP, DOWN, 4, 64, 16>(x, k, out, major, in_h, in_w, kh, kw, px0, py0,
+                                                out_h, out_w, st);
   if (out_w <= 32)
-    return launch_tiled<T, UP, DOWN, 4, 32>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h,
-                                            out_w, st);
-  return launch_tiled<T, UP, DOWN, 4, 64>(x, k, out, major, in_h, in_w, kh, kw, px0, py0, out_h,
-                                          out_w, st);
+    return launch_tiled<T, UP, DOWN, 4, 32, 32>(x, k, out, major, in_h, in_w, kh, kw, px0, py0,
+                                                out_h, out_w, st);
+  return launch_tiled<T, UP, DOWN, 4, 32, 64>(x, k, out, major, in_h, in_w, kh, kw, px0, py0,
+                                              out_h, out_w, st);
 }
 
 template <typename T>

@@ -474,8 +474,10 @@ class PCEngine:
             return None
         return self.noise_fn(i, draw).to(self.device, torch.float32).contiguous()
 
-    def _pc_step(self, model, x, x_mean, i=None):
-        """One PC iteration on the static buffers x / x_mean (graph-capturable when i is None)."""
+    def _segments(self, model, x, x_mean, i=None):
+        """One PC iteration on the static buffers x / x_mean, as a generator that yields at
+        every cross-rank exchange point (the Langevin norm all-reduce, only when sharded).
+        The code between two yields is a graph-capturable launch sequence."""
         sde_vp_like = not isinstance(self.sde, sde_lib.VESDE)
         mode = K.SCORE_DIV if sde_vp_like else K.SCORE_RAW
         K.fill_from_table(self.labels, self.label_table, self.step)
@@ -489,7 +491,7 @@ class PCEngine:
                                      score_mode=mode, seed=self.seed, draw=1 + j,
                                      sample_offset=self.sample_offset)
                     if self.world > 1:
-                        self.dist.all_reduce_sum_(self.red)
+                        yield "all_reduce"  # red <- sum over ranks
                 K.langevin_update(self.corr_mode, x, m, self.coef, self.step, self.red, x_out=x,
                                   x_mean=x_mean, noise=nz, B_global=self.B_global, score_mode=mode,
                                   snr=self.snr, seed=self.seed, draw=1 + j,
@@ -501,6 +503,10 @@ class PCEngine:
                         noise=nz, score_mode=mode, drift_mul_x=int(sde_vp_like), seed=self.seed,
                         draw=0, sample_offset=self.sample_offset)
         K.step_increment(self.step)
+
+    def _pc_step(self, model, x, x_mean, i=None):
+        for _ in self._segments(model, x, x_mean, i):
+            self.dist.all_reduce_sum_(self.red)
 
     def init_state(self, x_init=None):
         if x_init is None:
@@ -539,7 +545,10 @@ class PCEngine:
             raise ValueError(f"only {self.sde.N - self._done} steps left on the time grid")
         for k in range(n):
             if self.use_graph:
-                self.graph.replay()
+                for gi, g in enumerate(self.graph):
+                    if gi:
+                        self.dist.all_reduce_sum_(self.red)
+                    g.replay()
             else:
                 i = self._done if self.noise_fn is not None else None
                 self._pc_step(self._model, self._x, self._xm, i=i)
@@ -567,11 +576,24 @@ class PCEngine:
                 self._pc_step(model, self._gx, self._gxm)
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.step.zero_()
-        g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
-                self._pc_step(model, self._gx, self._gxm)
-            self.graph = g
+            # one graph per segment between exchange points (a single graph when unsharded);
+            # the segments share one memory pool and the generator keeps the tensors that
+            # cross a segment boundary (the model output) alive
+            graphs, pool = [], None
+            gen = self._segments(model, self._gx, self._gxm)
+            done = False
+            while not done:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    try:
+                        next(gen)
+                    except StopIteration:
+                        done = True
+                pool = g.pool()
+                graphs.append(g)
+            self._gen = gen
+            self.graph = graphs
         except Exception as e:  # capture unsupported by some library call: run eagerly
             self.use_graph = False
             self.graph = None
