@@ -19,6 +19,7 @@
 //    direct kernel; L1/L2 absorb the tap overlap.
 #include "bpk_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -209,6 +210,167 @@ int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w
                                               out_h, out_w, st);
 }
 
+// Register-streaming kernel for the FIR modes NCSN++ uses (and their adjoints):
+// (up, down) in {(1,2), (1,1), (2,1)}, taps <= 4x4, pad0 = P0 on both axes.  One wave owns
+// a strip of 64*NOC output columns x R output rows of one plane; per input row each lane
+// loads LV consecutive floats (8-byte loads when LV = 2) and takes its +-1 neighbours'
+// values with cross-lane shuffles, so every input byte is fetched once per strip and there
+// is no LDS staging and no workgroup barrier.  All tap/row/column bookkeeping is
+// compile-time: input row t of the strip feeds output row r through vertical tap
+// i = t*UP - r*DOWN, and output column oc of a lane reads relative input column
+// q = (oc*DOWN + j - P0) / UP of its own / neighbouring lane.
+template <int UP, int DOWN, int P0, int R>
+__global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict__ x,
+                                                         const float* __restrict__ kern,
+                                                         float* __restrict__ out, int in_h,
+                                                         int in_w, int kh, int kw, int out_h,
+                                                         int out_w, int strips_x, int strips_y,
+                                                         int64_t n_strips) {
+  constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;  // output columns per lane
+  constexpr int LV = NOC * DOWN / UP;                   // input columns loaded per lane
+  constexpr int NIR = ((R - 1) * DOWN + 3) / UP + 1;    // input rows feeding R output rows
+  const int lane = threadIdx.x & 63;
+  const int64_t strip = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (strip >= n_strips) return;  // wave-uniform
+  const int sxi = (int)(strip % strips_x);
+  const int syi = (int)((strip / strips_x) % strips_y);
+  const int64_t plane = strip / ((int64_t)strips_x * strips_y);
+  const int ox0 = sxi * 64 * NOC;
+  const int oyb = syi * R;  // R even -> (oyb*DOWN - P0) divisible by UP when UP = 2, P0 = 2
+  const int ixbase = ox0 * DOWN / UP;
+  const int iy_lo = bpk::floordiv(oyb * DOWN - P0, UP);
+  const int mycol = ixbase + LV * lane;
+
+  float w[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[i][j] = (i < kh && j < kw) ? kern[(kh - 1 - i) * kw + (kw - 1 - j)] : 0.f;
+
+  float acc[R][NOC];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int oc = 0; oc < NOC; ++oc) acc[r][oc] = 0.f;
+
+  const float* xp = x + plane * in_h * in_w;
+#pragma unroll
+  for (int t = 0; t < NIR; ++t) {
+    const int iy = iy_lo + t;
+    const bool row_ok = iy >= 0 && iy < in_h;
+    const float* row = xp + (int64_t)iy * in_w;
+    float own[LV], left[LV], right[LV];
+    if constexpr (LV == 2) {
+      if (row_ok && mycol + 1 < in_w) {
+        const float2 v = *reinterpret_cast<const float2*>(row + mycol);
+        own[0] = v.x;
+        own[1] = v.y;
+      } else {
+        own[0] = (row_ok && mycol < in_w) ? row[mycol] : 0.f;
+        own[1] = 0.f;
+      }
+    } else {
+      own[0] = (row_ok && mycol < in_w) ? row[mycol] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < LV; ++c) {
+      left[c] = __shfl_up(own[c], 1, 64);
+      right[c] = __shfl_down(own[c], 1, 64);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < LV; ++c) {
+        const int col = mycol - LV + c;
+        left[c] = (row_ok && col >= 0 && col < in_w) ? row[col] : 0.f;
+      }
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int c = 0; c < LV; ++c) {
+        const int col = mycol + LV + c;
+        right[c] = (row_ok && col < in_w) ? row[col] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = t * UP - r * DOWN;
+      if (i < 0 || i >= 4) continue;
+#pragma unroll
+      for (int oc = 0; oc < NOC; ++oc) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int u = oc * DOWN + j - P0;
+          if (bpk::floormod(u, UP) != 0) continue;
+          const int q = bpk::floordiv(u, UP);
+          const int lo = bpk::floordiv(q, LV);
+          const int comp = bpk::floormod(q, LV);
+          const float v = lo < 0 ? left[comp] : (lo == 0 ? own[comp] : right[comp]);
+          acc[r][oc] += v * w[i][j];
+        }
+      }
+    }
+  }
+  const int oxl = ox0 + NOC * lane;
+  float* op = out + plane * out_h * out_w;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int oy = oyb + r;
+    float* orow = op + (int64_t)oy * out_w;
+    if (oy < out_h) {
+      if constexpr (NOC == 2) {
+        if (oxl + 1 < out_w) {
+          *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[r][0], acc[r][1]);
+        } else if (oxl < out_w) {
+          orow[oxl] = acc[r][0];
+        }
+      } else {
+        if (oxl < out_w) orow[oxl] = acc[r][0];
+      }
+    }
+  }
+}
+
+template <int UP, int DOWN, int P0, int R>
+int launch_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
+                  int kh, int kw, int out_h, int out_w, hipStream_t st) {
+  constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;
+  const int strips_x = (int)bpk::ceil_div(out_w, 64 * NOC);
+  const int strips_y = (int)bpk::ceil_div(out_h, R);
+  const int64_t n = (int64_t)major * strips_x * strips_y;
+  if (n <= 0) return BPK_OK;
+  const int64_t blocks = bpk::ceil_div(n, 4);
+  BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
+  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R>), dim3((unsigned)blocks), dim3(256), 0,
+                     st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, strips_x, strips_y, n);
+  BPK_LAUNCH_CHECK("upfirdn2d_stream");
+  return BPK_OK;
+}
+
+// returns true (and sets *rc) when a streaming specialisation applies
+bool try_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
+                int kh, int kw, int up, int down, int p0, int out_h, int out_w, hipStream_t st,
+                int* rc) {
+  static const char* mode = getenv("BPK_UPFIRDN_PATH");
+  if (mode && mode[0] == 't') return false;  // force the LDS-tiled kernel (A/B testing)
+  if (kh > 4 || kw > 4 || (reinterpret_cast<uintptr_t>(x) & 7) || (reinterpret_cast<uintptr_t>(out) & 7))
+    return false;
+  const bool even = in_w % 2 == 0 && out_w % 2 == 0;
+  if (up == 1 && down == 2 && (in_w % 2 == 0)) {
+    if (p0 == 1) { *rc = launch_stream<1, 2, 1, 16>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
+    if (p0 == 2) { *rc = launch_stream<1, 2, 2, 16>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
+  }
+  if (up == 1 && down == 1 && even) {
+    if (p0 == 1) { *rc = launch_stream<1, 1, 1, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
+    if (p0 == 2) { *rc = launch_stream<1, 1, 2, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
+  }
+  if (up == 2 && down == 1 && p0 == 2 && even) {
+    *rc = launch_stream<2, 1, 2, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+    return true;
+  }
+  return false;
+}
+
 template <typename T>
 int upfirdn2d_impl(const T* x, const T* k, T* out, int major, int in_h, int in_w, int minor,
                    int kh, int kw, int ux, int uy, int dx, int dy, int px0, int px1, int py0,
@@ -223,6 +385,13 @@ int upfirdn2d_impl(const T* x, const T* k, T* out, int major, int in_h, int in_w
   BPK_REQUIRE(out_h > 0 && out_w > 0, "upfirdn2d: empty output");
   if (major == 0) return BPK_OK;
   hipStream_t st = bpk::as_stream(stream);
+  if constexpr (std::is_same<T, float>::value) {
+    if (minor == 1 && ux == uy && dx == dy && px0 == py0) {
+      int rc = BPK_OK;
+      if (try_stream(x, k, out, major, in_h, in_w, kh, kw, ux, dx, px0, out_h, out_w, st, &rc))
+        return rc;
+    }
+  }
   const bool tiled = minor == 1 && ux == uy && dx == dy && kh <= 4 && kw <= 4 &&
                      ((ux == 1 && dx == 1) || (ux == 2 && dx == 1) || (ux == 1 && dx == 2));
   if (tiled) {

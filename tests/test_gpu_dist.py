@@ -129,4 +129,9 @@ def test_ddp_train_step_matches_single_rank():
     one = _run(_train_worker, 1)[0][1]
     two = _run(_train_worker, 2)
     np.testing.assert_allclose(two[0][1], two[1][1], rtol=0, atol=0)  # replicas stay identical
-    np.testing.assert_allclose(two[0][1], one, rtol=1e-5, atol=1e-6)
+    # Adam's first step moves every parameter by ~lr * sign(grad) (lr = 2e-4 * 1000/5000 warm-up):
+    # a gradient within rounding of zero may flip sign between the sharded and the full-batch
+    # reduction order, so allow one Adam step of difference
+    diff = np.abs(two[0][1] - one)
+    assert diff.max() <= 2 * 4e-5 + 1e-6
+    assert (diff > 1e-5).mean() < 1e-4
