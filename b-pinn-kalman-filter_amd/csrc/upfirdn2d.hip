@@ -211,15 +211,16 @@ int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w
 }
 
 // Register-streaming kernel for the FIR modes NCSN++ uses (and their adjoints):
-// (up, down) in {(1,2), (1,1), (2,1)}, taps <= 4x4, pad0 = P0 on both axes.  One wave owns
-// a strip of 64*NOC output columns x R output rows of one plane; per input row each lane
+// (up, down) in {(1,2), (1,1), (2,1)}, taps <= 4x4, pad0 = P0 on both axes.  A lane segment of
+// SEGW lanes (SEGW = 64 / 32 / 16 / 8, matched to the plane width so no lane idles) owns a
+// strip of SEGW*NOC output columns x R output rows of one plane.  Per input row each lane
 // loads LV consecutive floats (8-byte loads when LV = 2) and takes its +-1 neighbours'
-// values with cross-lane shuffles, so every input byte is fetched once per strip and there
-// is no LDS staging and no workgroup barrier.  All tap/row/column bookkeeping is
-// compile-time: input row t of the strip feeds output row r through vertical tap
-// i = t*UP - r*DOWN, and output column oc of a lane reads relative input column
-// q = (oc*DOWN + j - P0) / UP of its own / neighbouring lane.
-template <int UP, int DOWN, int P0, int R>
+// values with cross-lane shuffles inside the segment, so there is no LDS staging and no
+// workgroup barrier; short strips (R = 4..8) keep many waves in flight, which is what an
+// HBM-bound stencil needs on MI355X.  All tap bookkeeping is compile-time: input row t of
+// the strip feeds output row r through vertical tap i = t*UP - r*DOWN, and output column oc
+// of a lane reads relative input column q = (oc*DOWN + j - P0) / UP.
+template <int UP, int DOWN, int P0, int R, int SEGW>
 __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict__ x,
                                                          const float* __restrict__ kern,
                                                          float* __restrict__ out, int in_h,
@@ -229,17 +230,20 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
   constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;  // output columns per lane
   constexpr int LV = NOC * DOWN / UP;                   // input columns loaded per lane
   constexpr int NIR = ((R - 1) * DOWN + 3) / UP + 1;    // input rows feeding R output rows
+  constexpr int SEGS = 64 / SEGW;
   const int lane = threadIdx.x & 63;
-  const int64_t strip = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (strip >= n_strips) return;  // wave-uniform
-  const int sxi = (int)(strip % strips_x);
-  const int syi = (int)((strip / strips_x) % strips_y);
-  const int64_t plane = strip / ((int64_t)strips_x * strips_y);
-  const int ox0 = sxi * 64 * NOC;
+  const int sl = lane % SEGW;  // lane within its segment
+  const int64_t strip = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * SEGS + lane / SEGW;
+  const bool active = strip < n_strips;
+  const int64_t sidx = active ? strip : 0;
+  const int sxi = (int)(sidx % strips_x);
+  const int syi = (int)((sidx / strips_x) % strips_y);
+  const int64_t plane = sidx / ((int64_t)strips_x * strips_y);
+  const int ox0 = sxi * SEGW * NOC;
   const int oyb = syi * R;  // R even -> (oyb*DOWN - P0) divisible by UP when UP = 2, P0 = 2
   const int ixbase = ox0 * DOWN / UP;
   const int iy_lo = bpk::floordiv(oyb * DOWN - P0, UP);
-  const int mycol = ixbase + LV * lane;
+  const int mycol = ixbase + LV * sl;
 
   float w[4][4];
 #pragma unroll
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
 #pragma unroll
   for (int t = 0; t < NIR; ++t) {
     const int iy = iy_lo + t;
-    const bool row_ok = iy >= 0 && iy < in_h;
+    const bool row_ok = active && iy >= 0 && iy < in_h;
     const float* row = xp + (int64_t)iy * in_w;
     float own[LV], left[LV], right[LV];
     if constexpr (LV == 2) {
@@ -275,17 +279,17 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
     }
 #pragma unroll
     for (int c = 0; c < LV; ++c) {
-      left[c] = __shfl_up(own[c], 1, 64);
-      right[c] = __shfl_down(own[c], 1, 64);
+      left[c] = __shfl_up(own[c], 1, SEGW);
+      right[c] = __shfl_down(own[c], 1, SEGW);
     }
-    if (lane == 0) {
+    if (sl == 0) {
 #pragma unroll
       for (int c = 0; c < LV; ++c) {
         const int col = mycol - LV + c;
         left[c] = (row_ok && col >= 0 && col < in_w) ? row[col] : 0.f;
       }
     }
-    if (lane == 63) {
+    if (sl == SEGW - 1) {
 #pragma unroll
       for (int c = 0; c < LV; ++c) {
         const int col = mycol + LV + c;
@@ -311,7 +315,8 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
       }
     }
   }
-  const int oxl = ox0 + NOC * lane;
+  if (!active) return;
+  const int oxl = ox0 + NOC * sl;
   float* op = out + plane * out_h * out_w;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -319,10 +324,12 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
     float* orow = op + (int64_t)oy * out_w;
     if (oy < out_h) {
       if constexpr (NOC == 2) {
-        if (oxl + 1 < out_w) {
+        // 8-byte store when the pair is aligned (odd out_w makes every other row odd)
+        if (oxl + 1 < out_w && (((int64_t)oy * out_w + oxl) & 1) == 0 && (out_h * out_w) % 2 == 0) {
           *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[r][0], acc[r][1]);
-        } else if (oxl < out_w) {
-          orow[oxl] = acc[r][0];
+        } else {
+          if (oxl < out_w) orow[oxl] = acc[r][0];
+          if (oxl + 1 < out_w) orow[oxl + 1] = acc[r][1];
         }
       } else {
         if (oxl < out_w) orow[oxl] = acc[r][0];
@@ -331,20 +338,35 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
   }
 }
 
+template <int UP, int DOWN, int P0, int R, int SEGW>
+int launch_stream_seg(const float* x, const float* k, float* out, int major, int in_h, int in_w,
+                      int kh, int kw, int out_h, int out_w, hipStream_t st) {
+  constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;
+  const int strips_x = (int)bpk::ceil_div(out_w, SEGW * NOC);
+  const int strips_y = (int)bpk::ceil_div(out_h, R);
+  const int64_t n = (int64_t)major * strips_x * strips_y;
+  if (n <= 0) return BPK_OK;
+  const int64_t blocks = bpk::ceil_div(n, 4 * (64 / SEGW));
+  BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
+  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R, SEGW>), dim3((unsigned)blocks), dim3(256),
+                     0, st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, strips_x, strips_y, n);
+  BPK_LAUNCH_CHECK("upfirdn2d_stream");
+  return BPK_OK;
+}
+
+// segment width = lanes needed for one output row of the plane (power of two, 8..64)
 template <int UP, int DOWN, int P0, int R>
 int launch_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                   int kh, int kw, int out_h, int out_w, hipStream_t st) {
   constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;
-  const int strips_x = (int)bpk::ceil_div(out_w, 64 * NOC);
-  const int strips_y = (int)bpk::ceil_div(out_h, R);
-  const int64_t n = (int64_t)major * strips_x * strips_y;
-  if (n <= 0) return BPK_OK;
-  const int64_t blocks = bpk::ceil_div(n, 4);
-  BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
-  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R>), dim3((unsigned)blocks), dim3(256), 0,
-                     st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, strips_x, strips_y, n);
-  BPK_LAUNCH_CHECK("upfirdn2d_stream");
-  return BPK_OK;
+  const int lanes = (int)bpk::ceil_div(out_w, NOC);
+  if (lanes <= 8)
+    return launch_stream_seg<UP, DOWN, P0, R, 8>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+  if (lanes <= 16)
+    return launch_stream_seg<UP, DOWN, P0, R, 16>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+  if (lanes <= 32)
+    return launch_stream_seg<UP, DOWN, P0, R, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+  return launch_stream_seg<UP, DOWN, P0, R, 64>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
 }
 
 // returns true (and sets *rc) when a streaming specialisation applies
@@ -352,22 +374,24 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
                 int kh, int kw, int up, int down, int p0, int out_h, int out_w, hipStream_t st,
                 int* rc) {
   static const char* mode = getenv("BPK_UPFIRDN_PATH");
-  if (mode && mode[0] == 't') return false;  // force the LDS-tiled kernel (A/B testing)
-  if (kh > 4 || kw > 4 || (reinterpret_cast<uintptr_t>(x) & 7) || (reinterpret_cast<uintptr_t>(out) & 7))
+  if (mode && mode[0] == 't') return false;  // BPK_UPFIRDN_PATH=tiled forces the LDS kernel
+  if (kh > 4 || kw > 4 || (reinterpret_cast<uintptr_t>(x) & 7) ||
+      (reinterpret_cast<uintptr_t>(out) & 7))
     return false;
-  const bool even = in_w % 2 == 0 && out_w % 2 == 0;
-  if (up == 1 && down == 2 && (in_w % 2 == 0)) {
-    if (p0 == 1) { *rc = launch_stream<1, 2, 1, 16>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
-    if (p0 == 2) { *rc = launch_stream<1, 2, 2, 16>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
+#define BPK_STREAM(U, D, P, RR) \
+  (*rc = launch_stream<U, D, P, RR>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true)
+  // strip heights measured on MI355X (tools/ab_upfirdn.sh): R = 4 (down2), 16 (up2), 8 (1x1)
+  if (in_w % 2 != 0) return false;  // 8-byte row loads need an even row pitch
+  if (up == 1 && down == 2) {
+    if (p0 == 1) return BPK_STREAM(1, 2, 1, 4);
+    if (p0 == 2) return BPK_STREAM(1, 2, 2, 4);
   }
-  if (up == 1 && down == 1 && even) {
-    if (p0 == 1) { *rc = launch_stream<1, 1, 1, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
-    if (p0 == 2) { *rc = launch_stream<1, 1, 2, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st); return true; }
+  if (up == 1 && down == 1) {
+    if (p0 == 1) return BPK_STREAM(1, 1, 1, 8);
+    if (p0 == 2) return BPK_STREAM(1, 1, 2, 8);
   }
-  if (up == 2 && down == 1 && p0 == 2 && even) {
-    *rc = launch_stream<2, 1, 2, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
-    return true;
-  }
+  if (up == 2 && down == 1 && p0 == 2) return BPK_STREAM(2, 1, 2, 16);
+#undef BPK_STREAM
   return false;
 }
 
