@@ -46,8 +46,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=4)
-    ap.add_argument("--miopen-find", type=int, default=1,
-                    help="1: MIOpen exhaustive find (cudnn.benchmark) for every conv shape")
+    ap.add_argument("--miopen-find", type=int, default=0,
+                    help="1: MIOpen exhaustive find (cudnn.benchmark); immediate mode (0) picks "
+                         "the same fp32 Winograd kernels for the forward and avoids minutes of "
+                         "backward-conv searches")
     return ap.parse_args()
 
 
@@ -139,6 +141,10 @@ def cpu_baseline(n_samples):
                       f"samples of 128x128x1, {dt:.1f}s, cpu={platform.processor() or 'x86_64'}"}
 
 
+def log(msg):
+    print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     import dist
@@ -159,8 +165,10 @@ def main():
                             sampling.LangevinCorrector, c.sampling.snr, c.sampling.n_steps_each,
                             continuous=True, device=dev, seed=1234 + ctx.rank * 0,
                             use_graph=not args.no_graph, dist_ctx=ctx if world > 1 else None)
+    log(f"rank {ctx.rank}/{world}: model built, capturing PC step")
     eng.reset(model)
     eng.advance(args.warmup)
+    log("warm-up done, timing PC steps")
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
@@ -193,6 +201,7 @@ def main():
         step_fn = losses.get_step_fn(sde, train=True, optimize_fn=losses.optimization_manager(c),
                                      reduce_mean=True, continuous=True)
         batch = torch.rand(B, 1, 128, 128, device=dev)
+        log(f"sampler {evals_per_s:.1f} evals/s; train warm-up")
         for _ in range(args.train_warmup):
             step_fn(state, batch)
         torch.cuda.synchronize(dev)
@@ -213,6 +222,7 @@ def main():
 
     result = None
     if ctx.rank == 0:
+        log("rooflines")
         roof = conv_roofline(dev, B)
         up_roof = upfirdn_roofline(dev, B)
         model_tflops = evals_per_s * NCSNPP_GFLOP_PER_EVAL / 1e3
@@ -236,6 +246,7 @@ def main():
         if train:
             result.update(train)
     if world == 1 and not args.no_cpu_baseline and ctx.rank == 0:
+        log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.cpu_samples)
         result["speedup_vs_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     if ctx.rank == 0:

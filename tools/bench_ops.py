@@ -56,4 +56,25 @@ bb = torch.randn(128, device=dev)
 with torch.no_grad():
     t = t_of(lambda: residual_rescale(x, h, bb, 2 ** 0.5))
 res["residual [64,128,128,128]"] = {"ms": round(t * 1e3, 4), "GB/s": round(12 * x.numel() / t / 1e9, 1)}
+# ns_step: simulator shape (pinn_kalman/simulator.py:49-52): B=256, 192x192, dt=0.0025, dx=0.005
+from op import ns_step
+g = torch.Generator(device=dev).manual_seed(0)
+B, n = 256, 192
+f = torch.rand(B, 1, n, n, device=dev, generator=g) * 0.9 + 0.1
+p = torch.randn(B, 1, n, n, device=dev, generator=g) * 0.01
+v = (torch.rand(B, 2, n, n, device=dev, generator=g) * 0.45 + 0.05) * \
+    torch.sign(torch.randn(B, 2, n, n, device=dev, generator=g))
+sites = B * n * n
+t = t_of(lambda: ns_step.full_step(f, v, p, 0.0025, 0.005))
+res["ns_step full_step fused B256 192^2"] = {"ms": round(t * 1e3, 4),
+                                            "Gsite/s": round(sites / t / 1e9, 2),
+                                            "GB/s@32B/site": round(32 * sites / t / 1e9, 1)}
+def three():
+    v1 = ns_step.update_velocity(v, p, 0.0025, 0.005)
+    p1 = ns_step.update_pressure(p, v1, 0.0025, 0.005)
+    return ns_step.update_density(f, v1, 0.0025, 0.005)
+t = t_of(three)
+res["ns_step 3 reference ops B256 192^2"] = {"ms": round(t * 1e3, 4),
+                                            "Gsite/s": round(sites / t / 1e9, 2),
+                                            "GB/s@32B/site": round(32 * sites / t / 1e9, 1)}
 print(json.dumps(res, indent=1))
