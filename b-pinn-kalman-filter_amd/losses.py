@@ -154,3 +154,147 @@ def get_step_fn(sde, train, optimize_fn=None, reduce_mean=False, continuous=True
         return loss
 
     return step_fn
+
+
+# ---------------------------------------------------------------- PINN steps
+
+def check_for_nans(model):
+    """True (and the offending name printed) if any parameter holds a NaN (losses.py:225-230)."""
+    for name, param in model.named_parameters():
+        if torch.isnan(param).any():
+            print(f"NaN detected in parameter: {name}")
+            return True
+    return False
+
+
+def _sync_grads(params, ctx):
+    """Batch-sharded PINN training: average the gradients over ranks with one coalesced
+    all-reduce per flat bucket (RCCL over xGMI).  Each rank's loss is a mean over its
+    shard, so the average equals the full-batch gradient."""
+    if ctx is None or not ctx.enabled:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch._utils._flatten_dense_tensors(grads)
+    ctx.all_reduce_sum_(flat)
+    flat.div_(ctx.world_size)
+    for g, s in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+        g.copy_(s)
+
+
+def _observe(config, operator, f):
+    """inpainting measurement + Gaussian noise of variance config.inverse.variance."""
+    return operator(f, keep_shape=True) + torch.randn_like(f) * config.inverse.variance ** 0.5
+
+
+def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
+    """Schedule 1 of PINN training: data losses of FlowNet and PressureNet, each with its
+    own Adam (reference losses.py:233-329).  Returns step_fn(state, operator, batch) ->
+    (loss, v_loss, p_loss) with batch = (f1, f2, x, y, t, target)."""
+    if is_bpinn:
+        raise NotImplementedError("B-PINN needs bayesian_torch (not on the MI355X hot path)")
+    error_fn = torch.nn.MSELoss()
+
+    def flow_loss_fn(model, operator, batch):
+        f1, f2, x, y, t, target = batch
+        f1 = _observe(config, operator, f1)
+        f2 = _observe(config, operator, f2)
+        return model.multiscale_data_mse(model(f1, f2, x, y, t), target, error_fn=error_fn)
+
+    def pres_loss_fn(model, batch):
+        f1, f2, x, y, t, target = batch
+        pyramid = [target[:, 0:2]]
+        for _ in range(len(config.model.feature_nums)):
+            flow = pyramid[-1]
+            pyramid.append(torch.nn.functional.interpolate(
+                flow, size=(flow.shape[2] // 2, flow.shape[3] // 2), mode="bilinear",
+                align_corners=False))
+        return model.data_mse(model(pyramid[::-1], x, y, t), target, error_fn=error_fn)
+
+    def step_fn(state, operator, batch):
+        model = state["model"]
+        flownet, pressurenet = model.flownet, model.pressurenet
+        operator.next()
+        if train:
+            opt_flow, opt_pres = state["optimizer"]
+            flownet.train()
+            opt_flow.zero_grad()
+            v_loss = flow_loss_fn(flownet, operator, batch)
+            v_loss.backward()
+            _sync_grads(list(flownet.parameters()), ctx)
+            optimize_fn(opt_flow, flownet.parameters(), step=state["step"])
+            pressurenet.train()
+            opt_pres.zero_grad()
+            p_loss = pres_loss_fn(pressurenet, batch)
+            p_loss.backward()
+            _sync_grads(list(pressurenet.parameters()), ctx)
+            optimize_fn(opt_pres, pressurenet.parameters(), step=state["step"])
+            state["step"] += 1
+            state["ema"].update(model.parameters())
+        else:
+            model.eval()
+            ema = state["ema"]
+            ema.store(model.parameters())
+            ema.copy_to(model.parameters())
+            v_loss = flow_loss_fn(flownet, operator, batch)
+            p_loss = pres_loss_fn(pressurenet, batch)
+            ema.restore(model.parameters())
+        return v_loss + p_loss, v_loss, p_loss
+
+    return step_fn
+
+
+def get_pinn_step_fn(config, train, optimize_fn, ctx=None):
+    """Schedule 2: data losses + pinn_loss_weight * Navier-Stokes residual (Re = 1e7), both
+    nets trained together; a NaN gradient on PressureNet's last 1x1 conv skips the update
+    (reference losses.py:332-386).  Returns step_fn(state, operator, batch) ->
+    (loss, pinn_loss, data_loss).
+
+    The reference probes that gradient with an extra autograd.grad pass before
+    backward(); here it is read from .grad after the one backward -- the same value, and
+    an identical skip (no optimizer step, no EMA update, step not advanced; the next
+    step starts with zero_grad).  Under batch sharding the averaged gradient carries any
+    rank's NaN, so every rank takes the same decision."""
+
+    def loss_fn(model, operator, batch):
+        f1, f2, x, y, t, target = batch
+        f1 = _observe(config, operator, f1)
+        f2 = _observe(config, operator, f2)
+        flow_pred, pres_pred = model(f1, f2, x, y, t)
+        data_loss = (model.flownet.multiscale_data_mse(flow_pred, target)
+                     + model.pressurenet.data_mse(pres_pred, target))
+        pinn_loss = (model.equation_mse(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
+                     * config.training.pinn_loss_weight)
+        return pinn_loss + data_loss, pinn_loss, data_loss
+
+    def step_fn(state, operator, batch):
+        model = state["model"]
+        operator.next()
+        if train:
+            opt_flow, opt_pres = state["optimizer"]
+            model.train()
+            opt_flow.zero_grad()
+            opt_pres.zero_grad()
+            loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
+            loss.backward()
+            params = list(model.parameters())
+            _sync_grads(params, ctx)
+            w = model.pressurenet.end[-1].weight
+            if w.grad is not None and torch.isnan(w.grad).any():
+                print(">>> Nan Grad Detected <<<")
+                return loss, pinn_loss, data_loss
+            optimize_fn(opt_flow, model.flownet.parameters(), step=state["step"])
+            optimize_fn(opt_pres, model.pressurenet.parameters(), step=state["step"])
+            state["step"] += 1
+            state["ema"].update(model.parameters())
+        else:
+            model.eval()
+            ema = state["ema"]
+            ema.store(model.parameters())
+            ema.copy_to(model.parameters())
+            loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
+            ema.restore(model.parameters())
+        return loss, pinn_loss, data_loss
+
+    return step_fn

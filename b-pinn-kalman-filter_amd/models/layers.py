@@ -219,3 +219,60 @@ class ResnetBlockDDPM(nn.Module):
         if self.in_ch != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
         return residual_rescale(x, h, self.Conv_1.bias, 1.0)
+
+
+# ---------------------------------------------------------------- PINN (NCSN-style) blocks
+
+def ncsn_conv1x1(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=0):
+    """1x1 conv, PyTorch default init scaled by init_scale (reference layers.py:44-50)."""
+    conv = nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=bias,
+                     dilation=dilation, padding=padding)
+    scale = 1e-10 if init_scale == 0 else init_scale
+    conv.weight.data *= scale
+    if bias:
+        conv.bias.data *= scale
+    return conv
+
+
+def ncsn_conv3x3(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=1):
+    """3x3 conv, PyTorch default init scaled by init_scale (reference layers.py:104-110)."""
+    scale = 1e-10 if init_scale == 0 else init_scale
+    conv = nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, bias=bias,
+                     dilation=dilation, padding=padding)
+    conv.weight.data *= scale
+    if bias:
+        conv.bias.data *= scale
+    return conv
+
+
+class ResidualBlock(nn.Module):
+    """Pre-activation residual block used by PressureNet (reference layers.py:438-491).
+
+    norm -> act -> conv3x3 -> norm -> act -> conv3x3, plus an identity or 1x1-conv
+    shortcut.  Only the `resample=None, dilation=1` form is on the hot path
+    (models/flownet.py get_double_res); InstanceNorm2d carries no parameters, so the
+    state-dict keys are conv1.*, conv2.* and shortcut.*.  Kept on aten ops: the PINN
+    residual differentiates through this block twice (create_graph=True).
+    """
+
+    def __init__(self, input_dim, output_dim, resample=None, act=nn.ELU(),
+                 normalization=nn.InstanceNorm2d, adjust_padding=False, dilation=1):
+        super().__init__()
+        if resample is not None or dilation != 1:
+            raise NotImplementedError("ResidualBlock: only resample=None, dilation=1 is built")
+        self.non_linearity = act
+        self.input_dim, self.output_dim = input_dim, output_dim
+        self.resample = resample
+        self.normalization = normalization
+        self.conv1 = ncsn_conv3x3(input_dim, output_dim)
+        self.normalize2 = normalization(output_dim)
+        self.conv2 = ncsn_conv3x3(output_dim, output_dim)
+        if output_dim != input_dim:
+            self.shortcut = ncsn_conv1x1(input_dim, output_dim)
+        self.normalize1 = normalization(input_dim)
+
+    def forward(self, x):
+        h = self.conv1(self.non_linearity(self.normalize1(x)))
+        h = self.conv2(self.non_linearity(self.normalize2(h)))
+        skip = x if self.output_dim == self.input_dim else self.shortcut(x)
+        return skip + h

@@ -2,12 +2,12 @@
 
 Mirrors the reference package `op/` (op/__init__.py:1-2): `upfirdn2d`,
 `fused_leaky_relu` / `FusedLeakyReLU`, and the submodules `grid_sample` and
-`ns_step`; plus the build's fused block ops (`norm_act`) and PC-sampler kernels
+`ns_step`, `correlation`; plus the build's fused block ops (`norm_act`) and PC-sampler kernels
 (`sde_kernels`).  All of them call libbpk.so through the C ABI of include/bpk.h.
 """
 from .fused_act import FusedLeakyReLU, fused_leaky_relu
 from .upfirdn2d import upfirdn2d
-from . import grid_sample, ns_step, norm_act, sde_kernels
+from . import correlation, grid_sample, ns_step, norm_act, sde_kernels
 
-__all__ = ["FusedLeakyReLU", "fused_leaky_relu", "upfirdn2d", "grid_sample", "ns_step",
+__all__ = ["FusedLeakyReLU", "fused_leaky_relu", "upfirdn2d", "correlation", "grid_sample", "ns_step",
            "norm_act", "sde_kernels"]

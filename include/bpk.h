@@ -252,6 +252,25 @@ int bpk_step_increment(int* step_ptr, void* stream);
 int bpk_fill_step_scalar_f32(float* labels, int B, const float* table, const int* step_ptr,
                              void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * FlowNet correlation (cost volume), 7x7 displacements of `stride` pixels.
+ *   first, second : [B, C, H, W] (NCHW, contiguous)
+ *   out           : [B, 49, ceil(H/stride), ceil(W/stride)]
+ *   out[b, (dy+3)*7 + (dx+3), oy, ox] = mean_c first[b,c,oy*s,ox*s] *
+ *                                      second[b,c,oy*s+dy*s, ox*s+dx*s]  (0 outside)
+ * Replaces the CuPy kernels kernel_Correlation_rearrange/updateOutput of
+ * op/correlation.py:13-102 launched by _FunctionCorrelation.forward (:291-370).
+ * bwd: grad_first / grad_second (either may be NULL) [B, C, H, W], fully
+ * written (zero off the stride grid); replaces kernel_Correlation_updateGrad
+ * {First,Second} (op/correlation.py:104-231) launched per sample by
+ * _FunctionCorrelation.backward (:374-460).
+ * ------------------------------------------------------------------------- */
+int bpk_correlation_fwd_f32(const float* first, const float* second, float* out, int B, int C,
+                            int H, int W, int stride, void* stream);
+int bpk_correlation_bwd_f32(const float* first, const float* second, const float* grad_out,
+                            float* grad_first, float* grad_second, int B, int C, int H, int W,
+                            int stride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,160 @@
+"""GPU parity of the PINN path (HIP correlation + grid_sample grad2 inside FlowNet /
+PressureNet, equation_mse, the PINN and preliminary train steps) against the oracle and
+the reference-generated fixtures (tests/golden/make_golden_pinn.py).
+
+Tolerances (fp32, different summation orders / conv algorithms): correlation 1e-5
+absolute on O(1) data; network outputs 1e-4 relative to max|ref|; equation_mse values and
+their input / parameter sensitivities 2e-3 relative (they are products and sums of
+first and second derivatives through ~30 layers); post-step parameters 1e-5 absolute
+(Adam moves each parameter by <= lr)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_golden
+from oracle import correlation_ref as cr
+
+sys.path.insert(0, GOLDEN)
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape,s", [((2, 16, 32, 32), 1), ((3, 5, 9, 13), 1),
+                                     ((2, 4, 10, 7), 2), ((1, 128, 2, 2), 1),
+                                     ((0, 3, 4, 4), 1)])
+def test_correlation_matches_oracle(hip, shape, s):
+    from op.correlation import FunctionCorrelation
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(*shape, generator=g)
+    b = torch.randn(*shape, generator=g)
+    ad, bd = a.to(hip).requires_grad_(), b.to(hip).requires_grad_()
+    out = FunctionCorrelation(ad, bd, s)
+    ref = cr.forward(a.numpy(), b.numpy(), s)
+    assert out.shape == ref.shape
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    if a.numel() == 0:
+        return
+    go = torch.randn(out.shape, generator=g)
+    out.backward(go.to(hip))
+    gf, gs = cr.backward(a.numpy(), b.numpy(), go.numpy(), s)
+    np.testing.assert_allclose(ad.grad.cpu().numpy(), gf, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(bd.grad.cpu().numpy(), gs, rtol=1e-5, atol=1e-5)
+
+
+def test_correlation_rejects_cpu_tensors():
+    from op.correlation import FunctionCorrelation
+    with pytest.raises(RuntimeError, match="HIP"):
+        FunctionCorrelation(torch.zeros(1, 1, 4, 4), torch.zeros(1, 1, 4, 4), 1)
+
+
+def _model(dev):
+    from configs.pinn import pinn_pde
+    from make_golden_pinn import build_weights, small_config
+    from pinn_kalman.pinn import PINN
+    c = small_config(pinn_pde.get_config)
+    m = build_weights(PINN, c).to(dev)
+    c.device = dev
+    return c, m
+
+
+def _close(a, ref, rel, what, floor=1e-30):
+    """max|a - ref| <= rel * max(max|ref|, floor); `floor` covers tensors whose exact
+    gradient is zero (e.g. conv biases feeding an InstanceNorm) and hold only rounding."""
+    a = np.asarray(a, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(a - ref).max() / max(np.abs(ref).max(), floor)
+    assert err <= rel, f"{what}: rel err {err:.3e} > {rel}"
+
+
+def test_pinn_forward_and_residual_match_reference(hip):
+    from make_golden_pinn import sample_idx
+    d = load_golden("pinn_fwd.npz")
+    c, m = _model(hip)
+    m.train()
+    T = lambda k: torch.tensor(d[k], device=hip)
+    x, y, t = (T(k).requires_grad_() for k in ("x", "y", "t"))
+    flows, pres = m(T("f1"), T("f2"), x, y, t)
+    assert len(flows) == int(d["n_flows"])
+    for i, fl in enumerate(flows):
+        _close(fl.detach().cpu(), d[f"flow{i}"], 1e-4, f"flow{i}")
+    _close(pres.detach().cpu(), d["pres"], 1e-4, "pressure")
+    eq7 = m.equation_mse(x, y, t, flows[-1], pres, 10000000.0)
+    _close(eq7.item(), d["eq7"], 2e-3, "equation_mse Re=1e7")
+    m.zero_grad()
+    eq50 = m.equation_mse(x, y, t, flows[-1], pres, 50.0)
+    _close(eq50.item(), d["eq50"], 2e-3, "equation_mse Re=50")
+    gx, gy, gt = torch.autograd.grad(eq50, (x, y, t), retain_graph=True)
+    for name, v in (("gx", gx), ("gy", gy), ("gt", gt)):
+        _close(v.cpu(), d[name], 2e-3, name)
+    eq50.backward()
+    n = 0
+    gscale = max(np.abs(d[k]).max() for k in d.files if k.startswith("g:"))
+    for k, p in m.named_parameters():
+        if "g:" + k in d.files:
+            v = p.grad.reshape(-1).cpu().numpy()
+            _close(v[sample_idx(v.size)], d["g:" + k], 5e-3, "grad " + k, 1e-4 * gscale)
+            n += 1
+    assert n > 50
+
+
+@pytest.mark.parametrize("fixture,factory", [("pinn_step.npz", "get_pinn_step_fn"),
+                                             ("prelim_step.npz", "get_prelim_step_fn")])
+def test_pinn_train_steps_match_reference(hip, fixture, factory):
+    import losses
+    from inverse.operators import InpaintOperator
+    from make_golden_pinn import sample_idx
+    from models.ema import ExponentialMovingAverage
+    d = load_golden(fixture)
+    c, m = _model(hip)
+    em = ExponentialMovingAverage(m.parameters(), decay=c.model.ema_rate)
+    opt_f = losses.get_optimizer(c, m.flownet.parameters())
+    opt_p = losses.get_optimizer(c, m.pressurenet.parameters(), 0.001)
+    state = dict(optimizer=(opt_f, opt_p), model=m, ema=em, step=50)
+    step_fn = getattr(losses, factory)(c, train=True, optimize_fn=losses.optimization_manager(c))
+    T = lambda k: torch.tensor(d[k], device=hip)
+    batch = (T("f1"), T("f2"), T("x").requires_grad_(), T("y").requires_grad_(),
+             T("t").requires_grad_(), T("target"))
+    op = InpaintOperator(mask=[T("mask")])
+    draws = [T(k) for k in sorted((k for k in d.files if k.startswith("noise")),
+                                  key=lambda s: int(s[5:]))]
+    real = torch.randn_like
+    it = iter(draws)
+    torch.randn_like = lambda v, *a, **k: next(it).clone()
+    grads = {}
+    for opt, pref in ((opt_f, "flownet."), (opt_p, "pressurenet.")):
+        net = getattr(m, pref[:-1])
+
+        def capture(*a, _real=opt.step, _net=net, _pref=pref, **k):
+            # after this net's clip_grad_norm_, as the fixture generator records it
+            for kk, p in _net.named_parameters():
+                if p.grad is not None:
+                    grads[_pref + kk] = p.grad.detach().clone()
+            return _real(*a, **k)
+
+        opt.step = capture
+    try:
+        out = step_fn(state, op, batch)
+    finally:
+        torch.randn_like = real
+    np.testing.assert_allclose([o.item() for o in out], d["losses"], rtol=2e-4, atol=1e-9)
+    assert state["step"] == int(d["step1"])
+    gscale = max(np.abs(d[k]).max() for k in d.files if k.startswith("g:"))
+    # parameters whose exact gradient is zero (conv biases feeding an InstanceNorm) hold
+    # rounding noise only, which Adam normalises to steps of up to lr: allow lr there
+    lr = c.optim.lr * min(50 / c.optim.warmup, 1.0)
+    atol = {}
+    for k, p in m.named_parameters():
+        noise_only = "g:" + k in d.files and np.abs(d["g:" + k]).max() <= 1e-4 * gscale
+        atol[k] = 2 * lr if noise_only else 1e-5
+        if "g:" + k in d.files:
+            g = grads[k].reshape(-1).cpu().numpy()
+            _close(g[sample_idx(g.size)], d["g:" + k], 5e-3, "grad " + k, 1e-4 * gscale)
+        v = p.detach().reshape(-1).cpu().numpy()
+        np.testing.assert_allclose(v[sample_idx(v.size)], d["p1:" + k], atol=atol[k],
+                                   err_msg="param " + k)
+    names = [k for k, p in m.named_parameters() if p.requires_grad]
+    for k, s in zip(names, em.shadow_params):
+        v = s.reshape(-1).cpu().numpy()
+        np.testing.assert_allclose(v[sample_idx(v.size)], d["ema:" + k], atol=atol[k])
