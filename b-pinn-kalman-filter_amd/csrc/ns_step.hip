@@ -37,19 +37,6 @@ __device__ inline int sgn(T v) {
   return 0;
 }
 
-// ---- reference device helpers (op/ns_step_kernel.cu:50-75) ----
-__device__ inline float ddx(const float* f, int x, int y, const Geo& g, float dx) {
-  const float* r = f + (int64_t)y * g.nx;
-  if (x == 0) return (r[x + 1] - r[x]) / dx;
-  if (x == g.nx - 1) return (r[x] - r[x - 1]) / dx;
-  return (r[x + 1] - r[x - 1]) / dx / 2;
-}
-__device__ inline float ddy(const float* f, int x, int y, const Geo& g, float dx) {
-  if (y == 0) return (f[(int64_t)(y + 1) * g.nx + x] - f[(int64_t)y * g.nx + x]) / dx;
-  if (y == g.ny - 1) return (f[(int64_t)y * g.nx + x] - f[(int64_t)(y - 1) * g.nx + x]) / dx;
-  return (f[(int64_t)(y + 1) * g.nx + x] - f[(int64_t)(y - 1) * g.nx + x]) / dx / 2;
-}
-
 // CIP advection of one site (op/ns_step_kernel.cu:115-158), operands passed as
 // plane pointers so callers can supply stored or recomputed fields.
 struct CipIn {
@@ -58,35 +45,133 @@ struct CipIn {
   float fy_c, fy_xm, fy_ym;       // fy(x,y) fy(xm,y) fy(x,ym)
 };
 
-__device__ inline float cip_site(const CipIn& q, float u, float v, float dt, float dx) {
+// Correctly rounded division without the IEEE divide sequence.  For b != 0 with
+// r = RN(1/b) and q = RN(a*r) (within 1 ulp of a/b), the residual a - b*q is exact
+// (one FMA) and RN(q + r*(a - b*q)) == RN(a/b) (Markstein's theorem) -- so these are
+// bit-identical to `a / b` while costing a multiply and two FMAs.  The theorem needs
+// every intermediate in the normal range: the fast path is taken only for
+// 1e-25 < |a| < 1e25 and a denominator in [1e-10, 1e10] (`ok`, decided once per
+// launch); everything else -- including exact zeros (sign of a zero quotient), inf
+// and NaN -- takes the true division.
+// The rare true divisions live out of line so the compiler cannot if-convert (and so
+// always execute) the IEEE divide sequence next to the fast path.
+__device__ __attribute__((noinline)) float div_true(float a, float b) { return a / b; }
+__device__ __attribute__((noinline)) double div_true(double a, double b) { return a / b; }
+
+__device__ inline float div_rn(float a, float b, float rb, bool ok) {
+  const float aa = fabsf(a);
+  if (__builtin_expect(!(ok && aa > 1e-25f && aa < 1e25f), 0)) return div_true(a, b);
+  const float q = a * rb;
+  const float rem = __builtin_fmaf(-q, b, a);
+  return __builtin_fmaf(rem, rb, q);
+}
+__device__ inline double div_rn(double a, double b, double rb, bool ok) {
+  const double aa = fabs(a);
+  if (__builtin_expect(!(ok && aa > 1e-200 && aa < 1e200), 0)) return div_true(a, b);
+  const double q = a * rb;
+  const double rem = __builtin_fma(-q, b, a);
+  return __builtin_fma(rem, rb, q);
+}
+
+__device__ inline bool denom_ok(float b) {
+  const float ab = fabsf(b);
+  return ab >= 1e-10f && ab <= 1e10f;
+}
+
+// Per-launch constants of the fast path: dx, dx^3 as the reference rounds them, and
+// their correctly rounded reciprocals (computed once per thread with true divisions).
+struct NsConst {
+  float dt, dx, rdx;       // 1/dx
+  float d3, rd3;           // (dx*dx)*dx, 1/d3 (float)
+  double dxd, rdxd;        // (double)dx, 1/(double)dx
+  double d3d, rd3d;        // (double)d3, 1/(double)d3
+  bool ok_dx, ok_d3;
+  __device__ explicit NsConst(float dt_, float dx_) : dt(dt_), dx(dx_) {
+    rdx = 1.0f / dx;
+    d3 = dx * dx * dx;
+    rd3 = 1.0f / d3;
+    dxd = (double)dx;
+    rdxd = 1.0 / dxd;
+    d3d = (double)d3;
+    rd3d = 1.0 / d3d;
+    ok_dx = denom_ok(dx);
+    ok_d3 = denom_ok(d3);
+  }
+  // reference (d / dx) for a float difference d
+  __device__ float over_dx(float d) const { return div_rn(d, dx, rdx, ok_dx); }
+  // reference central difference (d / dx / 2); /2 == *0.5 exactly
+  __device__ float over_2dx(float d) const { return div_rn(d, dx, rdx, ok_dx) * 0.5f; }
+};
+
+// d / (s * dx^3) in float for s = sgn(...) (the reference's x_s_denom); s == 0 keeps the
+// reference's division by zero (inf/nan)
+__device__ inline float div_sd3(float d, int s, const NsConst& k) {
+  if (s == 0) return div_true(d, (float)s * k.dx * k.dx * k.dx);
+  const float q = div_rn(d, k.d3, k.rd3, k.ok_d3);
+  return s > 0 ? q : -q;
+}
+__device__ inline double div_sd3(double d, int s, const NsConst& k) {
+  if (s == 0) return div_true(d, (double)((float)s * k.dx * k.dx * k.dx));
+  const double q = div_rn(d, k.d3d, k.rd3d, k.ok_d3);
+  return s > 0 ? q : -q;
+}
+
+// cip_site (op/ns_step_kernel.cu:115-158) with the cheap exact divisions; every
+// expression keeps the reference's float/double types and operation order.
+__device__ inline float cip_site_fast(const CipIn& q, float u, float v, const NsConst& k) {
   const int x_s = sgn(u);
   const int y_s = sgn(v);
+  const float dx = k.dx;
   float tmp1 = q.f_c - q.f_ym - q.f_xm + q.f_xmym;
   float tmp2 = q.f_xm - q.f_c;
   float tmp3 = q.f_ym - q.f_c;
-  float x_s_denom = x_s * dx * dx * dx;
-  float y_s_denom = y_s * dx * dx * dx;
-  float a = (x_s * (q.fx_xm + q.fx_c) * dx - 2.0 * (-tmp2)) / x_s_denom;
-  float b = (y_s * (q.fy_ym + q.fy_c) * dx - 2.0 * (-tmp3)) / y_s_denom;
-  float c = (-tmp1 - x_s * (q.fx_ym - q.fx_c) * dx) / y_s_denom;
-  float d = (-tmp1 - y_s * (q.fy_xm - q.fy_c) * dx) / x_s_denom;
-  float e = (3.0 * tmp2 + x_s * (q.fx_xm + 2.0 * q.fx_c) * dx) / dx / dx;
-  float f = (3.0 * tmp3 + y_s * (q.fy_ym + 2.0 * q.fy_c) * dx) / dx / dx;
-  float g = (-(q.fy_xm - q.fy_c) + c * dx * dx) / (x_s * dx);
-  float X = -u * dt;
-  float Y = -v * dt;
+  float a = (float)div_sd3((double)(x_s * (q.fx_xm + q.fx_c) * dx) - 2.0 * (-tmp2), x_s, k);
+  float b = (float)div_sd3((double)(y_s * (q.fy_ym + q.fy_c) * dx) - 2.0 * (-tmp3), y_s, k);
+  float c = div_sd3(-tmp1 - x_s * (q.fx_ym - q.fx_c) * dx, y_s, k);
+  float d = div_sd3(-tmp1 - y_s * (q.fy_xm - q.fy_c) * dx, x_s, k);
+  double en = 3.0 * tmp2 + x_s * (q.fx_xm + 2.0 * q.fx_c) * (double)dx;
+  double fn = 3.0 * tmp3 + y_s * (q.fy_ym + 2.0 * q.fy_c) * (double)dx;
+  float e = (float)div_rn(div_rn(en, k.dxd, k.rdxd, k.ok_dx), k.dxd, k.rdxd, k.ok_dx);
+  float f = (float)div_rn(div_rn(fn, k.dxd, k.rdxd, k.ok_dx), k.dxd, k.rdxd, k.ok_dx);
+  float gn = -(q.fy_xm - q.fy_c) + c * dx * dx;
+  float g;
+  if (x_s == 0) {
+    g = div_true(gn, x_s * dx);
+  } else {
+    const float gq = div_rn(gn, dx, k.rdx, k.ok_dx);
+    g = x_s > 0 ? gq : -gq;
+  }
+  float X = -u * k.dt;
+  float Y = -v * k.dt;
   return ((a * X + c * Y + e) * X + g * Y + q.fx_c) * X + ((b * Y + d * X + f) * Y + q.fy_c) * Y +
          q.f_c;
 }
 
+
+// ---- reference device helpers (op/ns_step_kernel.cu:50-75), exact fast division
+__device__ inline float ddx(const float* f, int x, int y, const Geo& g, const NsConst& c) {
+  const float* r = f + (int64_t)y * g.nx;
+  if (x == 0) return c.over_dx(r[x + 1] - r[x]);
+  if (x == g.nx - 1) return c.over_dx(r[x] - r[x - 1]);
+  return c.over_2dx(r[x + 1] - r[x - 1]);
+}
+__device__ inline float ddy(const float* f, int x, int y, const Geo& g, const NsConst& c) {
+  if (y == 0) return c.over_dx(f[(int64_t)(y + 1) * g.nx + x] - f[(int64_t)y * g.nx + x]);
+  if (y == g.ny - 1) return c.over_dx(f[(int64_t)y * g.nx + x] - f[(int64_t)(y - 1) * g.nx + x]);
+  return c.over_2dx(f[(int64_t)(y + 1) * g.nx + x] - f[(int64_t)(y - 1) * g.nx + x]);
+}
+
+// pressure update of one site (op/ns_step_kernel.cu:205-234):
+// sub_x = V(xu) - V(xd), sub_y = V(yu) - V(yd)
 __device__ inline float pres_site(float p_xd, float p_xu, float p_yd, float p_yu, float u_xu,
                                   float u_xd, float v_xu, float v_xd, float u_yu, float u_yd,
-                                  float v_yu, float v_yd, float dt, float dx) {
-  // sub_x = V(xu) - V(xd), sub_y = V(yu) - V(yd)   (op/ns_step_kernel.cu:219-231)
-  float sxx = u_xu - u_xd, sxy = v_xu - v_xd;
-  float syx = u_yu - u_yd, syy = v_yu - v_yd;
-  float aver_p = 0.25 * (p_xd + p_xu + p_yd + p_yu);
-  float pred_p = aver_p + (sxx * sxx + syy * syy + (syx * sxy)) / 8.0 - dx * (sxx + syy) / (8 * dt);
+                                  float v_yu, float v_yd, float dt, float dx, float r8dt,
+                                  bool ok8) {
+  const float sxx = u_xu - u_xd, sxy = v_xu - v_xd;
+  const float syx = u_yu - u_yd, syy = v_yu - v_yd;
+  const float aver_p = 0.25 * (p_xd + p_xu + p_yd + p_yu);
+  const float pred_p = aver_p + (sxx * sxx + syy * syy + (syx * sxy)) / 8.0 -
+                       div_rn(dx * (sxx + syy), 8 * dt, r8dt, ok8);
   return pred_p;
 }
 
@@ -95,6 +180,7 @@ __device__ inline float pres_site(float p_xd, float p_xu, float p_yd, float p_yu
 __global__ __launch_bounds__(256) void k_gradient(const float* __restrict__ f, int64_t fstride,
                                                   float* __restrict__ fx, float* __restrict__ fy,
                                                   int B, Geo g, float dx) {
+  const NsConst c(1.0f, dx);
   const int64_t total = (int64_t)B * g.hw;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -102,8 +188,8 @@ __global__ __launch_bounds__(256) void k_gradient(const float* __restrict__ f, i
     const int s = (int)(i - b * g.hw);
     const int y = s / g.nx, x = s - y * g.nx;
     const float* fp = f + b * fstride;
-    fx[i] = ddx(fp, x, y, g, dx);
-    fy[i] = ddy(fp, x, y, g, dx);
+    fx[i] = ddx(fp, x, y, g, c);
+    fy[i] = ddy(fp, x, y, g, c);
   }
 }
 
@@ -132,6 +218,7 @@ __global__ __launch_bounds__(256) void k_cip(const float* __restrict__ f, int64_
                                              const float* __restrict__ vel,
                                              float* __restrict__ out, int64_t ostride, int B,
                                              Geo g, float dt, float dx) {
+  const NsConst c(dt, dx);
   const int64_t total = (int64_t)B * g.hw;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -143,7 +230,7 @@ __global__ __launch_bounds__(256) void k_cip(const float* __restrict__ f, int64_
     const int xm = clampx(x - sgn(u), g.nx);
     const int ym = clampx(y - sgn(v), g.ny);
     const CipIn q = gather_cip(f + b * fstride, fx + b * g.hw, fy + b * g.hw, x, y, xm, ym, g.nx);
-    out[b * ostride + s] = cip_site(q, u, v, dt, dx);
+    out[b * ostride + s] = cip_site_fast(q, u, v, c);
   }
 }
 
@@ -181,6 +268,8 @@ __global__ __launch_bounds__(256) void k_pres_update(const float* __restrict__ p
                                                      const float* __restrict__ vel,
                                                      float* __restrict__ pres_n, int B, Geo g,
                                                      float dt, float dx) {
+  const float r8dt = 1.0f / (8 * dt);
+  const bool ok8 = denom_ok(8 * dt);
   const int64_t total = (int64_t)B * g.hw;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -195,73 +284,120 @@ __global__ __launch_bounds__(256) void k_pres_update(const float* __restrict__ p
     const int64_t ixu = (int64_t)y * g.nx + xu, ixd = (int64_t)y * g.nx + xd,
                   iyu = (int64_t)yu * g.nx + x, iyd = (int64_t)yd * g.nx + x;
     pres_n[i] = pres_site(p[ixd], p[ixu], p[iyd], p[iyu], u[ixu], u[ixd], v[ixu], v[ixd], u[iyu],
-                          u[iyd], v[iyu], v[iyd], dt, dx);
+                          u[iyd], v[iyu], v[iyd], dt, dx, r8dt, ok8);
   }
 }
 
 // ---------------------------------------------------------------- fused full step
-// Stage A (per site of sample b): vel' = CIP advection of the vel_n planes, where
-// vel_n = vel - dt grad(p) is recomputed on the fly (bit-identical to storing it).
-// The advected "u" field of batch b is vel_n plane  uplane(b) and the "v" field
-// plane vplane(b):  compat -> (b, b+1)  (reference unbind quirk), else (2b, 2b+1).
+// Stage A: vel' = CIP advection of the vel_n planes, where vel_n = vel - dt grad(p).
+// The advected "u" field of sample b is vel_n plane uplane(b) and the "v" field plane
+// vplane(b):  compat -> (b, b+1)  (reference unbind quirk), else (2b, 2b+1); the
+// advecting velocity is vel_n planes (2b, 2b+1) at the site.
+//
+// LDS-tiled: a block owns a TX x TY tile of one sample.  It computes vel_n of the two
+// field planes over the tile + 2-site halo into LDS once, then their x/y differences
+// over the tile + 1-site halo, then the CIP update of every site from LDS -- instead
+// of recomputing each vel_n value ~16 times per site from HBM.
+constexpr int kTX = 64, kTY = 4;
+constexpr int kFW = kTX + 4, kFH = kTY + 4;  // field tile (+2 halo)
+constexpr int kGW = kTX + 2, kGH = kTY + 2;  // gradient tile (+1 halo)
 
-struct VelN {
-  const float* vel;
-  const float* pres;
-  Geo g;
-  float dt, dx;
-  // vel_n value of memory plane k at (x,y): plane k = sample k>>1, component k&1
-  __device__ inline float at(int64_t k, int x, int y) const {
-    const float* p = pres + (k >> 1) * g.hw;
-    const float grad = (k & 1) ? ddy(p, x, y, g, dx) : ddx(p, x, y, g, dx);
-    return vel[k * g.hw + (int64_t)y * g.nx + x] - grad * dt;
+__device__ inline float veln_at(const float* __restrict__ vel, const float* __restrict__ pres,
+                                int64_t k, int x, int y, const Geo& g, const NsConst& c) {
+  const float* p = pres + (k >> 1) * g.hw;
+  float grad;
+  if (k & 1) {
+    if (y == 0) grad = c.over_dx(p[(int64_t)(y + 1) * g.nx + x] - p[(int64_t)y * g.nx + x]);
+    else if (y == g.ny - 1) grad = c.over_dx(p[(int64_t)y * g.nx + x] - p[(int64_t)(y - 1) * g.nx + x]);
+    else grad = c.over_2dx(p[(int64_t)(y + 1) * g.nx + x] - p[(int64_t)(y - 1) * g.nx + x]);
+  } else {
+    const float* r = p + (int64_t)y * g.nx;
+    if (x == 0) grad = c.over_dx(r[x + 1] - r[x]);
+    else if (x == g.nx - 1) grad = c.over_dx(r[x] - r[x - 1]);
+    else grad = c.over_2dx(r[x + 1] - r[x - 1]);
   }
-  // reference diff_x / diff_y of the vel_n plane k
-  __device__ inline float dfx(int64_t k, int x, int y) const {
-    if (x == 0) return (at(k, x + 1, y) - at(k, x, y)) / dx;
-    if (x == g.nx - 1) return (at(k, x, y) - at(k, x - 1, y)) / dx;
-    return (at(k, x + 1, y) - at(k, x - 1, y)) / dx / 2;
-  }
-  __device__ inline float dfy(int64_t k, int x, int y) const {
-    if (y == 0) return (at(k, x, y + 1) - at(k, x, y)) / dx;
-    if (y == g.ny - 1) return (at(k, x, y) - at(k, x, y - 1)) / dx;
-    return (at(k, x, y + 1) - at(k, x, y - 1)) / dx / 2;
-  }
-  __device__ inline float cip(int64_t k, int x, int y, float u, float v) const {
-    const int xm = clampx(x - sgn(u), g.nx);
-    const int ym = clampx(y - sgn(v), g.ny);
-    CipIn q;
-    q.f_c = at(k, x, y);
-    q.f_ym = at(k, x, ym);
-    q.f_xm = at(k, xm, y);
-    q.f_xmym = at(k, xm, ym);
-    q.fx_c = dfx(k, x, y);
-    q.fx_xm = dfx(k, xm, y);
-    q.fx_ym = dfx(k, x, ym);
-    q.fy_c = dfy(k, x, y);
-    q.fy_xm = dfy(k, xm, y);
-    q.fy_ym = dfy(k, x, ym);
-    return cip_site(q, u, v, dt, dx);
-  }
-};
+  return vel[k * g.hw + (int64_t)y * g.nx + x] - grad * c.dt;
+}
 
-__global__ __launch_bounds__(256) void k_fused_velocity(const float* __restrict__ vel,
-                                                        const float* __restrict__ pres,
-                                                        float* __restrict__ vel_out, int B, Geo g,
-                                                        float dt, float dx, int compat) {
-  const VelN vn{vel, pres, g, dt, dx};
-  const int64_t total = (int64_t)B * g.hw;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = i / g.hw;
-    const int s = (int)(i - b * g.hw);
-    const int y = s / g.nx, x = s - y * g.nx;
-    const float u = vn.at(2 * b, x, y);
-    const float v = vn.at(2 * b + 1, x, y);
-    const int64_t up = compat ? b : 2 * b;
-    const int64_t vp = compat ? b + 1 : 2 * b + 1;
-    vel_out[(2 * b) * g.hw + s] = vn.cip(up, x, y, u, v);
-    vel_out[(2 * b + 1) * g.hw + s] = vn.cip(vp, x, y, u, v);
+__global__ __launch_bounds__(256) void k_fused_velocity_lds(const float* __restrict__ vel,
+                                                            const float* __restrict__ pres,
+                                                            float* __restrict__ vel_out,
+                                                            int B, Geo g, float dt, float dx,
+                                                            int compat, int tiles_x,
+                                                            int tiles_y) {
+  __shared__ float sF[2][kFH][kFW];
+  __shared__ float sFx[2][kGH][kGW];
+  __shared__ float sFy[2][kGH][kGW];
+  const NsConst c(dt, dx);
+  const int tid = threadIdx.x;
+  const int64_t tiles_per_sample = (int64_t)tiles_x * tiles_y;
+  for (int64_t tile = blockIdx.x; tile < (int64_t)B * tiles_per_sample; tile += gridDim.x) {
+    const int b = (int)(tile / tiles_per_sample);
+    const int tr = (int)(tile - (int64_t)b * tiles_per_sample);
+    const int x0 = (tr % tiles_x) * kTX, y0 = (tr / tiles_x) * kTY;
+    const int64_t plane_k[2] = {compat ? (int64_t)b : 2 * (int64_t)b,
+                                compat ? (int64_t)b + 1 : 2 * (int64_t)b + 1};
+    __syncthreads();  // previous tile's readers are done with LDS
+    // 1. vel_n of both field planes over the tile + 2 halo (in-domain points only)
+    for (int i = tid; i < 2 * kFH * kFW; i += blockDim.x) {
+      const int pl = i / (kFH * kFW);
+      const int r = i - pl * (kFH * kFW);
+      const int ly = r / kFW, lx = r - ly * kFW;
+      const int gx = x0 - 2 + lx, gy = y0 - 2 + ly;
+      if (gx >= 0 && gx < g.nx && gy >= 0 && gy < g.ny)
+        sF[pl][ly][lx] = veln_at(vel, pres, plane_k[pl], gx, gy, g, c);
+    }
+    __syncthreads();
+    // 2. reference diff_x / diff_y of the field planes over the tile + 1 halo
+    for (int i = tid; i < 2 * kGH * kGW; i += blockDim.x) {
+      const int pl = i / (kGH * kGW);
+      const int r = i - pl * (kGH * kGW);
+      const int ly = r / kGW, lx = r - ly * kGW;
+      const int gx = x0 - 1 + lx, gy = y0 - 1 + ly;
+      if (gx >= 0 && gx < g.nx && gy >= 0 && gy < g.ny) {
+        const int fy = ly + 1, fx = lx + 1;  // position in sF
+        float dxv, dyv;
+        if (gx == 0) dxv = c.over_dx(sF[pl][fy][fx + 1] - sF[pl][fy][fx]);
+        else if (gx == g.nx - 1) dxv = c.over_dx(sF[pl][fy][fx] - sF[pl][fy][fx - 1]);
+        else dxv = c.over_2dx(sF[pl][fy][fx + 1] - sF[pl][fy][fx - 1]);
+        if (gy == 0) dyv = c.over_dx(sF[pl][fy + 1][fx] - sF[pl][fy][fx]);
+        else if (gy == g.ny - 1) dyv = c.over_dx(sF[pl][fy][fx] - sF[pl][fy - 1][fx]);
+        else dyv = c.over_2dx(sF[pl][fy + 1][fx] - sF[pl][fy - 1][fx]);
+        sFx[pl][ly][lx] = dxv;
+        sFy[pl][ly][lx] = dyv;
+      }
+    }
+    __syncthreads();
+    // 3. CIP update of the tile's sites, both components
+    {
+      const int lx = tid % kTX, ly = tid / kTX;
+      const int x = x0 + lx, y = y0 + ly;
+      if (ly < kTY && x < g.nx && y < g.ny) {
+        const float u = veln_at(vel, pres, 2 * (int64_t)b, x, y, g, c);
+        const float v = veln_at(vel, pres, 2 * (int64_t)b + 1, x, y, g, c);
+        const int xm = clampx(x - sgn(u), g.nx);
+        const int ym = clampx(y - sgn(v), g.ny);
+        // LDS coordinates: field tile origin (x0-2, y0-2), gradient tile origin (x0-1, y0-1)
+        const int fxc = x - x0 + 2, fyc = y - y0 + 2, fxm = xm - x0 + 2, fym = ym - y0 + 2;
+        const int gxc = x - x0 + 1, gyc = y - y0 + 1, gxm = xm - x0 + 1, gym = ym - y0 + 1;
+        const int64_t s = (int64_t)y * g.nx + x;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          CipIn q;
+          q.f_c = sF[pl][fyc][fxc];
+          q.f_ym = sF[pl][fym][fxc];
+          q.f_xm = sF[pl][fyc][fxm];
+          q.f_xmym = sF[pl][fym][fxm];
+          q.fx_c = sFx[pl][gyc][gxc];
+          q.fx_xm = sFx[pl][gyc][gxm];
+          q.fx_ym = sFx[pl][gym][gxc];
+          q.fy_c = sFy[pl][gyc][gxc];
+          q.fy_xm = sFy[pl][gyc][gxm];
+          q.fy_ym = sFy[pl][gym][gxc];
+          vel_out[(2 * (int64_t)b + pl) * g.hw + s] = cip_site_fast(q, u, v, c);
+        }
+      }
+    }
   }
 }
 
@@ -272,6 +408,9 @@ __global__ __launch_bounds__(256) void k_fused_pres_dens(const float* __restrict
                                                          float* __restrict__ dens_out,
                                                          float* __restrict__ pres_out, int B,
                                                          Geo g, float dt, float dx) {
+  const NsConst c(dt, dx);
+  const float r8dt = 1.0f / (8 * dt);
+  const bool ok8 = denom_ok(8 * dt);
   const int64_t total = (int64_t)B * g.hw;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -287,7 +426,7 @@ __global__ __launch_bounds__(256) void k_fused_pres_dens(const float* __restrict
       const int64_t ixu = (int64_t)y * g.nx + xu, ixd = (int64_t)y * g.nx + xd,
                     iyu = (int64_t)yu * g.nx + x, iyd = (int64_t)yd * g.nx + x;
       pres_out[i] = pres_site(p[ixd], p[ixu], p[iyd], p[iyu], u[ixu], u[ixd], v[ixu], v[ixd],
-                              u[iyu], u[iyd], v[iyu], v[iyd], dt, dx);
+                              u[iyu], u[iyd], v[iyu], v[iyd], dt, dx, r8dt, ok8);
     }
     const float uc = u[s], vc = v[s];
     const int xm = clampx(x - sgn(uc), g.nx);
@@ -298,13 +437,13 @@ __global__ __launch_bounds__(256) void k_fused_pres_dens(const float* __restrict
     q.f_ym = f[(int64_t)ym * g.nx + x];
     q.f_xm = f[(int64_t)y * g.nx + xm];
     q.f_xmym = f[(int64_t)ym * g.nx + xm];
-    q.fx_c = ddx(f, x, y, g, dx);
-    q.fx_xm = ddx(f, xm, y, g, dx);
-    q.fx_ym = ddx(f, x, ym, g, dx);
-    q.fy_c = ddy(f, x, y, g, dx);
-    q.fy_xm = ddy(f, xm, y, g, dx);
-    q.fy_ym = ddy(f, x, ym, g, dx);
-    dens_out[i] = cip_site(q, uc, vc, dt, dx);
+    q.fx_c = ddx(f, x, y, g, c);
+    q.fx_xm = ddx(f, xm, y, g, c);
+    q.fx_ym = ddx(f, x, ym, g, c);
+    q.fy_c = ddy(f, x, y, g, c);
+    q.fy_xm = ddy(f, xm, y, g, c);
+    q.fy_ym = ddy(f, x, ym, g, c);
+    dens_out[i] = cip_site_fast(q, uc, vc, c);
   }
 }
 
@@ -459,8 +598,11 @@ extern "C" int bpk_ns_full_step_f32(const float* dens, const float* vel, const f
   if (B == 0) return BPK_OK;
   const Geo g{nx, ny, (int64_t)nx * ny};
   hipStream_t st = bpk::as_stream(stream);
-  hipLaunchKernelGGL(k_fused_velocity, dim3(grid_for(B * g.hw)), dim3(256), 0, st, vel, pres,
-                     vel_out, B, g, dt, dx, compat);
+  const int tiles_x = (int)bpk::ceil_div(nx, kTX), tiles_y = (int)bpk::ceil_div(ny, kTY);
+  const int64_t tiles = (int64_t)B * tiles_x * tiles_y;
+  hipLaunchKernelGGL(k_fused_velocity_lds, dim3((unsigned)std::min<int64_t>(tiles, 1 << 20)),
+                     dim3(256), 0, st, vel, pres, vel_out, B, g, dt, dx, compat, tiles_x,
+                     tiles_y);
   BPK_LAUNCH_CHECK("ns_full_step(velocity)");
   hipLaunchKernelGGL(k_fused_pres_dens, dim3(grid_for(B * g.hw)), dim3(256), 0, st, dens, pres,
                      vel_out, dens_out, pres_out, B, g, dt, dx);

@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=6)
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--pinn-steps", type=int, default=5)
+    ap.add_argument("--pinn-warmup", type=int, default=2)
+    ap.add_argument("--no-pinn", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=4)
@@ -141,6 +144,65 @@ def cpu_baseline(n_samples):
                       f"samples of 128x128x1, {dt:.1f}s, cpu={platform.processor() or 'x86_64'}"}
 
 
+def pinn_batch(c, B, dev, seed=0):
+    """Synthetic configs[3] batch (SURVEY.md 8d cfg #4): frames f1, f2 ~ U[0,1), coordinate
+    channels = jittered meshes (an exact mesh puts sqrt(0) at the pixel holding both x.max()
+    and y.max() and makes every x/y sensitivity NaN, in the reference too), t ~ U{300..899},
+    target (u, v, p) ~ N(0, 0.25)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    n = c.data.image_size
+    lin = torch.linspace(0.05, 1.0, n, device=dev)
+    f1 = torch.rand(B, 1, n, n, device=dev, generator=g)
+    f2 = torch.rand(B, 1, n, n, device=dev, generator=g)
+    x = (lin.view(1, 1, 1, n) + 0.01 * torch.rand(B, 1, n, n, device=dev, generator=g))
+    y = (lin.view(1, 1, n, 1) + 0.01 * torch.rand(B, 1, n, n, device=dev, generator=g))
+    t = torch.randint(300, 900, (B,), device=dev, generator=g).float()
+    target = torch.randn(B, 3, n, n, device=dev, generator=g) * 0.5
+    return (f1, f2, x.contiguous().requires_grad_(), y.contiguous().requires_grad_(),
+            t.requires_grad_(), target)
+
+
+def bench_pinn(args, ctx, dev):
+    """configs[3]: one PINN train step (get_pinn_step_fn: FlowNet + PressureNet forward,
+    equation_mse with create_graph first derivatives and second derivatives -- correlation and
+    grid_sample grad2 on HIP --, backward, two Adams, EMA) at pinn_pde, batch 64/GPU, 64x64;
+    gradients averaged over ranks with one coalesced RCCL all-reduce."""
+    import losses
+    from configs.pinn import pinn_pde
+    from inverse.operators import get_operator
+    from models.ema import ExponentialMovingAverage
+    from pinn_kalman.pinn import PINN
+    c = pinn_pde.get_config()
+    c.device = dev
+    torch.manual_seed(0)
+    model = PINN(c)
+    ema = ExponentialMovingAverage(model.parameters(), decay=c.model.ema_rate)
+    opt_f = losses.get_optimizer(c, model.flownet.parameters())
+    opt_p = losses.get_optimizer(c, model.pressurenet.parameters(), 0.005)
+    state = dict(optimizer=(opt_f, opt_p), model=model, ema=ema, step=c.training.n_iters)
+    step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
+                                      ctx=ctx)
+    operator = get_operator(c)
+    batch = pinn_batch(c, args.batch, dev, seed=ctx.rank)
+    for _ in range(args.pinn_warmup):
+        step_fn(state, operator, batch)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.pinn_steps):
+        loss, pinn_loss, data_loss = step_fn(state, operator, batch)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
+    return {"pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
+            "pinn_ms_per_step": round(dt / args.pinn_steps * 1e3, 2),
+            "pinn_global_batch": args.batch * ctx.world_size,
+            "pinn_losses": [round(float(v.item()), 6) for v in (loss, pinn_loss, data_loss)],
+            "pinn_config": "configs[3]: pinn_pde (FlowNet 2.49M + PressureNet 7.54M), 64x64"}
+
+
 def log(msg):
     print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
 
@@ -220,6 +282,11 @@ def main():
                  "train_tflops": round(args.train_steps * B * world * NCSNPP_GFLOP_PER_TRAIN_SAMPLE
                                        / tdt / 1e3, 2)}
 
+    pinn = None
+    if not args.no_pinn:
+        log("PINN train steps")
+        pinn = bench_pinn(args, ctx, dev)
+
     result = None
     if ctx.rank == 0:
         log("rooflines")
@@ -245,6 +312,8 @@ def main():
         }
         if train:
             result.update(train)
+        if pinn:
+            result.update(pinn)
     if world == 1 and not args.no_cpu_baseline and ctx.rank == 0:
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.cpu_samples)

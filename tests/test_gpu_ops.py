@@ -158,6 +158,32 @@ def test_ns_step_bit_exact_vs_c_oracle(hip, B, nx, ny, compat):
     np.testing.assert_array_equal(d2, rd)
 
 
+@pytest.mark.parametrize("dt,dx", [(0.0037, 0.013), (0.5, 0.9), (1e-4, 2e-3)])
+def test_ns_step_bit_exact_varied_steps_and_degenerate_values(hip, dt, dx):
+    """Other (dt, dx) pairs, quantised fields (many exactly equal neighbours -> zero
+    differences), exact-zero velocities (the reference's division-by-zero NaNs) and a
+    wide magnitude range: the fast exactly-rounded divisions must still match."""
+    from op import ns_step
+    rng = np.random.default_rng(3)
+    B, nx, ny = 3, 40, 24
+    f = np.round(rng.uniform(0, 4, (B, 1, nx, ny))).astype(np.float32) * 0.25
+    p = (rng.normal(0, 1, (B, 1, nx, ny)) * 10.0 ** rng.integers(-6, 3, (B, 1, nx, ny)))
+    p = p.astype(np.float32)
+    v = rng.uniform(-0.5, 0.5, (B, 2, nx, ny)).astype(np.float32)
+    v[rng.random(v.shape) < 0.05] = 0.0
+    ft, vt, pt = (torch.tensor(a, device=hip) for a in (f, v, p))
+    for compat in (True, False):
+        d2, v2, p2 = (t.cpu().numpy() for t in ns_step.full_step(ft, vt, pt, dt, dx, compat=compat))
+        rd, rv, rp = ns_step_ref.full_step(f, v, p, dt, dx, compat)
+        np.testing.assert_array_equal(v2, rv)
+        np.testing.assert_array_equal(p2, rp)
+        np.testing.assert_array_equal(d2, rd)
+        v1 = ns_step.update_velocity(vt, pt, dt, dx, compat=compat).cpu().numpy()
+        np.testing.assert_array_equal(v1, ns_step_ref.update_velocity(v, p, dt, dx, compat))
+    np.testing.assert_array_equal(ns_step.update_density(ft, vt, dt, dx).cpu().numpy(),
+                                  ns_step_ref.update_density(f, v, dt, dx))
+
+
 def test_ns_step_nan_quirk_on_zero_velocity(hip):
     from op import ns_step
     f = torch.rand(1, 1, 8, 8, device=hip)
