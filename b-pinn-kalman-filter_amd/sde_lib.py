@@ -239,3 +239,56 @@ class VESDE(SDE):
         sigma = self.discrete_sigmas.to(t.device)[ts]
         adj = torch.where(ts == 0, torch.zeros_like(t), self.discrete_sigmas[ts - 1].to(t.device))
         return torch.zeros_like(x), torch.sqrt(sigma ** 2 - adj ** 2)
+
+
+class OBSVSDE(SDE):
+    """Observation process y_t of a hidden state SDE (reference sde_lib.py:122-133)."""
+
+    def __init__(self, N, y0, operator):
+        super().__init__(N)
+        self.y0 = y0
+        self.operator = operator
+
+    @abc.abstractmethod
+    def observe_sampling(self, z, t):
+        """y_t sample given standard-normal state noise z."""
+
+
+class LOBSVSDE(OBSVSDE):
+    """Linear observation y = A x of a state SDE (reference sde_lib.py:310-359).
+
+    `observe_sampling(z, t) = alpha(t) y0 + beta(t) A z` with (alpha, beta) the state SDE's
+    marginal coefficients.  A is the operator's gather form (inverse/operators.py); the
+    reference's dense `to_matrix` / `mat & mat` covariance (:327-334) is not materialised.
+    """
+
+    def __init__(self, state_sde: SDE, y0, operator):
+        super().__init__(state_sde.N, y0, operator)
+        self.state_sde = state_sde
+        self.mat = None
+
+    def observe_sampling(self, z, t):
+        alpha, beta = self.state_sde.marginal_coef(t)
+        return alpha[:, None, None] * self.y0 + beta[:, None, None] * self.operator(z, False)
+
+    def prior_sampling(self, shape):
+        return None
+
+    @property
+    def T(self):
+        return 1
+
+    def marginal_prob(self, z, t):
+        raise NotImplementedError("LOBSVSDE.marginal_prob needs the dense observation matrix")
+
+    def prior_logp(self, z):
+        return None
+
+    def sde(self, x, t):
+        return None
+
+    def coefficient(self, t):
+        return None
+
+    def marginal_coef(self, t):
+        return None
