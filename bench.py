@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--pinn-steps", type=int, default=5)
     ap.add_argument("--pinn-warmup", type=int, default=2)
     ap.add_argument("--no-pinn", action="store_true")
+    ap.add_argument("--dps-steps", type=int, default=2, help="accepted RK45 steps timed")
+    ap.add_argument("--no-dps", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=4)
@@ -203,6 +205,55 @@ def bench_pinn(args, ctx, dev):
             "pinn_config": "configs[3]: pinn_pde (FlowNet 2.49M + PressureNet 7.54M), 64x64"}
 
 
+def bench_dps(args, ctx, dev):
+    """configs[4]: DPS conditional sampling (nc_ddpmpp_inpaint_dps at 256x256, DDPM++ 'ddpm'
+    net, B = 16/GPU, inpainting with a Bernoulli(0.5) mask, variance 0.1, RK45 rtol = atol =
+    1e-3).  Unit of work = one function evaluation (score forward + input gradient through
+    the net) of the whole batch; timed over the first `--dps-steps` accepted RK45 steps
+    (incl. the initial-step selection and any rejected attempts)."""
+    import models  # noqa: F401
+    from configs._configdict import ConfigDict
+    from configs.vp import nc_ddpmpp
+    from inverse.conditional_sampling import get_dps_sampler, get_solver
+    from inverse.inverse_lib import get_obsvsde
+    from inverse.operators import InpaintOperator
+    from models import utils as mutils
+    c = nc_ddpmpp.get_config()
+    c.data.image_size = 256
+    c.training.batch_size = 16
+    c.device = dev
+    c.inverse = ConfigDict(dict(operator="inpaint", invert=False, ratio=0.5, sampler="dps",
+                                variance=0.1, solver="RK45", max_steps=args.dps_steps))
+    torch.manual_seed(0)
+    model = mutils.create_model(c, wrap=False).eval()
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    B, n = c.training.batch_size, 256
+    g = torch.Generator(device=dev).manual_seed(1 + ctx.rank)
+    mask = (torch.rand(1, 1, n, n, device=dev, generator=g) > 0.5).float().expand(B, 1, n, n)
+    op = InpaintOperator(mask=[mask.contiguous()])
+    origin = torch.rand(B, 1, n, n, device=dev, generator=g)
+    obs, eps = get_obsvsde(c, op(origin, keep_shape=False), op)
+    sampler = get_dps_sampler(c, obs, (B, 1, n, n), eps=eps, ctx=ctx if ctx.enabled else None)
+    z = torch.randn(B, 1, n, n, device=dev, generator=g)
+    c.inverse.max_steps = 1
+    sampler(model, z=z)  # warm-up (kernel selection, allocator)
+    c.inverse.max_steps = args.dps_steps
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    x = sampler(model, z=z)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
+    nfe = get_solver.last_nfe
+    return {"dps_nfe_per_s": round(nfe / dt, 3), "dps_sample_nfe_per_s": round(nfe * B * ctx.world_size / dt, 2),
+            "dps_nfe_timed": nfe, "dps_global_batch": B * ctx.world_size,
+            "dps_finite": bool(torch.isfinite(x).all().item()),
+            "dps_config": "configs[4]: nc_ddpmpp_inpaint_dps @256x256 (ddpm net), B=16/GPU, RK45"}
+
+
 def log(msg):
     print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
 
@@ -287,6 +338,11 @@ def main():
         log("PINN train steps")
         pinn = bench_pinn(args, ctx, dev)
 
+    dps = None
+    if not args.no_dps:
+        log("DPS function evaluations")
+        dps = bench_dps(args, ctx, dev)
+
     result = None
     if ctx.rank == 0:
         log("rooflines")
@@ -314,6 +370,8 @@ def main():
             result.update(train)
         if pinn:
             result.update(pinn)
+        if dps:
+            result.update(dps)
     if world == 1 and not args.no_cpu_baseline and ctx.rank == 0:
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.cpu_samples)
