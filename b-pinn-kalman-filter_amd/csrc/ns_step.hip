@@ -447,6 +447,36 @@ __global__ __launch_bounds__(256) void k_fused_pres_dens(const float* __restrict
   }
 }
 
+// out[x] = sum_j coef(j, x) g[j] for the 1-D stencil D of diff_x: interior rows j give
+// +-1/(2dx) to x = j+-1, border rows give +-1/dx (one-sided differences)
+__device__ inline float adj1d(const float* g, int64_t stride, int x, int n, float dx) {
+  float acc = 0.f;
+  auto coef = [&](int j, int xx) -> float {  // coefficient of f[xx] in (D f)[j]
+    if (j == 0) return xx == 1 ? 1.0f / dx : (xx == 0 ? -1.0f / dx : 0.f);
+    if (j == n - 1) return xx == n - 1 ? 1.0f / dx : (xx == n - 2 ? -1.0f / dx : 0.f);
+    return xx == j + 1 ? 0.5f / dx : (xx == j - 1 ? -0.5f / dx : 0.f);
+  };
+  for (int j = x - 1; j <= x + 1; ++j)
+    if (j >= 0 && j < n) acc += coef(j, x) * g[(int64_t)j * stride];
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_gradient_adjoint(const float* __restrict__ gx,
+                                                          const float* __restrict__ gy,
+                                                          float* __restrict__ out, int B, Geo g,
+                                                          float dx) {
+  const int64_t total = (int64_t)B * g.hw;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / g.hw;
+    const int s = (int)(i - b * g.hw);
+    const int y = s / g.nx, x = s - y * g.nx;
+    const float* rx = gx + b * g.hw + (int64_t)y * g.nx;  // row y of gx, stride 1 in x
+    const float* cy = gy + b * g.hw + x;                   // column x of gy, stride nx in y
+    out[i] = adj1d(rx, 1, x, g.nx, dx) + adj1d(cy, g.nx, y, g.ny, dx);
+  }
+}
+
 unsigned grid_for(int64_t total) {
   return (unsigned)std::min<int64_t>(bpk::ceil_div(total, 256), 256 * 64);
 }
@@ -466,6 +496,17 @@ extern "C" int bpk_ns_gradient_f32(const float* f, int64_t f_plane_stride, float
   hipLaunchKernelGGL(k_gradient, dim3(grid_for(B * g.hw)), dim3(256), 0, bpk::as_stream(stream), f,
                      f_plane_stride, fx, fy, B, g, dx);
   BPK_LAUNCH_CHECK("ns_gradient");
+  return BPK_OK;
+}
+
+extern "C" int bpk_ns_gradient_adjoint_f32(const float* gx, const float* gy, float* out, int B,
+                                           int nx, int ny, float dx, void* stream) {
+  NS_GEO_CHECK(B, nx, ny);
+  const Geo g{nx, ny, (int64_t)nx * ny};
+  if (B == 0) return BPK_OK;
+  hipLaunchKernelGGL(k_gradient_adjoint, dim3(grid_for(B * g.hw)), dim3(256), 0,
+                     bpk::as_stream(stream), gx, gy, out, B, g, dx);
+  BPK_LAUNCH_CHECK("ns_gradient_adjoint");
   return BPK_OK;
 }
 

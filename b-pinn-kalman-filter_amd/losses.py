@@ -249,7 +249,9 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None):
     """Schedule 2: data losses + pinn_loss_weight * Navier-Stokes residual (Re = 1e7), both
     nets trained together; a NaN gradient on PressureNet's last 1x1 conv skips the update
     (reference losses.py:332-386).  Returns step_fn(state, operator, batch) ->
-    (loss, pinn_loss, data_loss).
+    (loss, pinn_loss, data_loss).  config.training.pinn_residual = 'stencil' switches the
+    residual to `PINN.equation_mse_fd` (spatial derivatives on the ns_step stencil kernel);
+    the default 'autograd' is the reference's.
 
     The reference probes that gradient with an extra autograd.grad pass before
     backward(); here it is read from .grad after the one backward -- the same value, and
@@ -264,7 +266,10 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None):
         flow_pred, pres_pred = model(f1, f2, x, y, t)
         data_loss = (model.flownet.multiscale_data_mse(flow_pred, target)
                      + model.pressurenet.data_mse(pres_pred, target))
-        pinn_loss = (model.equation_mse(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
+        residual = model.equation_mse
+        if getattr(config.training, "pinn_residual", "autograd") == "stencil":
+            residual = model.equation_mse_fd
+        pinn_loss = (residual(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
                      * config.training.pinn_loss_weight)
         return pinn_loss + data_loss, pinn_loss, data_loss
 

@@ -104,3 +104,51 @@ def gradient(field, dx):
     check(lib.bpk_ns_gradient_f32(f.data_ptr(), nx * ny, fx.data_ptr(), fy.data_ptr(),
                                   B, nx, ny, float(dx), stream_ptr(f.device)), "ns_step.gradient")
     return fx, fy
+
+
+def gradient_adjoint(gx, gy, dx):
+    """Dx^T gx + Dy^T gy for the stencil of `gradient` (one launch)."""
+    _check("gradient_adjoint", gx, gy)
+    gx, gy = gx.contiguous(), gy.contiguous()
+    B, nx, ny = _geo(gx)
+    out = torch.empty_like(gx)
+    check(lib.bpk_ns_gradient_adjoint_f32(gx.data_ptr(), gy.data_ptr(), out.data_ptr(), B, nx,
+                                          ny, float(dx), stream_ptr(gx.device)),
+          "ns_step.gradient_adjoint")
+    return out
+
+
+class _StencilGradient(torch.autograd.Function):
+    """(fx, fy) = ns_step stencil gradient of a [B, 1, H, W] field, differentiable to any
+    order (the stencil is linear; its backward is the adjoint kernel, whose own backward
+    is the stencil again)."""
+
+    @staticmethod
+    def forward(ctx, f, dx):
+        ctx.dx = dx
+        return gradient(f, dx)
+
+    @staticmethod
+    def backward(ctx, gx, gy):
+        if gx is None:
+            gx = torch.zeros_like(gy)
+        if gy is None:
+            gy = torch.zeros_like(gx)
+        return _StencilGradientAdjoint.apply(gx, gy, ctx.dx), None
+
+
+class _StencilGradientAdjoint(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gx, gy, dx):
+        ctx.dx = dx
+        return gradient_adjoint(gx, gy, dx)
+
+    @staticmethod
+    def backward(ctx, g):
+        fx, fy = _StencilGradient.apply(g, ctx.dx)
+        return fx, fy, None
+
+
+def stencil_gradient(field, dx):
+    """Differentiable (d/dx, d/dy) of a [B, 1, H, W] field on the ns_step stencil."""
+    return _StencilGradient.apply(field, dx)

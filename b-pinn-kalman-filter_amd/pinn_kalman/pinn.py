@@ -79,6 +79,38 @@ class PINN(nn.Module):
         zeros = torch.zeros_like(x)
         return mse(res_x, zeros) + mse(res_y, zeros) + mse(res_mass, zeros)
 
+    def equation_mse_fd(self, x, y, t, flow, pres, Re, h=None):
+        """Navier-Stokes residual with SPATIAL derivatives on the ns_step stencil (the
+        reference's diff_x / diff_y, op/ns_step_kernel.cu:50-75, run by the same HIP
+        kernel as the simulator) instead of autograd input sensitivities; u_t, v_t stay
+        autograd derivatives w.r.t. t as in `equation_mse`.  `h` is the grid spacing
+        (default: the mean spacing of the x coordinate channel along the width).
+        Differentiable to any order (the stencil's backward is its adjoint kernel)."""
+        from op.ns_step import stencil_gradient
+        u = (self.mask_u * flow).sum(dim=1).unsqueeze(1)
+        v = (self.mask_v * flow).sum(dim=1).unsqueeze(1)
+        p = pres
+        if h is None:
+            h = float((x[:, :, :, -1] - x[:, :, :, 0]).mean()) / (x.shape[-1] - 1)
+        u_t = torch.autograd.grad(u.sum(), t, create_graph=True, retain_graph=True)[0]
+        v_t = torch.autograd.grad(v.sum(), t, create_graph=True, retain_graph=True)[0]
+        u_x, u_y = stencil_gradient(u, h)
+        v_x, v_y = stencil_gradient(v, h)
+        p_x, p_y = stencil_gradient(p, h)
+        u_xx = stencil_gradient(u_x, h)[0]
+        u_yy = stencil_gradient(u_y, h)[1]
+        v_xx = stencil_gradient(v_x, h)[0]
+        v_yy = stencil_gradient(v_y, h)[1]
+        u_t = u_t[:, None, None, None]
+        v_t = v_t[:, None, None, None]
+        nu = 1.0 / Re
+        res_x = u_t + (u * u_x + v * u_y) + p_x - nu * (u_xx + u_yy)
+        res_y = v_t + (u * v_x + v * v_y) + p_y - nu * (v_xx + v_yy)
+        res_mass = u_x + v_y
+        mse = torch.nn.MSELoss()
+        zeros = torch.zeros_like(x)
+        return mse(res_x, zeros) + mse(res_y, zeros) + mse(res_mass, zeros)
+
     def step(self, ft, u):
         """Advance a field by the predicted flow (reference pinn.py:113-114)."""
         return project(ft, u, self.dt)

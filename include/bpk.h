@@ -151,6 +151,12 @@ int bpk_ns_vel_update_f32(const float* vel, const float* px, const float* py, fl
                           int nx, int ny, float dt, void* stream);
 int bpk_ns_pres_update_f32(const float* pres, const float* vel, float* pres_n, int B, int nx, int ny,
                            float dt, float dx, void* stream);
+/* Adjoint of bpk_ns_gradient_f32 (the reference's diff_x / diff_y stencil, one-sided at
+ * the borders): out = Dx^T gx + Dy^T gy on B contiguous planes.  Lets autograd
+ * differentiate through the stencil (the PINN finite-difference residual,
+ * pinn_kalman/pinn.py equation_mse_fd); no reference counterpart. */
+int bpk_ns_gradient_adjoint_f32(const float* gx, const float* gy, float* out, int B, int nx,
+                                int ny, float dx, void* stream);
 int64_t bpk_ns_workspace_bytes(int op, int B, int nx, int ny);
 int bpk_ns_update_density_f32(const float* dens, const float* vel, float* out, void* workspace,
                               int B, int nx, int ny, float dt, float dx, void* stream);

@@ -158,3 +158,73 @@ def test_pinn_train_steps_match_reference(hip, fixture, factory):
     for k, s in zip(names, em.shadow_params):
         v = s.reshape(-1).cpu().numpy()
         np.testing.assert_allclose(v[sample_idx(v.size)], d["ema:" + k], atol=atol[k])
+
+
+def test_simulator_step_rollout_bit_exact(hip):
+    """pinn_kalman.simulator.step (fused ns_step rollout of replicated snapshots) equals the
+    reference's three-op sequence per step (C oracle), bit for bit."""
+    from oracle import ns_step_ref
+    from pinn_kalman import simulator
+    rng = np.random.default_rng(0)
+    begin = np.zeros((2, 6, 200, 200), np.float32)
+    begin[:, 2] = rng.uniform(0.1, 1.0, (2, 200, 200))
+    begin[:, 3:5] = rng.uniform(0.05, 0.5, (2, 2, 200, 200)) * rng.choice([-1, 1], (2, 2, 200, 200))
+    begin[:, 5] = rng.normal(0, 0.01, (2, 200, 200))
+    res, vel, pres = simulator.step(None, begin, t_range=(0, 3), replicas=2, device=hip)
+    f = np.repeat(begin[0, 2:3, 8:200, 4:-4][None], 2, 0)
+    v = begin[0, 3:5, 8:200, 4:-4][None][:, ::-1]
+    v = np.ascontiguousarray(np.repeat(v, 2, 0))
+    p = np.repeat(begin[0, 5:6, 8:200, 4:-4][None], 2, 0)
+    for i in range(3):
+        v = ns_step_ref.update_velocity(v, p, simulator.dt, simulator.dx, True)
+        p = ns_step_ref.update_pressure(p, v, simulator.dt, simulator.dx)
+        f = ns_step_ref.update_density(f, v, simulator.dt, simulator.dx)
+        np.testing.assert_array_equal(vel[i].cpu().numpy(), v)
+        np.testing.assert_array_equal(pres[i].cpu().numpy(), p)
+        np.testing.assert_array_equal(res[i].cpu().numpy(), f)
+
+
+def test_stencil_gradient_forward_exact_and_adjoint(hip):
+    """ns_step stencil gradient == C oracle bit for bit; its backward is the exact adjoint
+    (<D f, g> = <f, D^T g>) and second derivatives flow through it."""
+    from op.ns_step import stencil_gradient
+    from oracle import ns_step_ref
+    rng = np.random.default_rng(0)
+    f = rng.standard_normal((3, 1, 20, 20)).astype(np.float32)
+    ft = torch.tensor(f, device=hip, requires_grad=True)
+    fx, fy = stencil_gradient(ft, 0.05)
+    rx, ry = ns_step_ref.gradient(f, 0.05)
+    np.testing.assert_array_equal(fx.detach().cpu().numpy(), rx)
+    np.testing.assert_array_equal(fy.detach().cpu().numpy(), ry)
+    gx = torch.randn_like(fx)
+    gy = torch.randn_like(fy)
+    (gf,) = torch.autograd.grad((fx * gx).sum() + (fy * gy).sum(), ft, create_graph=True)
+    lhs = float((fx.double() * gx.double()).sum() + (fy.double() * gy.double()).sum())
+    rhs = float((gf.double() * ft.double()).sum())
+    assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
+    # d/df of sum(Dx(Dx f) * w) through the stencil twice == Dx^T Dx^T w
+    w = torch.randn_like(fx)
+    (g2,) = torch.autograd.grad((stencil_gradient(fx, 0.05)[0] * w).sum(), ft)
+    from op.ns_step import gradient_adjoint
+    z = torch.zeros_like(w)
+    ref2 = gradient_adjoint(gradient_adjoint(w, z, 0.05), z, 0.05)
+    np.testing.assert_allclose(g2.cpu().numpy(), ref2.cpu().numpy(), rtol=1e-5, atol=1e-3)
+
+
+def test_pinn_stencil_residual_step_runs(hip):
+    import losses
+    from inverse.operators import InpaintOperator
+    from models.ema import ExponentialMovingAverage
+    d = load_golden("pinn_step.npz")
+    c, m = _model(hip)
+    c.training.pinn_residual = "stencil"
+    em = ExponentialMovingAverage(m.parameters(), decay=c.model.ema_rate)
+    state = dict(optimizer=(losses.get_optimizer(c, m.flownet.parameters()),
+                            losses.get_optimizer(c, m.pressurenet.parameters(), 0.001)),
+                 model=m, ema=em, step=50)
+    step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c))
+    T = lambda k: torch.tensor(d[k], device=hip)
+    batch = (T("f1"), T("f2"), T("x").requires_grad_(), T("y").requires_grad_(),
+             T("t").requires_grad_(), T("target"))
+    loss, pinn_loss, data_loss = step_fn(state, InpaintOperator(mask=[T("mask")]), batch)
+    assert torch.isfinite(loss) and float(pinn_loss) > 0 and state["step"] == 51
