@@ -643,8 +643,11 @@ def get_pc_sampler(sde, shape, predictor, corrector, inverse_scaler, snr, n_step
 
 def get_ode_sampler(sde, shape, inverse_scaler, denoise=False, rtol=1e-5, atol=1e-5,
                     method="RK45", eps=1e-3, device="cuda"):
-    """Probability-flow ODE with scipy's RK45 on the host (reference sampling.py:414-485)."""
-    from scipy import integrate
+    """Probability-flow ODE sampler (reference sampling.py:414-485).  The reference runs
+    scipy's RK45 on a host copy of the batch; here the identical controller
+    (inverse.ode.solve_ivp_rk, same accepted steps and nfev as scipy) runs on the device
+    state, so no per-evaluation host round trip."""
+    from inverse.ode import solve_ivp_rk
 
     def denoise_update_fn(model, x):
         score_fn = get_score_fn(sde, model, train=False, continuous=True)
@@ -662,13 +665,13 @@ def get_ode_sampler(sde, shape, inverse_scaler, denoise=False, rtol=1e-5, atol=1
             x = sde.prior_sampling(shape).to(device) if z is None else z
 
             def ode_func(t, y):
-                y = from_flattened_numpy(y, shape).to(device).type(torch.float32)
+                y = y.reshape(shape).to(torch.float32)
                 vec_t = torch.ones(shape[0], device=y.device) * t
-                return to_flattened_numpy(drift_fn(model, y, vec_t))
+                return drift_fn(model, y, vec_t)
 
-            sol = integrate.solve_ivp(ode_func, (sde.T, eps), to_flattened_numpy(x), rtol=rtol,
-                                      atol=atol, method=method)
-            x = torch.tensor(sol.y[:, -1]).reshape(shape).to(device).type(torch.float32)
+            sol = solve_ivp_rk(ode_func, (sde.T, eps), x.reshape(-1), rtol=rtol, atol=atol,
+                               method=method)
+            x = sol.y.reshape(shape).to(torch.float32)
             if denoise:
                 x = denoise_update_fn(model, x)
             return inverse_scaler(x), sol.nfev
