@@ -1,0 +1,287 @@
+// 3x3 / stride 1 / pad 1 fp32 convolution as fused Winograd F(2x2, 3x3) on the
+// f32-input MFMA (v_mfma_f32_16x16x4_f32) for gfx950.
+//
+// The score networks' convolutions (models/layerspp.py, layers.py: every 3x3 conv of
+// NCSN++ / DDPM++) are ~99 % of their FLOPs.  Winograd F(2,3) computes a 2x2 output
+// tile from a 4x4 input tile with 16 multiplies per (cin, cout) instead of 36:
+//     Y = A^T [ sum_cin (G g G^T) .* (B^T d B) ] A
+// so for each of the 16 transform positions the contraction over cin is a GEMM
+//     M_pos[tile, cout] = sum_cin V_pos[tile, cin] * U_pos[cin, cout]
+// which runs on MFMA with exact f32 products (a k-ordered fma chain).
+//
+// Kernel shape (one workgroup = 4 waves, 256 threads):
+//   * output region: 4 x 8 tiles (8 x 16 pixels) of one image -> M = 32 tiles,
+//     64 output channels (wave w owns couts [16w, 16w + 16));
+//   * K loop over cin in chunks of 8: the 8 x 10 x 18 input patch is loaded to LDS,
+//     each thread transforms one (cin, tile) pair into its 16 V values (LDS), then every
+//     wave issues 16 positions x 2 M-blocks x 2 k-steps = 64 MFMAs 16x16x4 against its
+//     U operands, prefetched from global one chunk ahead;
+//   * accumulators: 16 positions x 2 M-blocks x 4 = 128 f32 per lane; the output
+//     transform is lane-local (all 16 positions of a (tile, cout) sit in one lane), the
+//     result goes through LDS so every global store is a 64-B row segment;
+//   * XCD-aware block order: the cout-blocks of one spatial region are consecutive in
+//     the logical order, which is dealt to one XCD, so they share the input patch in L2.
+// Filter transform U = G g G^T (16 x cin x cout) is a separate, tiny kernel; callers
+// cache U while the weights do not change (sampling).
+#include "bpk_common.h"
+
+#include <algorithm>
+
+namespace {
+
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int kTR = 4, kTC = 8;          // tiles per region (rows, cols)
+constexpr int kM = kTR * kTC;            // 32 tiles
+constexpr int kPR = 2 * kTR + 2;         // 10 patch rows
+constexpr int kPC = 2 * kTC + 2;         // 18 patch cols
+constexpr int kPCp = kPC + 1;            // padded LDS row
+constexpr int kCK = 8;                   // cin per chunk
+constexpr int kOutRows = 2 * kTR, kOutCols = 2 * kTC;  // 8 x 16 pixels
+
+// U[cin][cout][pos] = (G g G^T)[pos] with G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
+// (the 16 positions of one (cin, cout) pair are contiguous: one lane of the GEMM loads
+// its B operands for all positions with four 16-B loads)
+__global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restrict__ w,
+                                                          float* __restrict__ U, int Cin,
+                                                          int Cout) {
+  const int64_t total = (int64_t)Cin * Cout;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Cout);
+    const int ci = (int)(i / Cout);
+    const float* g = w + ((int64_t)co * Cin + ci) * 9;
+    float t[4][3];  // G g
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float g0 = g[c], g1 = g[3 + c], g2 = g[6 + c];
+      t[0][c] = g0;
+      t[1][c] = 0.5f * (g0 + g1 + g2);
+      t[2][c] = 0.5f * (g0 - g1 + g2);
+      t[3][c] = g2;
+    }
+    float* u = U + ((int64_t)ci * Cout + co) * 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a0 = t[r][0], a1 = t[r][1], a2 = t[r][2];
+      u[4 * r + 0] = a0;
+      u[4 * r + 1] = 0.5f * (a0 + a1 + a2);
+      u[4 * r + 2] = 0.5f * (a0 - a1 + a2);
+      u[4 * r + 3] = a2;
+    }
+  }
+}
+
+struct WinoGeo {
+  int N, Cin, Cout, H, W;
+  int regions_x, regions_y, cout_blocks;
+};
+
+constexpr int kWN = 32;                  // couts per wave (2 MFMA N-blocks)
+constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
+constexpr int kOS = kOutRows * kOutCols + 4;  // LDS stride of one staged output channel
+constexpr int kPatchPerThread = (kCK * kPR * kPC + 255) / 256;  // 6
+
+__global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ U,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ y, WinoGeo g,
+                                                          int xcd_remap) {
+  __shared__ float s_patch[kCK][kPR][kPCp];            //  6.1 KB
+  __shared__ __attribute__((aligned(16))) float s_v[kCK * kM * kVS];  // 20.5 KB
+  __shared__ __attribute__((aligned(16))) float s_out[4 * kWN * kOS];  // 67.6 KB
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+
+  // logical block index: blocks b and b + 8 share an XCD under round-robin placement,
+  // so consecutive logical blocks (the cout-blocks of one region) read one input patch
+  int64_t nblk = (int64_t)gridDim.x;
+  int64_t b = blockIdx.x;
+  if (xcd_remap) b = (b % 8) * (nblk / 8) + b / 8;
+  const int cb = (int)(b % g.cout_blocks);
+  int64_t r = b / g.cout_blocks;
+  const int rx = (int)(r % g.regions_x);
+  r /= g.regions_x;
+  const int ry = (int)(r % g.regions_y);
+  const int n = (int)(r / g.regions_y);
+  const int oy0 = ry * kOutRows, ox0 = rx * kOutCols;
+  const int cout_w = cb * (4 * kWN) + wave * kWN;  // first cout of this wave
+
+  f4 acc[16][2][2];
+#pragma unroll
+  for (int p = 0; p < 16; ++p)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) acc[p][mb][nb] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t plane = (int64_t)g.H * g.W;
+  const float* xn = x + (int64_t)n * g.Cin * plane;
+  const int kq = lane >> 4, jj = lane & 15;
+
+  // patch element i of this thread: (cin, row, col) of the 8 x 10 x 18 patch
+  float pv[kPatchPerThread];
+  auto load_patch = [&](int c0) {
+#pragma unroll
+    for (int e = 0; e < kPatchPerThread; ++e) {
+      const int i = tid + 256 * e;
+      float v = 0.f;
+      if (i < kCK * kPR * kPC) {
+        const int c = i / (kPR * kPC);
+        const int rr = i - c * (kPR * kPC);
+        const int py = rr / kPC, px = rr - py * kPC;
+        const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+        if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+          v = xn[(int64_t)(c0 + c) * plane + (int64_t)iy * g.W + ix];
+      }
+      pv[e] = v;
+    }
+  };
+  load_patch(0);
+
+  for (int c0 = 0; c0 < g.Cin; c0 += kCK) {
+    // B operands of this chunk: uo[ks][nb][q] = U[c0 + 4ks + kq][cout_w + 16nb + jj][4q..4q+3]
+    f4 uo[2][2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const f4* src = reinterpret_cast<const f4*>(
+            U + ((int64_t)(c0 + 4 * ks + kq) * g.Cout + cout_w + 16 * nb + jj) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) uo[ks][nb][q] = src[q];
+      }
+    // 1. patch registers -> LDS
+#pragma unroll
+    for (int e = 0; e < kPatchPerThread; ++e) {
+      const int i = tid + 256 * e;
+      if (i < kCK * kPR * kPC) {
+        const int c = i / (kPR * kPC);
+        const int rr = i - c * (kPR * kPC);
+        const int py = rr / kPC, px = rr - py * kPC;
+        s_patch[c][py][px] = pv[e];
+      }
+    }
+    __syncthreads();
+    // 2. V = B^T d B for one (cin, tile) per thread -> s_v[(c * 32 + m) * kVS + pos]
+    {
+      const int c = tid >> 5, m = tid & 31;
+      const int ty = m / kTC, tx = m - ty * kTC;
+      float d[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = s_patch[c][2 * ty + i][2 * tx + j];
+      float t[4][4];  // B^T d   (B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]])
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[0][j] = d[0][j] - d[2][j];
+        t[1][j] = d[1][j] + d[2][j];
+        t[2][j] = d[2][j] - d[1][j];
+        t[3][j] = d[1][j] - d[3][j];
+      }
+      f4* dst = reinterpret_cast<f4*>(&s_v[(c * kM + m) * kVS]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
+    }
+    __syncthreads();
+    // 3. next chunk's patch in flight during the MFMAs
+    if (c0 + kCK < g.Cin) load_patch(c0 + kCK);
+    // 4. MFMAs: acc[p][mb][nb] += V_p[mb*16 + i][4ks + k] * U_p[4ks + k][16nb + j]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        const f4* src = reinterpret_cast<const f4*>(&s_v[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
+        f4 a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = src[q];
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+            acc[p][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p >> 2][p & 3],
+                                                                  uo[ks][nb][p >> 2][p & 3],
+                                                                  acc[p][mb][nb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // 5. output transform (lane-local) -> per-wave LDS staging [cout][8 x 16 pixels]
+  // acc element (mb, nb, reg): tile m = mb*16 + 4*kq + reg, cout = cout_w + 16nb + jj
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    float* so = &s_out[(wave * kWN + 16 * nb + jj) * kOS];
+    const float bv = bias ? bias[cout_w + 16 * nb + jj] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int m = mb * 16 + 4 * kq + rg;
+        const int ty = m / kTC, tx = m - ty * kTC;
+        float t0[4], t1[4];  // A^T M with A^T = [[1,1,1,0],[0,1,-1,-1]]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          t0[j] = acc[j][mb][nb][rg] + acc[4 + j][mb][nb][rg] + acc[8 + j][mb][nb][rg];
+          t1[j] = acc[4 + j][mb][nb][rg] - acc[8 + j][mb][nb][rg] - acc[12 + j][mb][nb][rg];
+        }
+        so[(2 * ty) * kOutCols + 2 * tx] = t0[0] + t0[1] + t0[2] + bv;
+        so[(2 * ty) * kOutCols + 2 * tx + 1] = t0[1] - t0[2] - t0[3] + bv;
+        so[(2 * ty + 1) * kOutCols + 2 * tx] = t1[0] + t1[1] + t1[2] + bv;
+        so[(2 * ty + 1) * kOutCols + 2 * tx + 1] = t1[1] - t1[2] - t1[3] + bv;
+      }
+    }
+  }
+  __syncthreads();
+  // 6. coalesced stores: per wave 32 couts x 8 rows x 16 cols = 1024 float4
+  float* yn = y + (int64_t)n * g.Cout * plane;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int q = it * 64 + lane;
+    const int co = q >> 5;                 // 32 float4 per cout (8 rows x 4)
+    const int rem = q & 31;
+    const int row = rem >> 2, c4 = rem & 3;
+    const f4 v = *reinterpret_cast<const f4*>(&s_out[(wave * kWN + co) * kOS + row * kOutCols + 4 * c4]);
+    *reinterpret_cast<f4*>(&yn[(int64_t)(cout_w + co) * plane + (int64_t)(oy0 + row) * g.W +
+                               ox0 + 4 * c4]) = v;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
+  return (int64_t)16 * Cin * Cout * (int64_t)sizeof(float);
+}
+
+extern "C" int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout,
+                                           void* stream) {
+  BPK_REQUIRE(Cin > 0 && Cout > 0, "conv3x3_wino_filter: bad channels %d -> %d", Cin, Cout);
+  const int64_t total = (int64_t)Cin * Cout;
+  hipLaunchKernelGGL(wino_filter_kernel, dim3((unsigned)std::min<int64_t>(bpk::ceil_div(total, 256), 4096)),
+                     dim3(256), 0, bpk::as_stream(stream), weight, U, Cin, Cout);
+  BPK_LAUNCH_CHECK("conv3x3_wino_filter");
+  return BPK_OK;
+}
+
+extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W) {
+  return N > 0 && Cin > 0 && Cin % kCK == 0 && Cout % (4 * kWN) == 0 && H % kOutRows == 0 &&
+         W % kOutCols == 0;
+}
+
+extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y,
+                                    int N, int Cin, int Cout, int H, int W, void* stream) {
+  BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
+              "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
+              "Cout %% 128, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
+  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (4 * kWN)};
+  const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
+  BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
+  const int remap = (blocks % 8 == 0) ? 1 : 0;
+  hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     bpk::as_stream(stream), x, U, bias, y, g, remap);
+  BPK_LAUNCH_CHECK("conv3x3_wino");
+  return BPK_OK;
+}

@@ -1,0 +1,78 @@
+"""3x3 convolution on the fused Winograd F(2x2,3x3) MFMA kernel (csrc/conv_winograd.hip).
+
+`conv3x3(x, weight, bias=None)` == F.conv2d(x, weight, bias, stride=1, padding=1) for
+fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`); the backward
+(input and weight gradients) runs on MIOpen through torch.nn.grad.  The filter transform
+U = G w G^T is cached on the weight tensor itself (keyed by its version counter, which
+every in-place update such as an optimizer step bumps), so a sampler that never changes
+its weights transforms each filter once.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import check, lib, require_hip, stream_ptr
+
+
+def supported(x, weight):
+    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4:
+        return False
+    if tuple(weight.shape[2:]) != (3, 3) or not x.is_cuda:
+        return False
+    N, C, H, W = x.shape
+    return bool(lib.bpk_conv3x3_wino_supported(N, C, weight.shape[0], H, W)) and \
+        weight.shape[1] == C
+
+
+def filter_transform(weight):
+    """U [Cin, Cout, 16], cached on `weight` while its version counter is unchanged."""
+    cached = getattr(weight, "_bpk_wino_u", None)
+    if cached is not None and cached[0] == weight._version:
+        return cached[1]
+    w = weight.detach().contiguous()
+    Cout, Cin = w.shape[:2]
+    U = torch.empty((Cin, Cout, 16), dtype=torch.float32, device=w.device)
+    check(lib.bpk_conv3x3_wino_filter_f32(w.data_ptr(), U.data_ptr(), Cin, Cout,
+                                          stream_ptr(w.device)), "conv3x3 filter")
+    weight._bpk_wino_u = (weight._version, U)
+    return U
+
+
+def conv3x3_fwd_raw(x, weight, bias=None):
+    x = x.contiguous()
+    N, C, H, W = x.shape
+    Cout = weight.shape[0]
+    U = filter_transform(weight)
+    y = torch.empty((N, Cout, H, W), dtype=x.dtype, device=x.device)
+    b = None if bias is None else bias.detach().contiguous()
+    check(lib.bpk_conv3x3_wino_f32(x.data_ptr(), U.data_ptr(), None if b is None else b.data_ptr(),
+                                   y.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)),
+          "conv3x3_wino")
+    return y
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return conv3x3_fwd_raw(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+        if ctx.needs_input_grad[1]:
+            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 2, 3))
+        return gx, gw, gb
+
+
+def conv3x3(x, weight, bias=None):
+    require_hip(x, weight, bias, what="conv3x3")
+    if not supported(x, weight):
+        raise RuntimeError(f"conv3x3: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
+    return _Conv3x3.apply(x, weight, bias)

@@ -277,6 +277,20 @@ int bpk_correlation_bwd_f32(const float* first, const float* second, const float
                             float* grad_first, float* grad_second, int B, int C, int H, int W,
                             int stride, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * 3x3 / stride 1 / pad 1 convolution, fused Winograd F(2x2,3x3) on the f32 MFMA
+ * (the score networks' conv3x3: models/layers.py ddpm_conv3x3 / layerspp conv3x3,
+ * which the reference runs as torch.nn.Conv2d -> cuDNN).
+ *   filter: U [Cin, Cout, 16] = G w G^T of w [Cout, Cin, 3, 3] (cache while w is fixed)
+ *   conv  : y [N, Cout, H, W] = conv(x [N, Cin, H, W], w) (+ bias[Cout], may be NULL)
+ * supported(): Cin % 8 == 0, Cout % 128 == 0, H % 8 == 0, W % 16 == 0.
+ * ------------------------------------------------------------------------- */
+int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout);
+int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout, void* stream);
+int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W);
+int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y, int N,
+                         int Cin, int Cout, int H, int W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

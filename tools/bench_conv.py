@@ -1,0 +1,35 @@
+"""Winograd MFMA conv3x3 vs MIOpen on the NCSN++ shapes: correctness + time."""
+import json, os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
+import torch
+import torch.nn.functional as F
+from op.conv import conv3x3, filter_transform
+dev = torch.device("cuda:0")
+B = int(os.environ.get("B", 64))
+shapes = [(128, 128, 128), (256, 128, 128), (256, 256, 128), (256, 256, 64), (512, 256, 64),
+          (256, 256, 32), (512, 256, 32), (256, 256, 16), (128, 256, 64)]
+def t_of(fn, reps=10):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps): fn()
+    e.record(); e.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+for cin, cout, hw in shapes:
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(B, cin, hw, hw, device=dev, generator=g)
+    w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(cout, device=dev, generator=g)
+    ref = F.conv2d(x, w, b, padding=1)
+    out = conv3x3(x, w, b)
+    err = ((out - ref).abs().max() / ref.abs().max()).item()
+    filter_transform(w)
+    tw = t_of(lambda: conv3x3(x, w, b))
+    tm = t_of(lambda: F.conv2d(x, w, b, padding=1))
+    fl = 2.0 * B * cin * cout * 9 * hw * hw
+    print(json.dumps(dict(shape=f"{cin}->{cout}@{hw}", rel_err=float(f"{err:.2e}"),
+                          wino_ms=round(tw * 1e3, 3), miopen_ms=round(tm * 1e3, 3),
+                          wino_tflops_eff=round(fl / tw / 1e12, 1),
+                          miopen_tflops=round(fl / tm / 1e12, 1))), flush=True)
