@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import torch
 
-from models.utils import get_score_fn
+from models.utils import get_score_fn, input_grad_only
 from . import ode
 
 
@@ -150,8 +150,9 @@ def get_dps_sampler(config, obsv_sde, shape, eps=1e-3, ctx=None, noise=None):
 
     def dps_sampler(model, z=None):
         x = sde.prior_sampling(shape).to(device) if z is None else z
-        return get_solver(config, make_ode_func(model), x.reshape(-1), sde.T, shape, eps,
-                          ctx=ctx)
+        with input_grad_only(model):
+            return get_solver(config, make_ode_func(model), x.reshape(-1), sde.T, shape, eps,
+                              ctx=ctx)
 
     dps_sampler.make_ode_func = make_ode_func
     dps_sampler.observation = observation

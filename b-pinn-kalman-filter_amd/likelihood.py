@@ -59,7 +59,9 @@ def get_likelihood_fn(sde, inverse_scaler, hutchinson_type="Rademacher", rtol=1e
 
             init = torch.cat([data.reshape(-1).double(),
                               torch.zeros(B, dtype=torch.float64, device=data.device)])
-            sol = solve_ivp_rk(ode_func, (eps, sde.T), init, rtol=rtol, atol=atol, method=method)
+            with mutils.input_grad_only(model):
+                sol = solve_ivp_rk(ode_func, (eps, sde.T), init, rtol=rtol, atol=atol,
+                                   method=method)
             zp = sol.y
             z = zp[:-B].reshape(shape).to(torch.float32)
             delta_logp = zp[-B:].to(torch.float32)

@@ -7,12 +7,14 @@ the fused HIP ops of `op.norm_act` (GroupNorm + bias + SiLU, residual rescale).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from op import conv as conv_op
 from op.norm_act import ACT_NONE, ACT_SILU, group_norm_act, residual_rescale
 
 
@@ -70,9 +72,34 @@ def ddpm_conv1x1(in_planes, out_planes, stride=1, bias=True, init_scale=1., padd
     return conv
 
 
+_WINO_ENABLED = os.environ.get("BPK_CONV", "winograd") != "miopen"
+
+
+def _wino_eligible(x, conv: nn.Conv2d):
+    return (_WINO_ENABLED and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
+            and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+            and x.is_cuda and conv_op.supported(x, conv.weight))
+
+
+def conv2d(x, conv: nn.Conv2d, bias=True):
+    """conv(x) -- the fused Winograd F(2x2,3x3) MFMA kernel (op.conv) for every 3x3 /
+    stride-1 / pad-1 conv whose shape it supports, MIOpen (F.conv2d) otherwise."""
+    b = conv.bias if bias else None
+    if _wino_eligible(x, conv):
+        return conv_op.conv3x3(x, conv.weight, b)
+    return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters / state-dict keys) whose forward is `conv2d` above."""
+
+    def forward(self, x):
+        return conv2d(x, self)
+
+
 def ddpm_conv3x3(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=1):
-    conv = nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=padding,
-                     dilation=dilation, bias=bias)
+    conv = Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=padding,
+                  dilation=dilation, bias=bias)
     conv.weight.data = default_init(init_scale)(conv.weight.data.shape)
     if bias:
         nn.init.zeros_(conv.bias)
@@ -81,7 +108,7 @@ def ddpm_conv3x3(in_planes, out_planes, stride=1, bias=True, dilation=1, init_sc
 
 def conv_nobias(x, conv: nn.Conv2d):
     """Run a Conv2d module without its bias (the bias is folded into a later fused op)."""
-    return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    return conv2d(x, conv, bias=False)
 
 
 def get_timestep_embedding(timesteps, embedding_dim, max_positions=10000):

@@ -13,6 +13,8 @@
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -72,6 +74,22 @@ def create_model(config, wrap=True):
     model = get_model(config.model.name)(config)
     model = model.to(config.device)
     return ModelHolder(model) if wrap else model
+
+
+@contextlib.contextmanager
+def input_grad_only(model):
+    """Freeze the parameters for the duration (restored after): samplers that only need
+    gradients w.r.t. the INPUT (DPS, the likelihood's divergence) then skip every
+    weight-gradient kernel in backward.  Values are unchanged -- the reference computes the
+    same input gradients with the parameters still requiring grad."""
+    flags = [(p, p.requires_grad) for p in model.parameters()]
+    for p, _ in flags:
+        p.requires_grad_(False)
+    try:
+        yield model
+    finally:
+        for p, f in flags:
+            p.requires_grad_(f)
 
 
 def get_model_fn(model, train=False):

@@ -87,19 +87,34 @@ def time_kernel(fn, stream, reps=10):
 
 
 def conv_roofline(dev, batch):
-    """Dominant kernel of the score net: the 3x3 conv 128->128 @128^2 (13 per forward,
-    19% of the FLOPs).  fp32, MFMA-bound."""
+    """Dominant kernel of the score net (74 % of a PC step): the fused Winograd F(2x2,3x3)
+    MFMA conv3x3 (csrc/conv_winograd.hip), measured on its most frequent shape, 128 -> 128
+    channels @ 128x128 (13 per forward).  MFMA-bound.
+
+    achieved = the kernel's algorithmic MFMA FLOPs per launch -- Winograd F(2,3) multiplies
+    16 transformed values per 2x2 output tile per (cin, cout), i.e. 4/9 of the direct
+    convolution's 2*B*Cin*Cout*9*H*W -- over the HIP-event launch time on the launch
+    stream.  `direct_equivalent_tflops` restates the same time against the direct-conv FLOP
+    count (what MIOpen's implicit GEMM executes), `miopen_*` times F.conv2d on the same data."""
     import torch.nn.functional as F
+    from op.conv import conv3x3, filter_transform
     x = torch.randn(batch, 128, 128, 128, device=dev)
     w = torch.randn(128, 128, 3, 3, device=dev) * 0.02
     st = torch.cuda.Stream(dev)
-    t = time_kernel(lambda: F.conv2d(x, w, padding=1), st)
-    flops = 2.0 * batch * 128 * 128 * 9 * 128 * 128
-    ach = flops / t / 1e12
+    with torch.cuda.stream(st):
+        filter_transform(w)
+        t = time_kernel(lambda: conv3x3(x, w), st)
+        tm = time_kernel(lambda: F.conv2d(x, w, padding=1), st)
+    direct = 2.0 * batch * 128 * 128 * 9 * 128 * 128
+    wino = direct * 4.0 / 9.0
+    ach = wino / t / 1e12
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": "conv3x3 128->128 @128x128 fp32 (MIOpen)", "ms_per_launch": round(t * 1e3, 4),
-            "flop_per_launch": flops}
+            "kernel": "wino_f23_kernel conv3x3 128->128 @128x128 fp32 (hand-written, f32 MFMA)",
+            "ms_per_launch": round(t * 1e3, 4), "flop_per_launch": wino,
+            "direct_equivalent_tflops": round(direct / t / 1e12, 2),
+            "miopen_ms_per_launch": round(tm * 1e3, 4),
+            "miopen_tflops": round(direct / tm / 1e12, 2)}
 
 
 def upfirdn_roofline(dev, batch):

@@ -234,3 +234,45 @@ def test_grid_sample_double_backward_gradgradcheck(hip):
     f = lambda a, g: grid_sample_2d(a, g, "border", True)
     assert torch.autograd.gradcheck(f, (inp, grid))
     assert torch.autograd.gradgradcheck(f, (inp, grid))
+
+
+# ------------------------------------------------------------------ Winograd conv3x3
+@pytest.mark.parametrize("N,cin,cout,hw", [(1, 8, 128, 16), (3, 24, 128, 32), (2, 128, 256, 64),
+                                           (2, 256, 128, 16), (1, 512, 256, 32)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_conv3x3_winograd_matches_fp32_reference(hip, N, cin, cout, hw, with_bias):
+    """Fused Winograd F(2x2,3x3) MFMA conv vs a float64 direct convolution; the fp32 MIOpen
+    result is held to the same bound.  Tolerance 2e-5 relative to max|ref| (Winograd's
+    transforms add a few rounding steps per term; the network-level tolerance is 1e-4)."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3
+    g = torch.Generator().manual_seed(N * 1000 + cin)
+    x = torch.randn(N, cin, hw, hw, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(cout, generator=g) if with_bias else None
+    ref = F.conv2d(x.double(), w.double(), None if b is None else b.double(), padding=1)
+    out = conv3x3(x.to(hip), w.to(hip), None if b is None else b.to(hip)).double().cpu()
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() <= 2e-5 * scale
+    mi = F.conv2d(x.to(hip), w.to(hip), None if b is None else b.to(hip), padding=1).double().cpu()
+    assert (mi - ref).abs().max().item() <= 2e-5 * scale
+
+
+def test_conv3x3_winograd_backward_and_filter_cache(hip):
+    import torch.nn.functional as F
+    from op.conv import conv3x3
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 16, 16, 32, generator=g).to(hip).requires_grad_()
+    w = (torch.randn(128, 16, 3, 3, generator=g) * 0.1).to(hip).requires_grad_()
+    b = torch.randn(128, generator=g).to(hip).requires_grad_()
+    go = torch.randn(2, 128, 16, 32, generator=g).to(hip)
+    gx, gw, gb = torch.autograd.grad(conv3x3(x, w, b), (x, w, b), go)
+    rx, rw, rb = torch.autograd.grad(F.conv2d(x, w, b, padding=1), (x, w, b), go)
+    for a, r in ((gx, rx), (gw, rw), (gb, rb)):
+        assert (a - r).abs().max().item() <= 1e-5 * r.abs().max().item()
+    # an in-place weight update invalidates the cached filter transform
+    y0 = conv3x3(x.detach(), w.detach(), None)
+    with torch.no_grad():
+        w.mul_(2.0)
+    y1 = conv3x3(x.detach(), w.detach(), None)
+    assert torch.allclose(y1, 2 * y0, rtol=1e-5, atol=1e-5)
