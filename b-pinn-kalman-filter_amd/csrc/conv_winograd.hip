@@ -87,7 +87,10 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, WinoGeo g,
                                                           int xcd_remap) {
-  __shared__ float s_patch[kCK][kPR][kPCp];            //  6.1 KB
+  // patch [cin][row][col] + a tail that absorbs the writes of out-of-patch slots (so the
+  // stores are branch-free, like the loads)
+  __shared__ float s_patch_raw[kCK * kPR * kPCp + 256];  //  7.1 KB
+  float(*s_patch)[kPR][kPCp] = reinterpret_cast<float(*)[kPR][kPCp]>(s_patch_raw);
   __shared__ __attribute__((aligned(16))) float s_v[kCK * kM * kVS];  // 20.5 KB
   __shared__ __attribute__((aligned(16))) float s_out[4 * kWN * kOS];  // 67.6 KB
 
@@ -122,27 +125,36 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
 
   // patch element i of this thread: (cin, row, col) of the 8 x 10 x 18 patch
   float pv[kPatchPerThread];
+  // branch-free: every lane issues every load (out-of-image / tail elements read a valid
+  // in-plane address and are zeroed after), so the outstanding-load count is static and
+  // the compiler's vmcnt waits stay exact -- the prefetch really overlaps the MFMAs
+  // the zero-padding select is applied when the values are stored to LDS (next chunk),
+  // not here: a select right after a load would wait for that load immediately
+  unsigned pmask = 0;
   auto load_patch = [&](int c0) {
+    pmask = 0;
 #pragma unroll
     for (int e = 0; e < kPatchPerThread; ++e) {
       const int i = tid + 256 * e;
-      float v = 0.f;
-      if (i < kCK * kPR * kPC) {
-        const int c = i / (kPR * kPC);
-        const int rr = i - c * (kPR * kPC);
-        const int py = rr / kPC, px = rr - py * kPC;
-        const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
-        if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
-          v = xn[(int64_t)(c0 + c) * plane + (int64_t)iy * g.W + ix];
-      }
-      pv[e] = v;
+      const bool in_patch = i < kCK * kPR * kPC;
+      const int ii = in_patch ? i : 0;
+      const int c = ii / (kPR * kPC);
+      const int rr = ii - c * (kPR * kPC);
+      const int py = rr / kPC, px = rr - py * kPC;
+      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+      const bool inb = in_patch && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+      const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
+      pv[e] = xn[(int64_t)(c0 + c) * plane + (int64_t)cy * g.W + cx];
+      pmask |= inb ? (1u << e) : 0u;
     }
   };
   load_patch(0);
 
-  for (int c0 = 0; c0 < g.Cin; c0 += kCK) {
-    // B operands of this chunk: uo[ks][nb][q] = U[c0 + 4ks + kq][cout_w + 16nb + jj][4q..4q+3]
-    f4 uo[2][2][4];
+  // B operands: uo[ks][nb][q] = U[c0 + 4ks + kq][cout_w + 16nb + jj][4q..4q+3]; the next
+  // chunk's are loaded right after this chunk's MFMAs have issued, so their latency
+  // overlaps the patch store, the V transform and both barriers of the next chunk
+  f4 uo[2][2][4];
+  auto load_u = [&](int c0) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -152,16 +164,19 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
 #pragma unroll
         for (int q = 0; q < 4; ++q) uo[ks][nb][q] = src[q];
       }
+  };
+  load_u(0);
+
+  for (int c0 = 0; c0 < g.Cin; c0 += kCK) {
     // 1. patch registers -> LDS
 #pragma unroll
     for (int e = 0; e < kPatchPerThread; ++e) {
       const int i = tid + 256 * e;
-      if (i < kCK * kPR * kPC) {
-        const int c = i / (kPR * kPC);
-        const int rr = i - c * (kPR * kPC);
-        const int py = rr / kPC, px = rr - py * kPC;
-        s_patch[c][py][px] = pv[e];
-      }
+      const int c = i / (kPR * kPC);
+      const int rr = i - c * (kPR * kPC);
+      const int py = rr / kPC, px = rr - py * kPC;
+      const int dst = i < kCK * kPR * kPC ? (c * kPR + py) * kPCp + px : kCK * kPR * kPCp + tid;
+      s_patch_raw[dst] = ((pmask >> e) & 1u) ? pv[e] : 0.f;
     }
     __syncthreads();
     // 2. V = B^T d B for one (cin, tile) per thread -> s_v[(c * 32 + m) * kVS + pos]
@@ -188,7 +203,9 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
     }
     __syncthreads();
     // 3. next chunk's patch in flight during the MFMAs
-    if (c0 + kCK < g.Cin) load_patch(c0 + kCK);
+    // (unconditional: the last chunk re-loads itself, so every iteration issues the same
+    // loads and the compiler's vmcnt bookkeeping across the back edge stays exact)
+    load_patch(min(c0 + kCK, g.Cin - kCK));
     // 4. MFMAs: acc[p][mb][nb] += V_p[mb*16 + i][4ks + k] * U_p[4ks + k][16nb + j]
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -207,6 +224,7 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
                                                                   acc[p][mb][nb], 0, 0, 0);
       }
     }
+    load_u(min(c0 + kCK, g.Cin - kCK));
     __syncthreads();
   }
 
