@@ -26,6 +26,7 @@
 #include "bpk_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -77,12 +78,14 @@ struct WinoGeo {
   int regions_x, regions_y, cout_blocks;
 };
 
-constexpr int kWN = 32;                  // couts per wave (2 MFMA N-blocks)
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
 constexpr int kOS = kOutRows * kOutCols + 4;  // LDS stride of one staged output channel
 constexpr int kPatchPerThread = (kCK * kPR * kPC + 255) / 256;  // 6
 
-__global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restrict__ x,
+// NB = MFMA N-blocks (16 couts each) per wave: NB = 2 -> 256 accumulator registers, one
+// workgroup per CU; NB = 1 -> 128, two workgroups per CU whose phases interleave.
+template <int NB>
+__global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ U,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, WinoGeo g,
@@ -92,8 +95,9 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
   __shared__ float s_patch_raw[kCK * kPR * kPCp + 256];  //  7.1 KB
   float(*s_patch)[kPR][kPCp] = reinterpret_cast<float(*)[kPR][kPCp]>(s_patch_raw);
   __shared__ __attribute__((aligned(16))) float s_v[kCK * kM * kVS];  // 20.5 KB
-  __shared__ __attribute__((aligned(16))) float s_out[4 * kWN * kOS];  // 67.6 KB
+  __shared__ __attribute__((aligned(16))) float s_out[4 * 16 * NB * kOS];  // 33.8 KB per NB
 
+  constexpr int kWN = 16 * NB;  // couts per wave
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
 
@@ -111,13 +115,13 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
   const int oy0 = ry * kOutRows, ox0 = rx * kOutCols;
   const int cout_w = cb * (4 * kWN) + wave * kWN;  // first cout of this wave
 
-  f4 acc[16][2][2];
+  f4 acc[16][2][NB];
 #pragma unroll
   for (int p = 0; p < 16; ++p)
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) acc[p][mb][nb] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int64_t plane = (int64_t)g.H * g.W;
   const float* xn = x + (int64_t)n * g.Cin * plane;
@@ -153,12 +157,12 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
   // B operands: uo[ks][nb][q] = U[c0 + 4ks + kq][cout_w + 16nb + jj][4q..4q+3]; the next
   // chunk's are loaded right after this chunk's MFMAs have issued, so their latency
   // overlaps the patch store, the V transform and both barriers of the next chunk
-  f4 uo[2][2][4];
+  f4 uo[2][NB][4];
   auto load_u = [&](int c0) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
+      for (int nb = 0; nb < NB; ++nb) {
         const f4* src = reinterpret_cast<const f4*>(
             U + ((int64_t)(c0 + 4 * ks + kq) * g.Cout + cout_w + 16 * nb + jj) * 16);
 #pragma unroll
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
 #pragma unroll
         for (int p = 0; p < 16; ++p)
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
+          for (int nb = 0; nb < NB; ++nb)
             acc[p][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p >> 2][p & 3],
                                                                   uo[ks][nb][p >> 2][p & 3],
                                                                   acc[p][mb][nb], 0, 0, 0);
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
   // 5. output transform (lane-local) -> per-wave LDS staging [cout][8 x 16 pixels]
   // acc element (mb, nb, reg): tile m = mb*16 + 4*kq + reg, cout = cout_w + 16nb + jj
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     float* so = &s_out[(wave * kWN + 16 * nb + jj) * kOS];
     const float bv = bias ? bias[cout_w + 16 * nb + jj] : 0.f;
 #pragma unroll
@@ -254,10 +258,10 @@ __global__ __launch_bounds__(256, 1) void wino_f23_kernel(const float* __restric
     }
   }
   __syncthreads();
-  // 6. coalesced stores: per wave 32 couts x 8 rows x 16 cols = 1024 float4
+  // 6. coalesced stores: per wave kWN couts x 8 rows x 16 cols = 32 kWN float4
   float* yn = y + (int64_t)n * g.Cout * plane;
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < kWN / 2; ++it) {
     const int q = it * 64 + lane;
     const int co = q >> 5;                 // 32 float4 per cout (8 rows x 4)
     const int rem = q & 31;
@@ -285,7 +289,7 @@ extern "C" int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Ci
 }
 
 extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W) {
-  return N > 0 && Cin > 0 && Cin % kCK == 0 && Cout % (4 * kWN) == 0 && H % kOutRows == 0 &&
+  return N > 0 && Cin > 0 && Cin % kCK == 0 && Cout % 64 == 0 && H % kOutRows == 0 &&
          W % kOutCols == 0;
 }
 
@@ -293,13 +297,24 @@ extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float*
                                     int N, int Cin, int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
-              "Cout %% 128, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
-  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (4 * kWN)};
+              "Cout %% 64, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
+  // NB = 1 (64 couts per workgroup, two workgroups per CU: 2-4 % faster on the NCSN++
+  // shapes than NB = 2) unless BPK_WINO_NB=2 asks for the one-workgroup-per-CU form
+  static const int nb_env = [] {
+    const char* e = getenv("BPK_WINO_NB");
+    return e ? atoi(e) : 1;
+  }();
+  const int nb = (Cout % 128 == 0 && nb_env == 2) ? 2 : 1;
+  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb)};
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
-  hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                     bpk::as_stream(stream), x, U, bias, y, g, remap);
+  if (nb == 2)
+    hipLaunchKernelGGL(wino_f23_kernel<2>, dim3((unsigned)blocks), dim3(256), 0,
+                       bpk::as_stream(stream), x, U, bias, y, g, remap);
+  else
+    hipLaunchKernelGGL(wino_f23_kernel<1>, dim3((unsigned)blocks), dim3(256), 0,
+                       bpk::as_stream(stream), x, U, bias, y, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino");
   return BPK_OK;
 }

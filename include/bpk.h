@@ -283,7 +283,7 @@ int bpk_correlation_bwd_f32(const float* first, const float* second, const float
  * which the reference runs as torch.nn.Conv2d -> cuDNN).
  *   filter: U [Cin, Cout, 16] = G w G^T of w [Cout, Cin, 3, 3] (cache while w is fixed)
  *   conv  : y [N, Cout, H, W] = conv(x [N, Cin, H, W], w) (+ bias[Cout], may be NULL)
- * supported(): Cin % 8 == 0, Cout % 128 == 0, H % 8 == 0, W % 16 == 0.
+ * supported(): Cin % 8 == 0, Cout % 64 == 0, H % 8 == 0, W % 16 == 0.
  * ------------------------------------------------------------------------- */
 int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout);
 int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout, void* stream);
