@@ -211,21 +211,40 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
     // loads and the compiler's vmcnt bookkeeping across the back edge stays exact)
     load_patch(min(c0 + kCK, g.Cin - kCK));
     // 4. MFMAs: acc[p][mb][nb] += V_p[mb*16 + i][4ks + k] * U_p[4ks + k][16nb + j]
+    // A operands (16 positions of one (ks, mb) group = 4 x 16 B) are read one group
+    // ahead, so each group's LDS latency hides behind the previous group's MFMAs.
+    {
+      auto a_src = [&](int grp) {  // grp = 2 ks + mb
+        const int ks = grp >> 1, mb = grp & 1;
+        return reinterpret_cast<const f4*>(&s_v[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
+      };
+      f4 a_cur[4], a_nxt[4];
+      {
+        const f4* src = a_src(0);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+        for (int q = 0; q < 4; ++q) a_cur[q] = src[q];
+      }
 #pragma unroll
-      for (int mb = 0; mb < 2; ++mb) {
-        const f4* src = reinterpret_cast<const f4*>(&s_v[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
-        f4 a[4];
+      for (int grp = 0; grp < 4; ++grp) {
+        if (grp < 3) {
+          const f4* src = a_src(grp + 1);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = src[q];
+          for (int q = 0; q < 4; ++q) a_nxt[q] = src[q];
+        }
+        const int ks = grp >> 1, mb = grp & 1;
 #pragma unroll
         for (int p = 0; p < 16; ++p)
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
-            acc[p][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p >> 2][p & 3],
-                                                                  uo[ks][nb][p >> 2][p & 3],
-                                                                  acc[p][mb][nb], 0, 0, 0);
+            acc[p][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                a_cur[p >> 2][p & 3], uo[ks][nb][p >> 2][p & 3], acc[p][mb][nb], 0, 0, 0);
+        if (grp < 3) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a_cur[q] = a_nxt[q];
+        }
+        // keep the next group's 4 LDS reads ahead of this group's MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 16 * NB, 0);
       }
     }
     load_u(min(c0 + kCK, g.Cin - kCK));
