@@ -58,14 +58,18 @@ class DistContext:
 
 
 def init_from_env(backend=None) -> DistContext:
-    """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK (single process if unset)."""
+    """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK (single process if unset).
+    Backend: `backend`, else $BPK_DIST_BACKEND, else nccl (RCCL) with a GPU and gloo
+    without.  (gloo on GPU tensors lets several ranks share one device -- a rehearsal of
+    the multi-GPU code paths on a one-GPU box.)"""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return DistContext()
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("BPK_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not tdist.is_initialized():

@@ -280,7 +280,8 @@ def main():
     import sde_lib
     ctx = dist.init_from_env()
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
-    dev = torch.device("cuda", ctx.local_rank)
+    # one rank per GPU; more ranks than devices only in a gloo rehearsal on one box
+    dev = torch.device("cuda", ctx.local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     world = ctx.world_size
     B = args.batch
@@ -321,7 +322,7 @@ def main():
         tmodel = model
         tmodel.train()
         if world > 1:
-            tmodel = torch.nn.parallel.DistributedDataParallel(model, device_ids=[ctx.local_rank],
+            tmodel = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
                                                                bucket_cap_mb=100)
         opt = losses.get_optimizer(c, tmodel.parameters())
         ema = ExponentialMovingAverage(tmodel.parameters(), decay=c.model.ema_rate)
