@@ -76,6 +76,7 @@ __global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restric
 struct WinoGeo {
   int N, Cin, Cout, H, W;
   int regions_x, regions_y, cout_blocks;
+  float div;  // fused residual: y = (skip + (conv + bias)) / div when skip != nullptr
 };
 
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
@@ -88,6 +89,7 @@ template <int NB>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ U,
                                                           const float* __restrict__ bias,
+                                                          const float* __restrict__ skip,
                                                           float* __restrict__ y, WinoGeo g,
                                                           int xcd_remap) {
   // patch [cin][row][col] + a tail that absorbs the writes of out-of-patch slots (so the
@@ -278,16 +280,21 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
   }
   __syncthreads();
   // 6. coalesced stores: per wave kWN couts x 8 rows x 16 cols = 32 kWN float4
-  float* yn = y + (int64_t)n * g.Cout * plane;
 #pragma unroll
   for (int it = 0; it < kWN / 2; ++it) {
     const int q = it * 64 + lane;
     const int co = q >> 5;                 // 32 float4 per cout (8 rows x 4)
     const int rem = q & 31;
     const int row = rem >> 2, c4 = rem & 3;
-    const f4 v = *reinterpret_cast<const f4*>(&s_out[(wave * kWN + co) * kOS + row * kOutCols + 4 * c4]);
-    *reinterpret_cast<f4*>(&yn[(int64_t)(cout_w + co) * plane + (int64_t)(oy0 + row) * g.W +
-                               ox0 + 4 * c4]) = v;
+    f4 v = *reinterpret_cast<const f4*>(&s_out[(wave * kWN + co) * kOS + row * kOutCols + 4 * c4]);
+    const int64_t o = (int64_t)n * g.Cout * plane + (int64_t)(cout_w + co) * plane +
+                      (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
+    if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
+      const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+      v = f4{(sk[0] + v[0]) / g.div, (sk[1] + v[1]) / g.div, (sk[2] + v[2]) / g.div,
+             (sk[3] + v[3]) / g.div};
+    }
+    *reinterpret_cast<f4*>(&y[o]) = v;
   }
 }
 
@@ -312,8 +319,9 @@ extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W
          W % kOutCols == 0;
 }
 
-extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y,
-                                    int N, int Cin, int Cout, int H, int W, void* stream) {
+extern "C" int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,
+                                             const float* skip, float div, float* y, int N,
+                                             int Cin, int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
               "Cout %% 64, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
@@ -324,16 +332,21 @@ extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float*
     return e ? atoi(e) : 1;
   }();
   const int nb = (Cout % 128 == 0 && nb_env == 2) ? 2 : 1;
-  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb)};
+  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div};
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
   if (nb == 2)
     hipLaunchKernelGGL(wino_f23_kernel<2>, dim3((unsigned)blocks), dim3(256), 0,
-                       bpk::as_stream(stream), x, U, bias, y, g, remap);
+                       bpk::as_stream(stream), x, U, bias, skip, y, g, remap);
   else
     hipLaunchKernelGGL(wino_f23_kernel<1>, dim3((unsigned)blocks), dim3(256), 0,
-                       bpk::as_stream(stream), x, U, bias, y, g, remap);
+                       bpk::as_stream(stream), x, U, bias, skip, y, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino");
   return BPK_OK;
+}
+
+extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y,
+                                    int N, int Cin, int Cout, int H, int W, void* stream) {
+  return bpk_conv3x3_wino_residual_f32(x, U, bias, nullptr, 1.0f, y, N, Cin, Cout, H, W, stream);
 }

@@ -90,6 +90,14 @@ def conv2d(x, conv: nn.Conv2d, bias=True):
     return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
+def conv_residual(h, conv: nn.Conv2d, bias, skip, div):
+    """(skip + (conv(h) + bias)) / div -- the tail of every residual block -- as ONE
+    Winograd launch when the conv qualifies, else conv + the fused residual kernel."""
+    if _wino_eligible(h, conv) and skip.shape[1] == conv.out_channels:
+        return conv_op.conv3x3(h, conv.weight, bias, skip=skip, div=div)
+    return residual_rescale(skip, conv2d(h, conv, bias=False), bias, div)
+
+
 class Conv2d(nn.Conv2d):
     """nn.Conv2d (same parameters / state-dict keys) whose forward is `conv2d` above."""
 
@@ -242,10 +250,9 @@ class ResnetBlockDDPM(nn.Module):
             bias_nc = bias_nc + self.Dense_0(self.act(temb))
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
         h = self.Dropout_0(h)
-        h = conv_nobias(h, self.Conv_1)
         if self.in_ch != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
-        return residual_rescale(x, h, self.Conv_1.bias, 1.0)
+        return conv_residual(h, self.Conv_1, self.Conv_1.bias, x, 1.0)
 
 
 # ---------------------------------------------------------------- PINN (NCSN-style) blocks

@@ -169,10 +169,10 @@ class ResnetBlockDDPMpp(nn.Module):
             bias_nc = bias_nc + self.Dense_0(self.act(temb))
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
         h = self.Dropout_0(h)
-        h = conv_nobias(h, self.Conv_1)
         if x.shape[1] != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
-        return residual_rescale(x, h, self.Conv_1.bias, np.sqrt(2.) if self.skip_rescale else 1.0)
+        return layers.conv_residual(h, self.Conv_1, self.Conv_1.bias, x,
+                                    np.sqrt(2.) if self.skip_rescale else 1.0)
 
 
 class ResnetBlockBigGANpp(nn.Module):
@@ -220,11 +220,11 @@ class ResnetBlockBigGANpp(nn.Module):
             bias_nc = bias_nc + self.Dense_0(self.act(temb))
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
         h = self.Dropout_0(h)
-        h = conv_nobias(h, self.Conv_1)
         bias = self.Conv_1.bias
         if self.in_ch != self.out_ch or self.up or self.down:
             # the 1x1 skip conv's bias joins Conv_1's in the fused residual (no separate
             # full-tensor bias add after the GEMM)
             x = conv_nobias(x, self.Conv_2)
             bias = bias + self.Conv_2.bias
-        return residual_rescale(x, h, bias, np.sqrt(2.) if self.skip_rescale else 1.0)
+        return layers.conv_residual(h, self.Conv_1, bias, x,
+                                    np.sqrt(2.) if self.skip_rescale else 1.0)

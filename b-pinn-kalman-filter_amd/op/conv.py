@@ -38,41 +38,53 @@ def filter_transform(weight):
     return U
 
 
-def conv3x3_fwd_raw(x, weight, bias=None):
+def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0):
+    """conv(x, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch)."""
     x = x.contiguous()
     N, C, H, W = x.shape
     Cout = weight.shape[0]
     U = filter_transform(weight)
     y = torch.empty((N, Cout, H, W), dtype=x.dtype, device=x.device)
     b = None if bias is None else bias.detach().contiguous()
-    check(lib.bpk_conv3x3_wino_f32(x.data_ptr(), U.data_ptr(), None if b is None else b.data_ptr(),
-                                   y.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)),
-          "conv3x3_wino")
+    sk = None if skip is None else skip.detach().contiguous()
+    if sk is not None and sk.shape != y.shape:
+        raise RuntimeError(f"conv3x3: skip {tuple(sk.shape)} != output {tuple(y.shape)}")
+    check(lib.bpk_conv3x3_wino_residual_f32(
+        x.data_ptr(), U.data_ptr(), None if b is None else b.data_ptr(),
+        None if sk is None else sk.data_ptr(), float(div), y.data_ptr(), N, C, Cout, H, W,
+        stream_ptr(x.device)), "conv3x3_wino")
     return y
 
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, skip, div):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        return conv3x3_fwd_raw(x, weight, bias)
+        ctx.div = float(div)
+        return conv3x3_fwd_raw(x, weight, bias, skip, div)
 
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
-        gx = gw = gb = None
+        gx = gw = gb = gs = None
+        if ctx.div != 1.0:
+            gy = gy / ctx.div
+        if ctx.needs_input_grad[3]:
+            gs = gy
         if ctx.needs_input_grad[0]:
             gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
         if ctx.needs_input_grad[1]:
             gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum((0, 2, 3))
-        return gx, gw, gb
+        return gx, gw, gb, gs, None
 
 
-def conv3x3(x, weight, bias=None):
-    require_hip(x, weight, bias, what="conv3x3")
+def conv3x3(x, weight, bias=None, skip=None, div=1.0):
+    """F.conv2d(x, weight, bias, padding=1), or the residual-block tail
+    (skip + conv2d(x, weight, bias)) / div fused into the same launch."""
+    require_hip(x, weight, bias, skip, what="conv3x3")
     if not supported(x, weight):
         raise RuntimeError(f"conv3x3: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
-    return _Conv3x3.apply(x, weight, bias)
+    return _Conv3x3.apply(x, weight, bias, skip, div)

@@ -24,6 +24,12 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
+# MIOpen compiles the backward-convolution kernels (DSM / PINN training, DPS input
+# gradients) on first use; an in-tree cache directory (filled by an earlier run on the same
+# image) skips minutes of compilation on a fresh box.  Set before torch loads MIOpen.
+_MIOPEN_CACHE = os.path.join(REPO, "b-pinn-kalman-filter_amd", "miopen_cache")
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_MIOPEN_CACHE, "kernels"))
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_MIOPEN_CACHE, "db"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -290,6 +290,12 @@ int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout
 int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W);
 int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y, int N,
                          int Cin, int Cout, int H, int W, void* stream);
+/* Same conv with the residual-block tail fused into the epilogue (layerspp.py:272-274,
+ * ResnetBlockBigGANpp / DDPMpp): y = (skip + (conv(x) + bias)) / div, skip [N, Cout, H, W]
+ * (NULL: plain conv) -- bit-identical to bpk_residual_rescale_f32 on the conv output. */
+int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,
+                                  const float* skip, float div, float* y, int N, int Cin,
+                                  int Cout, int H, int W, void* stream);
 
 #ifdef __cplusplus
 }

@@ -276,3 +276,24 @@ def test_conv3x3_winograd_backward_and_filter_cache(hip):
         w.mul_(2.0)
     y1 = conv3x3(x.detach(), w.detach(), None)
     assert torch.allclose(y1, 2 * y0, rtol=1e-5, atol=1e-5)
+
+
+def test_conv3x3_winograd_fused_residual_tail(hip):
+    """conv3x3(h, w, b, skip=x, div) == residual_rescale(x, conv3x3(h, w), b, div) bit for bit
+    (same epilogue arithmetic), and its gradients match the unfused composition."""
+    from op.conv import conv3x3
+    from op.norm_act import residual_rescale
+    g = torch.Generator().manual_seed(3)
+    h = torch.randn(2, 64, 16, 32, generator=g).to(hip).requires_grad_()
+    w = (torch.randn(64, 64, 3, 3, generator=g) * 0.05).to(hip).requires_grad_()
+    b = torch.randn(64, generator=g).to(hip).requires_grad_()
+    x = torch.randn(2, 64, 16, 32, generator=g).to(hip).requires_grad_()
+    div = float(np.sqrt(2.0))
+    fused = conv3x3(h, w, b, skip=x, div=div)
+    plain = residual_rescale(x, conv3x3(h, w), b, div)
+    assert torch.equal(fused, plain)
+    go = torch.randn_like(fused)
+    g1 = torch.autograd.grad(fused, (h, w, b, x), go)
+    g2 = torch.autograd.grad(plain, (h, w, b, x), go)
+    for a, r in zip(g1, g2):
+        assert (a - r).abs().max().item() <= 1e-5 * max(1.0, r.abs().max().item())
