@@ -78,6 +78,16 @@ def build_model(dev, seed=0):
     return c, model
 
 
+def _pmc_traffic(kernel_key):
+    """HBM bytes per launch of a roofline kernel, from the committed PMC passes
+    (profiles/r01_pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, same kernel and shape)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "r01_pmc_traffic.json")) as f:
+            return json.load(f)[kernel_key]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def time_kernel(fn, stream, reps=10):
     """Average duration (s) of fn() measured with HIP events on `stream`."""
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -115,7 +125,10 @@ def conv_roofline(dev, batch):
     wino = direct * 4.0 / 9.0
     ach = wino / t / 1e12
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": _pmc_traffic("wino_f23_kernel conv3x3 128->128 @128x128 B=64")
+            if batch == 64 else None,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
             "kernel": "wino_f23_kernel conv3x3 128->128 @128x128 fp32 (hand-written, f32 MFMA)",
             "ms_per_launch": round(t * 1e3, 4), "flop_per_launch": wino,
             "direct_equivalent_tflops": round(direct / t / 1e12, 2),
@@ -134,7 +147,9 @@ def upfirdn_roofline(dev, batch):
     nbytes = 4.0 * (x.numel() + x.numel() // 4)
     ach = nbytes / t / 1e9
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": _pmc_traffic("upfirdn2d down2 k4 [64,128,128,128]") if batch == 64 else None,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
             "kernel": "upfirdn2d down2 k4 [B,128,128,128]", "ms_per_launch": round(t * 1e3, 4),
             "bytes_per_launch": nbytes}
 
