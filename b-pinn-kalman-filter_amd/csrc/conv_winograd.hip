@@ -85,13 +85,20 @@ constexpr int kPatchPerThread = (kCK * kPR * kPC + 255) / 256;  // 6
 
 // NB = MFMA N-blocks (16 couts each) per wave: NB = 2 -> 256 accumulator registers, one
 // workgroup per CU; NB = 1 -> 128, two workgroups per CU whose phases interleave.
-template <int NB>
+// PRE: the conv input is act(GroupNorm(x + b)) given as x and its per-(n, cin) affine form
+// pre[n][cin] = (s, t) (bpk_group_norm_affine_f32): the patch load applies silu(x s + t)
+// (zero padding stays zero), so the normalized tensor is never written to HBM.
+__device__ inline float silu_f(float z) { return z / (1.f + expf(-z)); }
+
+template <int NB, bool PRE>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ U,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ skip,
+                                                          const float2* __restrict__ pre,
                                                           float* __restrict__ y, WinoGeo g,
                                                           int xcd_remap) {
+  __shared__ float2 s_ss[2][kCK];  // PRE: (s, t) of the chunk's input channels
   // patch [cin][row][col] + a tail that absorbs the writes of out-of-patch slots (so the
   // stores are branch-free, like the loads)
   __shared__ float s_patch_raw[kCK * kPR * kPCp + 256];  //  7.1 KB
@@ -172,8 +179,15 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
       }
   };
   load_u(0);
+  const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
+  float2 ss_next = make_float2(1.f, 0.f);
+  if (PRE) {
+    if (tid < kCK) s_ss[0][tid] = pre_n[tid];
+    __syncthreads();
+  }
 
   for (int c0 = 0; c0 < g.Cin; c0 += kCK) {
+    const int sbuf = (c0 / kCK) & 1;
     // 1. patch registers -> LDS
 #pragma unroll
     for (int e = 0; e < kPatchPerThread; ++e) {
@@ -182,7 +196,12 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
       const int rr = i - c * (kPR * kPC);
       const int py = rr / kPC, px = rr - py * kPC;
       const int dst = i < kCK * kPR * kPC ? (c * kPR + py) * kPCp + px : kCK * kPR * kPCp + tid;
-      s_patch_raw[dst] = ((pmask >> e) & 1u) ? pv[e] : 0.f;
+      float v = pv[e];
+      if (PRE) {
+        const float2 st = s_ss[sbuf][min(c, kCK - 1)];
+        v = silu_f(v * st.x + st.y);
+      }
+      s_patch_raw[dst] = ((pmask >> e) & 1u) ? v : 0.f;
     }
     __syncthreads();
     // 2. V = B^T d B for one (cin, tile) per thread -> s_v[(c * 32 + m) * kVS + pos]
@@ -212,6 +231,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
     // (unconditional: the last chunk re-loads itself, so every iteration issues the same
     // loads and the compiler's vmcnt bookkeeping across the back edge stays exact)
     load_patch(min(c0 + kCK, g.Cin - kCK));
+    if (PRE && tid < kCK) ss_next = pre_n[min(c0 + kCK, g.Cin - kCK) + tid];
     // 4. MFMAs: acc[p][mb][nb] += V_p[mb*16 + i][4ks + k] * U_p[4ks + k][16nb + j]
     // A operands (16 positions of one (ks, mb) group = 4 x 16 B) are read one group
     // ahead, so each group's LDS latency hides behind the previous group's MFMAs.
@@ -250,6 +270,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
       }
     }
     load_u(min(c0 + kCK, g.Cin - kCK));
+    if (PRE && tid < kCK) s_ss[sbuf ^ 1][tid] = ss_next;
     __syncthreads();
   }
 
@@ -319,9 +340,9 @@ extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W
          W % kOutCols == 0;
 }
 
-extern "C" int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,
-                                             const float* skip, float div, float* y, int N,
-                                             int Cin, int Cout, int H, int W, void* stream) {
+extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U,
+                                        const float* bias, const float* skip, float div, float* y,
+                                        int N, int Cin, int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
               "Cout %% 64, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
@@ -336,17 +357,29 @@ extern "C" int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, con
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
-  if (nb == 2)
-    hipLaunchKernelGGL(wino_f23_kernel<2>, dim3((unsigned)blocks), dim3(256), 0,
-                       bpk::as_stream(stream), x, U, bias, skip, y, g, remap);
-  else
-    hipLaunchKernelGGL(wino_f23_kernel<1>, dim3((unsigned)blocks), dim3(256), 0,
-                       bpk::as_stream(stream), x, U, bias, skip, y, g, remap);
+  const float2* pre2 = reinterpret_cast<const float2*>(pre);
+  hipStream_t st = bpk::as_stream(stream);
+#define WINO_LAUNCH(NB_, PRE_)                                                                 \
+  hipLaunchKernelGGL((wino_f23_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, x, \
+                     U, bias, skip, pre2, y, g, remap)
+  if (nb == 2) {
+    if (pre) WINO_LAUNCH(2, true); else WINO_LAUNCH(2, false);
+  } else {
+    if (pre) WINO_LAUNCH(1, true); else WINO_LAUNCH(1, false);
+  }
+#undef WINO_LAUNCH
   BPK_LAUNCH_CHECK("conv3x3_wino");
   return BPK_OK;
 }
 
+extern "C" int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,
+                                             const float* skip, float div, float* y, int N,
+                                             int Cin, int Cout, int H, int W, void* stream) {
+  return bpk_conv3x3_wino_pre_f32(x, nullptr, U, bias, skip, div, y, N, Cin, Cout, H, W, stream);
+}
+
 extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y,
                                     int N, int Cin, int Cout, int H, int W, void* stream) {
-  return bpk_conv3x3_wino_residual_f32(x, U, bias, nullptr, 1.0f, y, N, Cin, Cout, H, W, stream);
+  return bpk_conv3x3_wino_pre_f32(x, nullptr, U, bias, nullptr, 1.0f, y, N, Cin, Cout, H, W,
+                                  stream);
 }

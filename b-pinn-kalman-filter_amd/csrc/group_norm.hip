@@ -255,6 +255,35 @@ __global__ __launch_bounds__(256) void gn_fwd_apply(const float* __restrict__ x,
   }
 }
 
+// per-(n, c) affine form of act(GroupNorm(x + bias_nc)): act(x * s + t) with
+// s = rstd * gamma[c], t = beta[c] + (bias_nc[n, c] - mean) * s -- consumed by the
+// Winograd conv's patch load so the normalized tensor never round-trips HBM
+__global__ __launch_bounds__(64) void gn_affine_kernel(const float* __restrict__ part,
+                                                       const float* __restrict__ bias_nc,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta,
+                                                       float2* __restrict__ ss, int C, int G,
+                                                       int splits, float eps) {
+  __shared__ float s_stat[2];
+  const int ng = blockIdx.x;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  if (threadIdx.x == 0) {
+    float mean, m2, count;
+    combine_partials(part + (int64_t)ng * splits * 3, splits, mean, m2, count);
+    s_stat[0] = mean;
+    s_stat[1] = 1.f / sqrtf(m2 / count + eps);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < cpg; j += blockDim.x) {
+    const int c = g * cpg + j;
+    const float sc = s_stat[1] * (gamma ? gamma[c] : 1.f);
+    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+    ss[(int64_t)n * C + c] = make_float2(sc, (beta ? beta[c] : 0.f) + (b - s_stat[0]) * sc);
+  }
+}
+
 // ---------------------------------------------------------------- backward
 
 template <int T, int VPT, int W>
@@ -601,5 +630,32 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
                        rstd, part, dx, C, (int)HW, G, p.splits, p.chunk, act);
   }
   BPK_LAUNCH_CHECK("group_norm_bwd_apply");
+  return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float* gamma,
+                                         const float* beta, float* scale_shift, void* workspace,
+                                         int N, int C, int64_t HW, int G, float eps,
+                                         void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && G > 0, "group_norm_affine: bad shape");
+  BPK_REQUIRE(C % G == 0, "group_norm_affine: C (%d) not divisible by G (%d)", C, G);
+  BPK_REQUIRE(workspace != nullptr, "group_norm_affine: workspace required");
+  if (N == 0) return BPK_OK;
+  const int64_t S = (int64_t)(C / G) * HW;
+  BPK_REQUIRE(S < (1ll << 31), "group_norm_affine: slab too large");
+  hipStream_t st = bpk::as_stream(stream);
+  const Plan p = make_plan(S, HW, is_aligned16(x), 0);
+  float* part = static_cast<float*>(workspace);
+  dim3 grid(p.splits, N * G);
+  if (p.W == 4)
+    hipLaunchKernelGGL((gn_fwd_partial<256, 16, 4>), grid, dim3(256), 0, st, x, bias_nc, part, C,
+                       (int)HW, G, p.splits);
+  else
+    hipLaunchKernelGGL((gn_fwd_partial<256, 16, 1>), grid, dim3(256), 0, st, x, bias_nc, part, C,
+                       (int)HW, G, p.splits);
+  BPK_LAUNCH_CHECK("group_norm_affine(partial)");
+  hipLaunchKernelGGL(gn_affine_kernel, dim3(N * G), dim3(64), 0, st, part, bias_nc, gamma, beta,
+                     reinterpret_cast<float2*>(scale_shift), C, G, p.splits, eps);
+  BPK_LAUNCH_CHECK("group_norm_affine");
   return BPK_OK;
 }

@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from op import conv as conv_op
-from op.norm_act import ACT_NONE, ACT_SILU, group_norm_act, residual_rescale
+from op.norm_act import ACT_NONE, ACT_SILU, group_norm_act, group_norm_affine, residual_rescale
 
 
 def get_act(config):
@@ -88,6 +88,27 @@ def conv2d(x, conv: nn.Conv2d, bias=True):
     if _wino_eligible(x, conv):
         return conv_op.conv3x3(x, conv.weight, b)
     return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def fused_inference_ok(module: nn.Module, x, act) -> bool:
+    """True when a block may take the inference-only fused paths (GroupNorm + SiLU applied
+    inside the Winograd conv's input load): eval mode (dropout is the identity), SiLU, and no
+    autograd graph to record."""
+    if module.training or not isinstance(act, nn.SiLU) or not _WINO_ENABLED:
+        return False
+    return not (torch.is_grad_enabled() and (x.requires_grad or any(
+        p.requires_grad for p in module.parameters())))
+
+
+def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=None,
+                 skip=None, div=1.0):
+    """conv(SiLU(GroupNorm(x + bias_nc))) [+ residual tail] in two launches -- the GroupNorm
+    statistics pass and the Winograd conv whose patch load applies the normalization -- or
+    None when the conv does not qualify."""
+    if not _wino_eligible(x, conv) or (skip is not None and skip.shape[1] != conv.out_channels):
+        return None
+    ss = group_norm_affine(x, gn, bias_nc)
+    return conv_op.conv3x3(x, conv.weight, conv_bias, skip=skip, div=div, pre=ss)
 
 
 def conv_residual(h, conv: nn.Conv2d, bias, skip, div):

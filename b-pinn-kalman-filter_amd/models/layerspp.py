@@ -211,20 +211,31 @@ class ResnetBlockBigGANpp(nn.Module):
         return t
 
     def forward(self, x, temb=None):
-        h = gn_act(x, self.GroupNorm_0, self.act)
-        h = self._resample(h)
-        x = self._resample(x)
-        h = conv_nobias(h, self.Conv_0)
+        fused = layers.fused_inference_ok(self, x, self.act)
+        h = None
+        if fused and not (self.up or self.down):
+            # GroupNorm_0 + SiLU applied inside Conv_0's input load (inference)
+            h = layers.gn_silu_conv(x, self.GroupNorm_0, self.Conv_0)
+        if h is None:
+            h = gn_act(x, self.GroupNorm_0, self.act)
+            h = self._resample(h)
+            x = self._resample(x)
+            h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
         if temb is not None:
             bias_nc = bias_nc + self.Dense_0(self.act(temb))
-        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
-        h = self.Dropout_0(h)
         bias = self.Conv_1.bias
         if self.in_ch != self.out_ch or self.up or self.down:
             # the 1x1 skip conv's bias joins Conv_1's in the fused residual (no separate
             # full-tensor bias add after the GEMM)
             x = conv_nobias(x, self.Conv_2)
             bias = bias + self.Conv_2.bias
-        return layers.conv_residual(h, self.Conv_1, bias, x,
-                                    np.sqrt(2.) if self.skip_rescale else 1.0)
+        div = np.sqrt(2.) if self.skip_rescale else 1.0
+        if fused:
+            # GroupNorm_1 (+ time bias) + SiLU + Conv_1 + residual tail: two launches
+            out = layers.gn_silu_conv(h, self.GroupNorm_1, self.Conv_1, bias_nc, bias, x, div)
+            if out is not None:
+                return out
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        h = self.Dropout_0(h)
+        return layers.conv_residual(h, self.Conv_1, bias, x, div)

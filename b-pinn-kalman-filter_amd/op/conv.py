@@ -38,8 +38,9 @@ def filter_transform(weight):
     return U
 
 
-def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0):
-    """conv(x, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch)."""
+def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None):
+    """conv(a, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch),
+    where a = x, or silu(x * s + t) with pre[n, c] = (s, t) (GroupNorm+SiLU fused in)."""
     x = x.contiguous()
     N, C, H, W = x.shape
     Cout = weight.shape[0]
@@ -49,10 +50,13 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0):
     sk = None if skip is None else skip.detach().contiguous()
     if sk is not None and sk.shape != y.shape:
         raise RuntimeError(f"conv3x3: skip {tuple(sk.shape)} != output {tuple(y.shape)}")
-    check(lib.bpk_conv3x3_wino_residual_f32(
-        x.data_ptr(), U.data_ptr(), None if b is None else b.data_ptr(),
-        None if sk is None else sk.data_ptr(), float(div), y.data_ptr(), N, C, Cout, H, W,
-        stream_ptr(x.device)), "conv3x3_wino")
+    pr = None if pre is None else pre.contiguous()
+    if pr is not None and tuple(pr.shape) != (N, C, 2):
+        raise RuntimeError(f"conv3x3: pre must be [N, Cin, 2], got {tuple(pr.shape)}")
+    check(lib.bpk_conv3x3_wino_pre_f32(
+        x.data_ptr(), None if pr is None else pr.data_ptr(), U.data_ptr(),
+        None if b is None else b.data_ptr(), None if sk is None else sk.data_ptr(), float(div),
+        y.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)), "conv3x3_wino")
     return y
 
 
@@ -81,10 +85,17 @@ class _Conv3x3(torch.autograd.Function):
         return gx, gw, gb, gs, None
 
 
-def conv3x3(x, weight, bias=None, skip=None, div=1.0):
+def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None):
     """F.conv2d(x, weight, bias, padding=1), or the residual-block tail
-    (skip + conv2d(x, weight, bias)) / div fused into the same launch."""
-    require_hip(x, weight, bias, skip, what="conv3x3")
+    (skip + conv2d(x, weight, bias)) / div fused into the same launch.  With `pre`
+    ([N, Cin, 2] from op.norm_act.group_norm_affine) the convolved tensor is
+    silu(x * s + t) = act(GroupNorm(x + b)) -- inference only (no autograd)."""
+    require_hip(x, weight, bias, skip, pre, what="conv3x3")
     if not supported(x, weight):
         raise RuntimeError(f"conv3x3: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
+    if pre is not None:
+        if torch.is_grad_enabled() and any(t is not None and t.requires_grad
+                                           for t in (x, weight, bias, skip)):
+            raise RuntimeError("conv3x3(pre=...) is inference-only")
+        return conv3x3_fwd_raw(x, weight, bias, skip, div, pre)
     return _Conv3x3.apply(x, weight, bias, skip, div)

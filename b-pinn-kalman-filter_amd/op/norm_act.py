@@ -83,6 +83,29 @@ def group_norm_act_f(x, num_groups, weight, bias, eps, act=ACT_SILU, bias_nc=Non
     return _GroupNormAct.apply(x, bias_nc, weight, bias, num_groups, eps, act)
 
 
+def group_norm_affine(x, gn: torch.nn.GroupNorm, bias_nc=None):
+    """Per-(n, c) (scale, shift) [N, C, 2] with act(GN(x + bias_nc)) == act(x * s + t):
+    the statistics pass of GroupNorm alone (one read of x), for convolutions that apply the
+    normalization in their input load (op.conv.conv3x3(..., pre=)).  Inference only."""
+    require_hip(x, bias_nc, what="group_norm_affine")
+    x = x.contiguous()
+    N, C = x.shape[:2]
+    HW = x.numel() // max(N * C, 1)
+    G = gn.num_groups
+    ss = torch.empty((N, C, 2), device=x.device, dtype=torch.float32)
+    ws = _ws(N, C, HW, G, x.device)
+    bnc = bias_nc.contiguous() if bias_nc is not None else None
+    w = gn.weight if gn.affine else None
+    b = gn.bias if gn.affine else None
+    check(lib.bpk_group_norm_affine_f32(
+        x.data_ptr(), bnc.data_ptr() if bnc is not None else None,
+        w.detach().data_ptr() if w is not None else None,
+        b.detach().data_ptr() if b is not None else None, ss.data_ptr(),
+        ws.data_ptr() if ws is not None else None, N, C, HW, G, float(gn.eps),
+        stream_ptr(x.device)), "group_norm_affine")
+    return ss
+
+
 class _Residual(Function):
     @staticmethod
     def forward(ctx, x, h, bias, div):

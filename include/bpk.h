@@ -186,6 +186,14 @@ int64_t bpk_group_norm_workspace_bytes(int N, int C, int64_t HW, int G);
 int bpk_group_norm_fwd_f32(const float* x, const float* bias_nc, const float* gamma,
                            const float* beta, float* y, float* mean, float* rstd, void* workspace,
                            int N, int C, int64_t HW, int G, float eps, int act, void* stream);
+/* Statistics of GroupNorm(x + bias_nc) folded into a per-(n, c) affine form:
+ * scale_shift[n][c] = (s, t) with act(GN(x + b)) == act(x * s + t); s = rstd * gamma[c],
+ * t = beta[c] + (b[n, c] - mean) * s.  One read of x.  Consumed by the Winograd conv's
+ * fused prologue (bpk_conv3x3_wino_pre_f32) so the normalized tensor is never stored.
+ * workspace: bpk_group_norm_workspace_bytes(N, C, HW, G). */
+int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float* gamma,
+                              const float* beta, float* scale_shift, void* workspace, int N, int C,
+                              int64_t HW, int G, float eps, void* stream);
 int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
                            const float* gamma, const float* beta, const float* mean,
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,
@@ -296,6 +304,12 @@ int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, floa
 int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,
                                   const float* skip, float div, float* y, int N, int Cin,
                                   int Cout, int H, int W, void* stream);
+/* General form: the conv input is silu(x * s + t) with pre[n][cin] = (s, t) from
+ * bpk_group_norm_affine_f32 (pre NULL: x itself), i.e. GroupNorm + SiLU + conv (+ residual
+ * tail) in one launch without materialising the normalized tensor. */
+int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U, const float* bias,
+                             const float* skip, float div, float* y, int N, int Cin, int Cout,
+                             int H, int W, void* stream);
 
 #ifdef __cplusplus
 }

@@ -297,3 +297,23 @@ def test_conv3x3_winograd_fused_residual_tail(hip):
     g2 = torch.autograd.grad(plain, (h, w, b, x), go)
     for a, r in zip(g1, g2):
         assert (a - r).abs().max().item() <= 1e-5 * max(1.0, r.abs().max().item())
+
+
+def test_conv3x3_winograd_fused_groupnorm_silu_prologue(hip):
+    """conv3x3(x, pre=group_norm_affine(x, gn, b)) == conv3x3(SiLU(GroupNorm(x + b))) up to
+    fp32 rounding of the folded affine form (1e-5 relative), incl. the residual tail."""
+    from op.conv import conv3x3
+    from op.norm_act import ACT_SILU, group_norm_act, group_norm_affine
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(2, 128, 32, 32, generator=g) * 3 + 1).to(hip)
+    gn = torch.nn.GroupNorm(32, 128, eps=1e-6).to(hip)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(128, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(128, generator=g))
+        bnc = torch.randn(2, 128, generator=g).to(hip)
+        w = (torch.randn(64, 128, 3, 3, generator=g) * 0.03).to(hip)
+        b = torch.randn(64, generator=g).to(hip)
+        skip = torch.randn(2, 64, 32, 32, generator=g).to(hip)
+        ref = conv3x3(group_norm_act(x, gn, ACT_SILU, bnc), w, b, skip=skip, div=2 ** 0.5)
+        out = conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=group_norm_affine(x, gn, bnc))
+    assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
