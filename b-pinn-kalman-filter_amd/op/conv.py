@@ -77,7 +77,13 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[3]:
             gs = gy
         if ctx.needs_input_grad[0]:
-            gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+            # backward-data of a 3x3 / stride-1 / pad-1 conv is the forward conv of gy with
+            # the flipped, transposed filter: the Winograd kernel when the shape qualifies
+            wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
+            if not torch.is_grad_enabled() and supported(gy, wt):
+                gx = conv3x3_fwd_raw(gy, wt)
+            else:
+                gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
         if ctx.needs_input_grad[1]:
             gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:

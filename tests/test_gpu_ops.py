@@ -258,18 +258,21 @@ def test_conv3x3_winograd_matches_fp32_reference(hip, N, cin, cout, hw, with_bia
     assert (mi - ref).abs().max().item() <= 2e-5 * scale
 
 
-def test_conv3x3_winograd_backward_and_filter_cache(hip):
+@pytest.mark.parametrize("cin", [16, 64])
+def test_conv3x3_winograd_backward_and_filter_cache(hip, cin):
+    """gradients vs MIOpen's; cin = 64 takes the Winograd backward-data path (the forward
+    conv of gy with the flipped, transposed filter), cin = 16 the MIOpen fallback."""
     import torch.nn.functional as F
     from op.conv import conv3x3
     g = torch.Generator().manual_seed(1)
-    x = torch.randn(2, 16, 16, 32, generator=g).to(hip).requires_grad_()
-    w = (torch.randn(128, 16, 3, 3, generator=g) * 0.1).to(hip).requires_grad_()
+    x = torch.randn(2, cin, 16, 32, generator=g).to(hip).requires_grad_()
+    w = (torch.randn(128, cin, 3, 3, generator=g) * 0.1).to(hip).requires_grad_()
     b = torch.randn(128, generator=g).to(hip).requires_grad_()
     go = torch.randn(2, 128, 16, 32, generator=g).to(hip)
     gx, gw, gb = torch.autograd.grad(conv3x3(x, w, b), (x, w, b), go)
     rx, rw, rb = torch.autograd.grad(F.conv2d(x, w, b, padding=1), (x, w, b), go)
     for a, r in ((gx, rx), (gw, rw), (gb, rb)):
-        assert (a - r).abs().max().item() <= 1e-5 * r.abs().max().item()
+        assert (a - r).abs().max().item() <= 3e-5 * r.abs().max().item()
     # an in-place weight update invalidates the cached filter transform
     y0 = conv3x3(x.detach(), w.detach(), None)
     with torch.no_grad():
