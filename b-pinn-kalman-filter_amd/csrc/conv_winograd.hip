@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -82,6 +83,7 @@ struct WinoGeo {
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
 constexpr int kOS = kOutRows * kOutCols + 4;  // LDS stride of one staged output channel
 constexpr int kPatchPerThread = (kCK * kPR * kPC + 255) / 256;  // 6
+constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine table in LDS
 
 // NB = MFMA N-blocks (16 couts each) per wave: NB = 2 -> 256 accumulator registers, one
 // workgroup per CU; NB = 1 -> 128, two workgroups per CU whose phases interleave.
@@ -89,7 +91,7 @@ constexpr int kPatchPerThread = (kCK * kPR * kPC + 255) / 256;  // 6
 // pre[n][cin] = (s, t) (bpk_group_norm_affine_f32): the patch load applies silu(x s + t)
 // (zero padding stays zero), so the normalized tensor is never written to HBM.
 // fast exp / reciprocal: a few ulp, far inside the network tolerance (1e-4)
-__device__ inline float silu_f(float z) { return z * __frcp_rn(1.f + __expf(-z)); }
+__device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 
 template <int NB, bool PRE>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const float* __restrict__ x,
@@ -320,6 +322,265 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
   }
 }
 
+// Software-pipelined form (one workgroup per CU, 4 waves x 32 couts = 128 couts, 32 tiles).
+// The serial form above runs store-patch | barrier | transform | barrier | MFMAs per chunk,
+// so a wave's MFMA pipe idles through the transform phase unless a second workgroup
+// happens to be out of phase.  Here the work of three chunks overlaps inside each wave:
+// while the MFMAs of chunk k read V(k) from one LDS buffer, the same wave transforms
+// patch(k+1) (already in LDS) into the other V buffer, stores patch(k+2) (in registers)
+// into the free patch buffer and issues the global loads of patch(k+3) and of U(k+1) into
+// a second register set -- one barrier per chunk.  The VALU / LDS work (~70 instructions
+// per chunk) fills MFMA issue gaps (128 MFMAs of 32 cycles per chunk per wave).
+template <int NB, bool PRE>
+__global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
+    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
+    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
+    WinoGeo g, int xcd_remap) {
+  constexpr int kWN = 16 * NB;  // couts per wave
+  constexpr int kPatch = kCK * kPR * kPCp;
+  __shared__ float s_patch_raw[2][kPatch];                                  // 2 x 5.9 KB
+  // V double buffer; after the K loop the same LDS stages the output (NB x 33.8 KB)
+  constexpr int kVBuf = kCK * kM * kVS;                                      // 20.5 KB
+  constexpr int kOutLds = 4 * kWN * kOS;
+  __shared__ __attribute__((aligned(16))) float s_vo[2 * kVBuf > kOutLds ? 2 * kVBuf : kOutLds];
+  float(*s_v)[kVBuf] = reinterpret_cast<float(*)[kVBuf]>(s_vo);
+  float* s_out = s_vo;
+  __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];  // PRE: (s, t) of every input channel
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  int64_t nblk = (int64_t)gridDim.x;
+  int64_t b = blockIdx.x;
+  if (xcd_remap) b = (b % 8) * (nblk / 8) + b / 8;
+  const int cb = (int)(b % g.cout_blocks);
+  int64_t r = b / g.cout_blocks;
+  const int rx = (int)(r % g.regions_x);
+  r /= g.regions_x;
+  const int ry = (int)(r % g.regions_y);
+  const int n = (int)(r / g.regions_y);
+  const int oy0 = ry * kOutRows, ox0 = rx * kOutCols;
+  const int cout_w = cb * (4 * kWN) + wave * kWN;
+
+  f4 acc[16][2][NB];
+#pragma unroll
+  for (int p = 0; p < 16; ++p)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t plane = (int64_t)g.H * g.W;
+  const float* xn = x + (int64_t)n * g.Cin * plane;
+  const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
+  const int kq = lane >> 4, jj = lane & 15;
+  const int nch = g.Cin / kCK;
+
+  // Global loads go through buffer descriptors (base in SGPRs, 32-bit per-lane offsets,
+  // the chunk offset in soffset): no 64-bit address registers next to the accumulators.
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xn), 0, (int)(g.Cin * plane * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
+
+  // patch loads, position-major: thread t < 180 owns patch position (py, px) = (t / 18,
+  // t % 18) for all 8 channels of a chunk (one in-plane offset, one LDS slot, one
+  // in-image bit per thread; the channel stride goes into soffset / the LDS immediate).
+  // Threads >= 180 duplicate thread 0 (same loads, same values to the same LDS words), so
+  // every lane runs the same branch-free code.
+  constexpr int kPos = kPR * kPC;  // 180
+  int poff, pdst;
+  bool pin;
+  {
+    const int t = tid < kPos ? tid : 0;
+    const int py = t / kPC, px = t - py * kPC;
+    const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+    pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+    const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
+    poff = (cy * g.W + cx) * 4;
+    pdst = py * kPCp + px;
+  }
+  if (PRE) {
+    for (int c = tid; c < g.Cin; c += 256) s_ss[c] = pre_n[c];
+    __syncthreads();
+  }
+  float pv[kCK];
+  auto load_patch = [&](int k) {
+    const int soff = (min(k, nch - 1) * kCK) * (int)plane * 4;
+#pragma unroll
+    for (int c = 0; c < kCK; ++c)
+      pv[c] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(xrs, poff, soff + c * (int)plane * 4, 0));
+  };
+  auto store_patch = [&](float* sp, int k) {
+    const int c0 = min(k, nch - 1) * kCK;
+#pragma unroll
+    for (int c = 0; c < kCK; ++c) {
+      float v = pv[c];
+      if (PRE) {
+        const float2 st = s_ss[c0 + c];
+        v = silu_f(v * st.x + st.y);
+      }
+      sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
+    }
+  };
+  // B operands of one k-step half: uo[ks][nb][q] = U[c0 + 4ks + kq][cout_w + 16nb + jj][4q..]
+  f4 uo[2][NB][4];
+  const int uoff = ((kq * g.Cout + cout_w + jj) * 16) * 4;
+  auto load_u = [&](int ks, int k) {
+    const int soff = ((min(k, nch - 1) * kCK + 4 * ks) * g.Cout) * 64;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        using u4 = __attribute__((ext_vector_type(4))) unsigned;
+        const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + nb * 1024 + q * 16, soff, 0);
+        uo[ks][nb][q] = __builtin_bit_cast(f4, w);
+      }
+  };
+  // V = B^T d B of one (cin, tile) per thread
+  const int tc = tid >> 5, tm = tid & 31;
+  const int tty = tm / kTC, ttx = tm - tty * kTC;
+  float d[4][4];
+  auto read_d = [&](const float* sp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[i][j] = sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j];
+  };
+  auto write_v = [&](float* sv) {
+    float t[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[0][j] = d[0][j] - d[2][j];
+      t[1][j] = d[1][j] + d[2][j];
+      t[2][j] = d[2][j] - d[1][j];
+      t[3][j] = d[1][j] - d[3][j];
+    }
+    f4* dst = reinterpret_cast<f4*>(&sv[(tc * kM + tm) * kVS]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
+  };
+
+  // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight
+  load_patch(0);
+  store_patch(s_patch_raw[0], 0);
+  load_patch(1);
+  store_patch(s_patch_raw[1], 1);
+  load_patch(2);
+  load_u(0, 0);
+  load_u(1, 0);
+  __syncthreads();
+  read_d(s_patch_raw[0]);
+  write_v(s_v[0]);
+  __syncthreads();
+
+  // A operands a[q] = V[pos 4q..4q+3] of (ks, mb) = this lane's tile row of one LDS record;
+  // each a[q] / uo[ks][nb][q] register is refilled (next group's A, next chunk's U) right
+  // after the last MFMA that reads it, so A needs 16 registers and U 64, and every load
+  // has most of a group (>= 24 MFMAs) to land
+  f4 a[4];
+  auto a_src = [&](const float* sv, int grp) {  // grp = 2 ks + mb
+    const int ks = grp >> 1, mb = grp & 1;
+    return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
+  };
+  {
+    const f4* src = a_src(s_v[0], 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = src[q];
+  }
+  auto step = [&](int k, auto sb_c) {
+    constexpr int SB = decltype(sb_c)::value;
+    const float* sv = s_v[SB];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      const int ks = grp >> 1, mb = grp & 1;
+      // side work of the next chunks, spread over the four MFMA groups
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                // patch(k+1)
+      if (grp == 1) write_v(s_v[SB ^ 1]);                       // V(k+1)
+      if (grp == 2) store_patch(s_patch_raw[SB], k + 2);        // patch(k+2)
+      if (grp == 3) load_patch(k + 3);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[4 * q + pp][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                a[q][pp], uo[ks][nb][q][pp], acc[4 * q + pp][mb][nb], 0, 0, 0);
+        // refill: A of the next group (the next chunk's group 0 comes after the barrier)
+        if (grp < 3) a[q] = a_src(sv, grp + 1)[q];
+        if (mb == 1) {
+          const int soff = ((min(k + 1, nch - 1) * kCK + 4 * ks) * g.Cout) * 64;
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            using u4 = __attribute__((ext_vector_type(4))) unsigned;
+            const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + nb * 1024 + q * 16,
+                                                               soff, 0);
+            uo[ks][nb][q] = __builtin_bit_cast(f4, w);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const f4* src = a_src(s_v[SB ^ 1], 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = src[q];
+    }
+  };
+  int k = 0;
+  for (; k + 1 < nch; k += 2) {
+    step(k, std::integral_constant<int, 0>{});
+    step(k + 1, std::integral_constant<int, 1>{});
+  }
+  if (k < nch) step(k, std::integral_constant<int, 0>{});
+
+  // output transform (lane-local) -> per-wave LDS staging [cout][8 x 16 pixels]
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    float* so = &s_out[(wave * kWN + 16 * nb + jj) * kOS];
+    const float bv = bias ? bias[cout_w + 16 * nb + jj] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int m = mb * 16 + 4 * kq + rg;
+        const int ty = m / kTC, tx = m - ty * kTC;
+        float t0[4], t1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          t0[j] = acc[j][mb][nb][rg] + acc[4 + j][mb][nb][rg] + acc[8 + j][mb][nb][rg];
+          t1[j] = acc[4 + j][mb][nb][rg] - acc[8 + j][mb][nb][rg] - acc[12 + j][mb][nb][rg];
+        }
+        so[(2 * ty) * kOutCols + 2 * tx] = t0[0] + t0[1] + t0[2] + bv;
+        so[(2 * ty) * kOutCols + 2 * tx + 1] = t0[1] - t0[2] - t0[3] + bv;
+        so[(2 * ty + 1) * kOutCols + 2 * tx] = t1[0] + t1[1] + t1[2] + bv;
+        so[(2 * ty + 1) * kOutCols + 2 * tx + 1] = t1[1] - t1[2] - t1[3] + bv;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kWN / 2; ++it) {
+    const int q = it * 64 + lane;
+    const int co = q >> 5;
+    const int rem = q & 31;
+    const int row = rem >> 2, c4 = rem & 3;
+    f4 v = *reinterpret_cast<const f4*>(&s_out[(wave * kWN + co) * kOS + row * kOutCols + 4 * c4]);
+    const int64_t o = (int64_t)n * g.Cout * plane + (int64_t)(cout_w + co) * plane +
+                      (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
+    if (skip) {
+      const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+      v = f4{(sk[0] + v[0]) / g.div, (sk[1] + v[1]) / g.div, (sk[2] + v[2]) / g.div,
+             (sk[3] + v[3]) / g.div};
+    }
+    *reinterpret_cast<f4*>(&y[o]) = v;
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
@@ -353,6 +614,32 @@ extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const 
     const char* e = getenv("BPK_WINO_NB");
     return e ? atoi(e) : 1;
   }();
+  // the software-pipelined kernel (128 couts per workgroup) unless BPK_WINO_PIPE=0
+  static const int pipe_env = [] {
+    const char* e = getenv("BPK_WINO_PIPE");
+    return e ? atoi(e) : 0;
+  }();
+  if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
+    // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup
+    const int pnb = (pipe_env == 2 && Cout % 128 == 0) ? 2 : 1;
+    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * pnb), div};
+    const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
+    BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
+    const int remap = (blocks % 8 == 0) ? 1 : 0;
+    const float2* pre2 = reinterpret_cast<const float2*>(pre);
+    hipStream_t st = bpk::as_stream(stream);
+#define WINO_PIPE(NB_, PRE_)                                                                  \
+  hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, \
+                     x, U, bias, skip, pre2, y, g, remap)
+    if (pnb == 2) {
+      if (pre) WINO_PIPE(2, true); else WINO_PIPE(2, false);
+    } else {
+      if (pre) WINO_PIPE(1, true); else WINO_PIPE(1, false);
+    }
+#undef WINO_PIPE
+    BPK_LAUNCH_CHECK("conv3x3_wino_pipe");
+    return BPK_OK;
+  }
   const int nb = (Cout % 128 == 0 && nb_env == 2) ? 2 : 1;
   WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div};
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;

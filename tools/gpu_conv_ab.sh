@@ -1,0 +1,11 @@
+#!/bin/bash
+# Winograd conv A/B: the software-pipelined kernel (default) vs the serial one, then the
+# conv parity tests.  Each GPU step has its own time limit; stop at the first failure.
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+BPK_WINO_PIPE=1 timeout -k 10 300 python tools/bench_conv.py > gpurun_out/conv_pipe.log 2>&1 || { cat gpurun_out/conv_pipe.log; exit 1; }
+cat gpurun_out/conv_pipe.log
+BPK_WINO_PIPE=0 timeout -k 10 300 python tools/bench_conv.py > gpurun_out/conv_serial.log 2>&1 || exit 1
+cat gpurun_out/conv_serial.log
+BPK_WINO_PIPE=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -k "conv3x3" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_conv.log 2>&1
+rc=$?; tail -5 gpurun_out/pytest_conv.log; exit $rc
