@@ -1,13 +1,18 @@
 """3x3 convolution on the fused Winograd F(2x2,3x3) MFMA kernel (csrc/conv_winograd.hip).
 
 `conv3x3(x, weight, bias=None)` == F.conv2d(x, weight, bias, stride=1, padding=1) for
-fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`); the backward
-(input and weight gradients) runs on MIOpen through torch.nn.grad.  The filter transform
-U = G w G^T is cached on the weight tensor itself (keyed by its version counter, which
+fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`).  Backward: the
+input gradient is the same Winograd forward kernel on the flipped, transposed filter and
+the weight gradient the Winograd split-K kernel (csrc/conv_winograd_wgrad.hip) when the
+shapes qualify, MIOpen through torch.nn.grad otherwise (and for double backward).
+BPK_WINO_WGRAD=0 routes the weight gradient to MIOpen (A/B measurements).  The filter
+transform U = G w G^T is cached on the weight tensor itself (keyed by its version counter, which
 every in-place update such as an optimizer step bumps), so a sampler that never changes
 its weights transforms each filter once.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -60,6 +65,37 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None):
     return y
 
 
+_WGRAD = os.environ.get("BPK_WINO_WGRAD", "1") != "0"
+
+
+def wgrad_supported(x, weight):
+    if not _WGRAD:
+        return False
+    if x.dtype != torch.float32 or x.dim() != 4 or not x.is_cuda:
+        return False
+    N, C, H, W = x.shape
+    return bool(lib.bpk_conv3x3_wino_wgrad_supported(N, C, weight.shape[0], H, W))
+
+
+def conv3x3_wgrad_raw(x, gy, wshape):
+    """dw [Cout, Cin, 3, 3] of conv3x3(x, w) for the output gradient gy (Winograd split-K,
+    csrc/conv_winograd_wgrad.hip); == torch.nn.grad.conv2d_weight(x, wshape, gy, padding=1)."""
+    x = x.detach().contiguous()
+    gy = gy.detach().contiguous()
+    N, C, H, W = x.shape
+    Cout = wshape[0]
+    if tuple(gy.shape) != (N, Cout, H, W) or tuple(wshape[1:]) != (C, 3, 3):
+        raise RuntimeError(f"conv3x3_wgrad: x {tuple(x.shape)}, gy {tuple(gy.shape)}, "
+                           f"w {tuple(wshape)}")
+    nbytes = lib.bpk_conv3x3_wino_wgrad_workspace_bytes(N, C, Cout, H, W)
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
+    dw = torch.empty((Cout, C, 3, 3), dtype=torch.float32, device=x.device)
+    check(lib.bpk_conv3x3_wino_wgrad_f32(x.data_ptr(), gy.data_ptr(), dw.data_ptr(),
+                                         ws.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)),
+          "conv3x3_wgrad")
+    return dw
+
+
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, skip, div):
@@ -85,7 +121,10 @@ class _Conv3x3(torch.autograd.Function):
             else:
                 gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
         if ctx.needs_input_grad[1]:
-            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
+            if not torch.is_grad_enabled() and wgrad_supported(x, weight):
+                gw = conv3x3_wgrad_raw(x, gy, weight.shape)
+            else:
+                gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum((0, 2, 3))
         return gx, gw, gb, gs, None

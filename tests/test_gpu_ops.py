@@ -281,6 +281,31 @@ def test_conv3x3_winograd_backward_and_filter_cache(hip, cin):
     assert torch.allclose(y1, 2 * y0, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("N,cin,cout,h,w", [(1, 32, 64, 2, 16), (2, 64, 128, 16, 32),
+                                             (3, 96, 64, 10, 48), (2, 256, 128, 32, 32)])
+def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
+    """Winograd split-K weight gradient vs a float64 direct computation (and MIOpen's fp32
+    backward-weights held to the same bound): 2e-5 relative to max|ref|.  Shapes cover one
+    K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3_wgrad_raw, wgrad_supported
+    g = torch.Generator().manual_seed(N * 100 + cin + h)
+    x = torch.randn(N, cin, h, w, generator=g)
+    gy = torch.randn(N, cout, h, w, generator=g)
+    wt = torch.empty(cout, cin, 3, 3)
+    assert wgrad_supported(x.to(hip), wt)
+    ref = torch.nn.grad.conv2d_weight(x.double(), wt.shape, gy.double(), padding=1)
+    out = conv3x3_wgrad_raw(x.to(hip), gy.to(hip), wt.shape).double().cpu()
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() <= 2e-5 * scale
+    mi = torch.nn.grad.conv2d_weight(x.to(hip), wt.shape, gy.to(hip), padding=1).double().cpu()
+    assert (mi - ref).abs().max().item() <= 2e-5 * scale
+    # deterministic: the same inputs give the same bits
+    again = conv3x3_wgrad_raw(x.to(hip), gy.to(hip), wt.shape).double().cpu()
+    assert torch.equal(out, again)
+    del F
+
+
 def test_conv3x3_winograd_fused_residual_tail(hip):
     """conv3x3(h, w, b, skip=x, div) == residual_rescale(x, conv3x3(h, w), b, div) bit for bit
     (same epilogue arithmetic), and its gradients match the unfused composition."""
