@@ -5,7 +5,7 @@ fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`).  Backw
 input gradient is the same Winograd forward kernel on the flipped, transposed filter and
 the weight gradient the Winograd split-K kernel (csrc/conv_winograd_wgrad.hip) when the
 shapes qualify, MIOpen through torch.nn.grad otherwise (and for double backward).
-BPK_WINO_WGRAD=0 routes the weight gradient to MIOpen (A/B measurements).  The filter
+BPK_WINO_WGRAD=1 selects the Winograd weight gradient (opt-in while being measured).  The filter
 transform U = G w G^T is cached on the weight tensor itself (keyed by its version counter, which
 every in-place update such as an optimizer step bumps), so a sampler that never changes
 its weights transforms each filter once.
@@ -65,7 +65,7 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None):
     return y
 
 
-_WGRAD = os.environ.get("BPK_WINO_WGRAD", "1") != "0"
+_WGRAD = os.environ.get("BPK_WINO_WGRAD", "0") != "0"  # opt-in until measured on the GPU
 
 
 def wgrad_supported(x, weight):

@@ -288,12 +288,13 @@ def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
     backward-weights held to the same bound): 2e-5 relative to max|ref|.  Shapes cover one
     K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths."""
     import torch.nn.functional as F
-    from op.conv import conv3x3_wgrad_raw, wgrad_supported
+    from op import conv as conv_mod
+    from op.conv import conv3x3_wgrad_raw
     g = torch.Generator().manual_seed(N * 100 + cin + h)
     x = torch.randn(N, cin, h, w, generator=g)
     gy = torch.randn(N, cout, h, w, generator=g)
     wt = torch.empty(cout, cin, 3, 3)
-    assert wgrad_supported(x.to(hip), wt)
+    assert conv_mod.lib.bpk_conv3x3_wino_wgrad_supported(N, cin, cout, h, w)
     ref = torch.nn.grad.conv2d_weight(x.double(), wt.shape, gy.double(), padding=1)
     out = conv3x3_wgrad_raw(x.to(hip), gy.to(hip), wt.shape).double().cpu()
     scale = ref.abs().max().item()
