@@ -617,7 +617,7 @@ extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const 
   // the software-pipelined kernel (128 couts per workgroup) unless BPK_WINO_PIPE=0
   static const int pipe_env = [] {
     const char* e = getenv("BPK_WINO_PIPE");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
     // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup

@@ -5,7 +5,8 @@ fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`).  Backw
 input gradient is the same Winograd forward kernel on the flipped, transposed filter and
 the weight gradient the Winograd split-K kernel (csrc/conv_winograd_wgrad.hip) when the
 shapes qualify, MIOpen through torch.nn.grad otherwise (and for double backward).
-BPK_WINO_WGRAD=1 selects the Winograd weight gradient (opt-in while being measured).  The filter
+BPK_WINO_WGRAD=0 falls back to MIOpen for the weight gradient (Winograd: 2.42 vs 2.83 ms on
+128->128 @128^2, B=64; 1.1-1.2x on every NCSN++ shape, profiles/r01_conv_ab.txt).  The filter
 transform U = G w G^T is cached on the weight tensor itself (keyed by its version counter, which
 every in-place update such as an optimizer step bumps), so a sampler that never changes
 its weights transforms each filter once.
@@ -65,7 +66,7 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None):
     return y
 
 
-_WGRAD = os.environ.get("BPK_WINO_WGRAD", "0") != "0"  # opt-in until measured on the GPU
+_WGRAD = os.environ.get("BPK_WINO_WGRAD", "1") != "0"
 
 
 def wgrad_supported(x, weight):

@@ -290,12 +290,31 @@ def bench_dps(args, ctx, dev):
             "dps_config": "configs[4]: nc_ddpmpp_inpaint_dps @256x256 (ddpm net), B=16/GPU, RK45"}
 
 
+_PHASE = ["start"]
+
+
 def log(msg):
+    _PHASE[0] = msg
     print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
+def _heartbeat(period=45.0):
+    """A line on stderr every `period` s while a phase runs (first-use MIOpen kernel
+    compilation can keep a phase silent for minutes on a fresh box)."""
+    import threading
+
+    def run():
+        t0 = time.time()
+        while True:
+            time.sleep(period)
+            print(f"[bench] {time.strftime('%H:%M:%S')} ... ({_PHASE[0]}; {time.time() - t0:.0f}s)",
+                  file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
 
 
 def main():
     args = parse()
+    _heartbeat()
     import dist
     import sampling
     import sde_lib
