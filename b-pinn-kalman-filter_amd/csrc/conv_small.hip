@@ -1,0 +1,215 @@
+// 3x3 / stride 1 / pad 1 fp32 convolution for a small channel count on one side, on the
+// VALU (gfx950).
+//
+// NCSN++ / DDPM++ have per score evaluation one conv with Cin = 1 (conv_in: image -> nf
+// channels, models/ncsnpp.py conv_in) and, with progressive = 'output_skip', one conv with
+// Cout = 1 per resolution (the pyramid heads: GroupNorm -> SiLU -> conv3x3(C -> 1)).  Neither
+// is GEMM-shaped (one GEMM dimension is 1): the work is 9 * Cin * Cout FMAs per pixel against
+// one full read (Cout small) or one full write (Cin small) of a [B, C, H, W] tensor, so both
+// are HBM-bound.  (MIOpen runs them as Winograd at ~1 ms each for B = 64 @ 128^2, 10-15x the
+// byte time.)
+//
+//   * small_cout_kernel<COUT>: a workgroup owns a 16 x 64 output tile of one image; the
+//     18 x 66 input patch of 4 channels at a time is staged in LDS (GroupNorm affine + SiLU
+//     applied on the way in when `pre` is given; the zero padding stays zero), every thread
+//     accumulates a 1 x 4 pixel strip for all COUT outputs from a 3 x 6 register window;
+//     weights are workgroup-uniform (scalar loads).
+//   * small_cin_kernel<CIN>: the CIN x 18 x 66 patch is loaded once, each thread keeps its
+//     3 x 6 x CIN window in registers and loops over the output channels, storing one
+//     16-byte strip per channel (coalesced rows of the output planes).
+// Backward-data of one form is the other form with the flipped, transposed filter
+// (op/conv.py), so training and the DPS input gradient use the same two kernels.
+#include "bpk_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int kTH = 16, kTW = 64;         // output tile
+constexpr int kPH = kTH + 2, kPW = kTW + 2;  // 18 x 66 input patch
+constexpr int kPWp = kPW + 1;             // padded LDS row
+constexpr int kCK = 4;                    // input channels per LDS chunk (small-Cout form)
+
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+
+struct SmallGeo {
+  int N, Cin, Cout, H, W, tiles_x, tiles_y;
+};
+
+// stage channels [c0, c0 + nc) of image n into s[c][row][col] (zero outside the image)
+template <bool PRE>
+__device__ inline void stage_patch(float* s, const float* __restrict__ xn,
+                                   const float2* __restrict__ pre_n, int c0, int nc, int oy0,
+                                   int ox0, const SmallGeo& g) {
+  const int64_t plane = (int64_t)g.H * g.W;
+  const int total = nc * kPH * kPW;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int c = i / (kPH * kPW);
+    const int r = i - c * (kPH * kPW);
+    const int py = r / kPW, px = r - py * kPW;
+    const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+    float v = 0.f;
+    if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) {
+      v = xn[(int64_t)(c0 + c) * plane + (int64_t)iy * g.W + ix];
+      if (PRE) {
+        const float2 st = pre_n[c0 + c];
+        v = silu_f(v * st.x + st.y);
+      }
+    }
+    s[(c * kPH + py) * kPWp + px] = v;
+  }
+}
+
+template <int COUT, bool PRE>
+__global__ __launch_bounds__(256) void small_cout_kernel(const float* __restrict__ x,
+                                                         const float2* __restrict__ pre,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ y, SmallGeo g) {
+  __shared__ float s_patch[kCK * kPH * kPWp];  // 19.3 KB
+  const int tile = blockIdx.x;
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int n = tile / (g.tiles_x * g.tiles_y);
+  const int oy0 = ty * kTH, ox0 = tx * kTW;
+  const int lr = threadIdx.x >> 4, lc = (threadIdx.x & 15) * 4;  // strip (lr, lc..lc+3)
+  const int64_t plane = (int64_t)g.H * g.W;
+  const float* xn = x + (int64_t)n * g.Cin * plane;
+  const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
+
+  float acc[COUT][4];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[co][j] = 0.f;
+
+  for (int c0 = 0; c0 < g.Cin; c0 += kCK) {
+    const int nc = min(kCK, g.Cin - c0);
+    __syncthreads();
+    stage_patch<PRE>(s_patch, xn, pre_n, c0, nc, oy0, ox0, g);
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+      float win[3][6];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) win[r][j] = s_patch[(c * kPH + lr + r) * kPWp + lc + j];
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        const float* wk = w + ((int64_t)co * g.Cin + c0 + c) * 9;  // uniform
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            const float wv = wk[r * 3 + s];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[co][j] = fmaf(win[r][j + s], wv, acc[co][j]);
+          }
+      }
+    }
+  }
+  const int oy = oy0 + lr, ox = ox0 + lc;
+  if (oy < g.H && ox < g.W) {  // W % 4 == 0: a strip is all in or all out
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      const float b = bias ? bias[co] : 0.f;
+      *reinterpret_cast<f4*>(&y[((int64_t)n * g.Cout + co) * plane + (int64_t)oy * g.W + ox]) =
+          f4{acc[co][0] + b, acc[co][1] + b, acc[co][2] + b, acc[co][3] + b};
+    }
+  }
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256) void small_cin_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ y, SmallGeo g) {
+  __shared__ float s_patch[CIN * kPH * kPWp];
+  const int tile = blockIdx.x;
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int n = tile / (g.tiles_x * g.tiles_y);
+  const int oy0 = ty * kTH, ox0 = tx * kTW;
+  const int lr = threadIdx.x >> 4, lc = (threadIdx.x & 15) * 4;
+  const int64_t plane = (int64_t)g.H * g.W;
+  stage_patch<false>(s_patch, x + (int64_t)n * CIN * plane, nullptr, 0, CIN, oy0, ox0, g);
+  __syncthreads();
+  float win[CIN][3][6];
+#pragma unroll
+  for (int c = 0; c < CIN; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) win[c][r][j] = s_patch[(c * kPH + lr + r) * kPWp + lc + j];
+  const int oy = oy0 + lr, ox = ox0 + lc;
+  if (oy >= g.H || ox >= g.W) return;  // no barrier below
+  float* yo = y + (int64_t)n * g.Cout * plane + (int64_t)oy * g.W + ox;
+  for (int co = 0; co < g.Cout; ++co) {
+    const float b = bias ? bias[co] : 0.f;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < CIN; ++c) {
+      const float* wk = w + ((int64_t)co * CIN + c) * 9;  // uniform
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const float wv = wk[r * 3 + s];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = fmaf(win[c][r][j + s], wv, a[j]);
+        }
+    }
+    *reinterpret_cast<f4*>(&yo[(int64_t)co * plane]) = f4{a[0] + b, a[1] + b, a[2] + b, a[3] + b};
+  }
+}
+
+}  // namespace
+
+extern "C" int bpk_conv3x3_small_supported(int N, int Cin, int Cout, int H, int W) {
+  return N > 0 && Cin > 0 && Cout > 0 && H > 0 && W > 0 && W % 4 == 0 &&
+         (Cout <= 4 || Cin <= 4);
+}
+
+extern "C" int bpk_conv3x3_small_f32(const float* x, const float* pre, const float* weight,
+                                     const float* bias, float* y, int N, int Cin, int Cout, int H,
+                                     int W, void* stream) {
+  BPK_REQUIRE(bpk_conv3x3_small_supported(N, Cin, Cout, H, W),
+              "conv3x3_small: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need W %% 4 == 0 "
+              "and Cin <= 4 or Cout <= 4)", N, Cin, Cout, H, W);
+  SmallGeo g{N, Cin, Cout, H, W, (int)bpk::ceil_div(W, kTW), (int)bpk::ceil_div(H, kTH)};
+  const int64_t blocks = (int64_t)N * g.tiles_x * g.tiles_y;
+  BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_small: grid too large");
+  hipStream_t st = bpk::as_stream(stream);
+  const float2* pre2 = reinterpret_cast<const float2*>(pre);
+  const dim3 grid((unsigned)blocks), block(256);
+  if (Cout <= 4 && (Cout <= Cin || pre)) {
+#define SC(C_)                                                                           \
+  do {                                                                                   \
+    if (pre)                                                                             \
+      hipLaunchKernelGGL((small_cout_kernel<C_, true>), grid, block, 0, st, x, pre2, weight, \
+                         bias, y, g);                                                    \
+    else                                                                                 \
+      hipLaunchKernelGGL((small_cout_kernel<C_, false>), grid, block, 0, st, x, pre2,    \
+                         weight, bias, y, g);                                            \
+  } while (0)
+    switch (Cout) {
+      case 1: SC(1); break;
+      case 2: SC(2); break;
+      case 3: SC(3); break;
+      default: SC(4); break;
+    }
+#undef SC
+  } else {
+    BPK_REQUIRE(pre == nullptr, "conv3x3_small: the GroupNorm prologue needs Cout <= 4");
+    switch (Cin) {
+      case 1: hipLaunchKernelGGL((small_cin_kernel<1>), grid, block, 0, st, x, weight, bias, y, g); break;
+      case 2: hipLaunchKernelGGL((small_cin_kernel<2>), grid, block, 0, st, x, weight, bias, y, g); break;
+      case 3: hipLaunchKernelGGL((small_cin_kernel<3>), grid, block, 0, st, x, weight, bias, y, g); break;
+      default: hipLaunchKernelGGL((small_cin_kernel<4>), grid, block, 0, st, x, weight, bias, y, g); break;
+    }
+  }
+  BPK_LAUNCH_CHECK("conv3x3_small");
+  return BPK_OK;
+}

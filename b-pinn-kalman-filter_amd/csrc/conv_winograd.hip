@@ -399,10 +399,6 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
     poff = (cy * g.W + cx) * 4;
     pdst = py * kPCp + px;
   }
-  if (PRE) {
-    for (int c = tid; c < g.Cin; c += 256) s_ss[c] = pre_n[c];
-    __syncthreads();
-  }
   float pv[kCK];
   auto load_patch = [&](int k) {
     const int soff = (min(k, nch - 1) * kCK) * (int)plane * 4;
@@ -411,11 +407,11 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       pv[c] = __uint_as_float(
           __builtin_amdgcn_raw_buffer_load_b32(xrs, poff, soff + c * (int)plane * 4, 0));
   };
-  auto store_patch = [&](float* sp, int k) {
+  auto store_patch_from = [&](const float* src, float* sp, int k) {
     const int c0 = min(k, nch - 1) * kCK;
 #pragma unroll
     for (int c = 0; c < kCK; ++c) {
-      float v = pv[c];
+      float v = src[c];
       if (PRE) {
         const float2 st = s_ss[c0 + c];
         v = silu_f(v * st.x + st.y);
@@ -423,6 +419,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
     }
   };
+  auto store_patch = [&](float* sp, int k) { store_patch_from(pv, sp, k); };
   // B operands of one k-step half: uo[ks][nb][q] = U[c0 + 4ks + kq][cout_w + 16nb + jj][4q..]
   f4 uo[2][NB][4];
   const int uoff = ((kq * g.Cout + cout_w + jj) * 16) * 4;
@@ -462,14 +459,25 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
   };
 
-  // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight
+  // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight.  The
+  // global loads of patches 0-2, U(0) and the GroupNorm table are all issued before the
+  // first wait, so a workgroup pays one memory latency here, not four.
+  float pv0[kCK], pv1[kCK];
   load_patch(0);
-  store_patch(s_patch_raw[0], 0);
+#pragma unroll
+  for (int c = 0; c < kCK; ++c) pv0[c] = pv[c];
   load_patch(1);
-  store_patch(s_patch_raw[1], 1);
+#pragma unroll
+  for (int c = 0; c < kCK; ++c) pv1[c] = pv[c];
   load_patch(2);
   load_u(0, 0);
   load_u(1, 0);
+  if (PRE) {
+    for (int c = tid; c < g.Cin; c += 256) s_ss[c] = pre_n[c];
+    __syncthreads();
+  }
+  store_patch_from(pv0, s_patch_raw[0], 0);
+  store_patch_from(pv1, s_patch_raw[1], 1);
   __syncthreads();
   read_d(s_patch_raw[0]);
   write_v(s_v[0]);

@@ -107,6 +107,8 @@ def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=N
     None when the conv does not qualify."""
     if not _wino_eligible(x, conv) or (skip is not None and skip.shape[1] != conv.out_channels):
         return None
+    if conv_op.small_supported(x, conv.weight) and conv.out_channels > 4:
+        return None  # the small-Cin kernel has no GroupNorm prologue
     ss = group_norm_affine(x, gn, bias_nc)
     return conv_op.conv3x3(x, conv.weight, conv_bias, skip=skip, div=div, pre=ss)
 

@@ -196,6 +196,16 @@ class NCSNpp(nn.Module):
             temb = None
         return temb, used_sigmas
 
+    def _gn_act_conv(self, h, gn, conv):
+        """conv(act(GroupNorm(h))) -- the pyramid / output heads (reference ncsnpp.py:
+        `self.act(modules[m_idx](h))` then conv3x3).  At inference the normalization is
+        applied inside the conv's input load (statistics pass + conv, op.conv pre=)."""
+        if layers.fused_inference_ok(self, h, self.act):
+            y = layers.gn_silu_conv(h, gn, conv, conv_bias=conv.bias)
+            if y is not None:
+                return y
+        return conv(layers.gn_act(h, gn, self.act))
+
     def forward(self, x, time_cond):
         mods = self.all_modules
         temb, used_sigmas = self._time_embedding(time_cond)
@@ -232,18 +242,17 @@ class NCSNpp(nn.Module):
             elif kind == "res_cat":
                 h = mods[step[1]](torch.cat([h, hs.pop()], dim=1), temb)
             elif kind == "pyr_head":
-                pyramid = layers.gn_act(h, mods[step[1]], self.act)
-                pyramid = mods[step[2]](pyramid)
+                pyramid = self._gn_act_conv(h, mods[step[1]], mods[step[2]])
             elif kind == "pyr_out_skip":
                 pyramid = self.pyramid_upsample(pyramid)
-                ph = mods[step[2]](layers.gn_act(h, mods[step[1]], self.act))
+                ph = self._gn_act_conv(h, mods[step[1]], mods[step[2]])
                 pyramid = pyramid + ph
             elif kind == "pyr_up":
                 pyramid = mods[step[1]](pyramid)
                 pyramid = residual_rescale(pyramid, h, None, _SQRT2 if self.skip_rescale else 1.0)
                 h = pyramid
             elif kind == "head":
-                h = mods[step[2]](layers.gn_act(h, mods[step[1]], self.act))
+                h = self._gn_act_conv(h, mods[step[1]], mods[step[2]])
             elif kind == "head_pyramid":
                 h = pyramid
             else:  # pragma: no cover

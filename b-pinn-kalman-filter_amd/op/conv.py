@@ -1,4 +1,5 @@
-"""3x3 convolution on the fused Winograd F(2x2,3x3) MFMA kernel (csrc/conv_winograd.hip).
+"""3x3 convolution on the fused Winograd F(2x2,3x3) MFMA kernel (csrc/conv_winograd.hip), or
+on the small-channel VALU kernel (csrc/conv_small.hip) when Cin <= 4 or Cout <= 4.
 
 `conv3x3(x, weight, bias=None)` == F.conv2d(x, weight, bias, stride=1, padding=1) for
 fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`).  Backward: the
@@ -20,14 +21,29 @@ import torch
 from ._lib import check, lib, require_hip, stream_ptr
 
 
-def supported(x, weight):
-    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4:
-        return False
-    if tuple(weight.shape[2:]) != (3, 3) or not x.is_cuda:
+def _shape_ok(x, weight):
+    return (x.dtype == torch.float32 and weight.dtype == torch.float32 and x.dim() == 4
+            and tuple(weight.shape[2:]) == (3, 3) and x.is_cuda and weight.shape[1] == x.shape[1])
+
+
+def wino_supported(x, weight):
+    if not _shape_ok(x, weight):
         return False
     N, C, H, W = x.shape
-    return bool(lib.bpk_conv3x3_wino_supported(N, C, weight.shape[0], H, W)) and \
-        weight.shape[1] == C
+    return bool(lib.bpk_conv3x3_wino_supported(N, C, weight.shape[0], H, W))
+
+
+def small_supported(x, weight):
+    """The VALU small-channel kernel (csrc/conv_small.hip): Cin <= 4 or Cout <= 4."""
+    if not _shape_ok(x, weight):
+        return False
+    N, C, H, W = x.shape
+    return bool(lib.bpk_conv3x3_small_supported(N, C, weight.shape[0], H, W))
+
+
+def supported(x, weight):
+    """conv3x3() runs this conv natively: small-channel kernel or Winograd MFMA kernel."""
+    return small_supported(x, weight) or wino_supported(x, weight)
 
 
 def filter_transform(weight):
@@ -97,6 +113,50 @@ def conv3x3_wgrad_raw(x, gy, wshape):
     return dw
 
 
+def conv3x3_small_raw(x, weight, bias=None, pre=None):
+    """conv(a, weight) + bias on the small-channel kernel, a = x or silu(x * s + t)."""
+    x = x.contiguous()
+    N, C, H, W = x.shape
+    Cout = weight.shape[0]
+    w = weight.detach().contiguous()
+    y = torch.empty((N, Cout, H, W), dtype=x.dtype, device=x.device)
+    b = None if bias is None else bias.detach().contiguous()
+    pr = None if pre is None else pre.contiguous()
+    if pr is not None and tuple(pr.shape) != (N, C, 2):
+        raise RuntimeError(f"conv3x3: pre must be [N, Cin, 2], got {tuple(pr.shape)}")
+    check(lib.bpk_conv3x3_small_f32(
+        x.data_ptr(), None if pr is None else pr.data_ptr(), w.data_ptr(),
+        None if b is None else b.data_ptr(), y.data_ptr(), N, C, Cout, H, W,
+        stream_ptr(x.device)), "conv3x3_small")
+    return y
+
+
+class _Conv3x3Small(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return conv3x3_small_raw(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            # backward-data = forward conv of gy with the flipped, transposed filter (the
+            # small side moves from Cout to Cin or back: the same kernel pair)
+            wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
+            if not torch.is_grad_enabled() and small_supported(gy, wt):
+                gx = conv3x3_small_raw(gy, wt)
+            else:
+                gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+        if ctx.needs_input_grad[1]:
+            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 2, 3))
+        return gx, gw, gb
+
+
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, skip, div):
@@ -117,7 +177,7 @@ class _Conv3x3(torch.autograd.Function):
             # backward-data of a 3x3 / stride-1 / pad-1 conv is the forward conv of gy with
             # the flipped, transposed filter: the Winograd kernel when the shape qualifies
             wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
-            if not torch.is_grad_enabled() and supported(gy, wt):
+            if not torch.is_grad_enabled() and wino_supported(gy, wt):
                 gx = conv3x3_fwd_raw(gy, wt)
             else:
                 gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
@@ -131,17 +191,30 @@ class _Conv3x3(torch.autograd.Function):
         return gx, gw, gb, gs, None
 
 
+def _inference_only(*ts):
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
+        raise RuntimeError("conv3x3(pre=...) is inference-only")
+
+
 def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None):
     """F.conv2d(x, weight, bias, padding=1), or the residual-block tail
     (skip + conv2d(x, weight, bias)) / div fused into the same launch.  With `pre`
     ([N, Cin, 2] from op.norm_act.group_norm_affine) the convolved tensor is
     silu(x * s + t) = act(GroupNorm(x + b)) -- inference only (no autograd)."""
     require_hip(x, weight, bias, skip, pre, what="conv3x3")
-    if not supported(x, weight):
+    if small_supported(x, weight) and (pre is None or weight.shape[0] <= 4):
+        if pre is not None:
+            _inference_only(x, weight, bias, skip)
+            y = conv3x3_small_raw(x, weight, bias, pre)
+        else:
+            y = _Conv3x3Small.apply(x, weight, bias)
+        if skip is not None:
+            from .norm_act import residual_rescale
+            y = residual_rescale(skip, y, None, div)
+        return y
+    if not wino_supported(x, weight):
         raise RuntimeError(f"conv3x3: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
     if pre is not None:
-        if torch.is_grad_enabled() and any(t is not None and t.requires_grad
-                                           for t in (x, weight, bias, skip)):
-            raise RuntimeError("conv3x3(pre=...) is inference-only")
+        _inference_only(x, weight, bias, skip)
         return conv3x3_fwd_raw(x, weight, bias, skip, div, pre)
     return _Conv3x3.apply(x, weight, bias, skip, div)

@@ -321,6 +321,17 @@ int64_t bpk_conv3x3_wino_wgrad_workspace_bytes(int N, int Cin, int Cout, int H, 
 int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float* dw, float* workspace,
                                int N, int Cin, int Cout, int H, int W, void* stream);
 
+/* 3x3 / stride 1 / pad 1 conv with a small channel count on one side (VALU, HBM-bound):
+ * the score networks' conv_in (Cin = image channels, models/ncsnpp.py) and output_skip
+ * pyramid heads (Cout = image channels), which the reference runs through nn.Conv2d ->
+ * cuDNN.  y [N, Cout, H, W] = conv(a, w [Cout, Cin, 3, 3]) (+ bias, may be NULL) with
+ * a = x, or a = silu(x * s + t) for pre[n][cin] = (s, t) (bpk_group_norm_affine_f32;
+ * Cout <= 4 only).  supported(): W % 4 == 0 and (Cin <= 4 or Cout <= 4). */
+int bpk_conv3x3_small_supported(int N, int Cin, int Cout, int H, int W);
+int bpk_conv3x3_small_f32(const float* x, const float* pre, const float* weight,
+                          const float* bias, float* y, int N, int Cin, int Cout, int H, int W,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

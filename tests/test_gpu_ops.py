@@ -346,3 +346,61 @@ def test_conv3x3_winograd_fused_groupnorm_silu_prologue(hip):
         ref = conv3x3(group_norm_act(x, gn, ACT_SILU, bnc), w, b, skip=skip, div=2 ** 0.5)
         out = conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=group_norm_affine(x, gn, bnc))
     assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+# ------------------------------------------------------------------ small-channel conv3x3
+@pytest.mark.parametrize("N,cin,cout,h,w", [(2, 1, 128, 128, 128), (3, 3, 64, 20, 36),
+                                             (2, 128, 1, 64, 64), (2, 256, 1, 16, 16),
+                                             (1, 37, 3, 18, 68), (2, 2, 4, 8, 12),
+                                             (1, 4, 2, 33, 100)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_conv3x3_small_channel_matches_fp32_reference(hip, N, cin, cout, h, w, with_bias):
+    """Small-channel VALU conv (Cin <= 4 or Cout <= 4: NCSN++ conv_in and pyramid heads) vs a
+    float64 direct convolution, 2e-6 relative to max|ref| (plain fp32 FMA chains); shapes
+    cover partial 16 x 64 tiles, both kernel forms and ragged channel chunks."""
+    from op.conv import conv3x3, small_supported
+    g = torch.Generator().manual_seed(N * 7 + cin * 3 + cout)
+    x = torch.randn(N, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(cout, generator=g) if with_bias else None
+    assert small_supported(x.to(hip), wt.to(hip))
+    ref = F.conv2d(x.double(), wt.double(), None if b is None else b.double(), padding=1)
+    out = conv3x3(x.to(hip), wt.to(hip), None if b is None else b.to(hip)).double().cpu()
+    assert (out - ref).abs().max().item() <= 2e-6 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("cin,cout", [(1, 64), (64, 1), (3, 2)])
+def test_conv3x3_small_channel_backward(hip, cin, cout):
+    """input / weight / bias gradients of the small-channel conv vs MIOpen (the input
+    gradient runs on the other small-channel form with the flipped, transposed filter)."""
+    from op.conv import conv3x3
+    g = torch.Generator().manual_seed(cin + 10 * cout)
+    x = torch.randn(2, cin, 24, 40, generator=g).to(hip).requires_grad_()
+    w = (torch.randn(cout, cin, 3, 3, generator=g) * 0.2).to(hip).requires_grad_()
+    b = torch.randn(cout, generator=g).to(hip).requires_grad_()
+    go = torch.randn(2, cout, 24, 40, generator=g).to(hip)
+    got = torch.autograd.grad(conv3x3(x, w, b), (x, w, b), go)
+    ref = torch.autograd.grad(F.conv2d(x, w, b, padding=1), (x, w, b), go)
+    for a, r in zip(got, ref):
+        assert (a - r).abs().max().item() <= 2e-5 * r.abs().max().item()
+
+
+def test_conv3x3_small_channel_groupnorm_prologue_and_skip(hip):
+    """pyramid head form: conv(SiLU(GroupNorm(x)), Cout = 1) with the normalization applied in
+    the kernel's patch load == the unfused composition (1e-5 relative); skip + div tail."""
+    from op.conv import conv3x3
+    from op.norm_act import ACT_SILU, group_norm_act, group_norm_affine
+    g = torch.Generator().manual_seed(9)
+    x = (torch.randn(2, 128, 32, 32, generator=g) * 2 + 0.5).to(hip)
+    gn = torch.nn.GroupNorm(32, 128, eps=1e-6).to(hip)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(128, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(128, generator=g))
+        w = (torch.randn(1, 128, 3, 3, generator=g) * 0.03).to(hip)
+        b = torch.randn(1, generator=g).to(hip)
+        skip = torch.randn(2, 1, 32, 32, generator=g).to(hip)
+        ref = F.conv2d(group_norm_act(x, gn, ACT_SILU), w, b, padding=1)
+        out = conv3x3(x, w, b, pre=group_norm_affine(x, gn))
+        assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+        tail = conv3x3(x, w, b, skip=skip, div=2.0, pre=group_norm_affine(x, gn))
+        assert (tail - (skip + ref) / 2.0).abs().max().item() <= 1e-5 * ref.abs().max().item()
