@@ -93,13 +93,91 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 // fast exp / reciprocal: a few ulp, far inside the network tolerance (1e-4)
 __device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 
+// Coalesced stores of one wave's staged output (kWN couts x 8 rows x 16 cols, LDS s_w[co]
+// at stride kOS), with the residual-block tail, and -- stats != nullptr -- the GroupNorm
+// partial statistics of the stored values: stats[n][cout][region] = (mean, M2) of the
+// region's 128 pixels (bpk_group_norm_affine_partials_f32 consumes them, so the next
+// GroupNorm needs no statistics pass over this tensor).  Per iteration the 32 lanes of a
+// half-wave hold one channel's 128 values; the butterfly merge (equal counts) gives every
+// lane the same bits.
+template <int CTRL>
+__device__ inline float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Chan merge of two equal-count partials (count c each); symmetric in its arguments, so both
+// partners of a butterfly get the same bits
+__device__ inline void merge_stats(float& m, float& m2, float mo, float m2o, float c) {
+  const float d = mo - m;
+  m2 = (m2 + m2o) + d * d * (0.5f * c);
+  m = 0.5f * (m + mo);
+}
+
+template <int kWN>
+__device__ inline void store_tile(const float* s_w, const float* __restrict__ skip,
+                                  float* __restrict__ y, float2* __restrict__ stats,
+                                  const WinoGeo& g, int n, int cout_w, int oy0, int ox0, int lane) {
+  const int64_t plane = (int64_t)g.H * g.W;
+  constexpr int kIt = kWN / 2;
+  float mm[kIt], qq[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int q = it * 64 + lane;
+    const int co = q >> 5;                 // 32 float4 per cout (8 rows x 4)
+    const int rem = q & 31;
+    const int row = rem >> 2, c4 = rem & 3;
+    f4 v = *reinterpret_cast<const f4*>(&s_w[co * kOS + row * kOutCols + 4 * c4]);
+    const int64_t o = (int64_t)n * g.Cout * plane + (int64_t)(cout_w + co) * plane +
+                      (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
+    if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
+      const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+      v = f4{(sk[0] + v[0]) / g.div, (sk[1] + v[1]) / g.div, (sk[2] + v[2]) / g.div,
+             (sk[3] + v[3]) / g.div};
+    }
+    *reinterpret_cast<f4*>(&y[o]) = v;
+    mm[it] = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+    float m2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m2 = fmaf(v[e] - mm[it], v[e] - mm[it], m2);
+    qq[it] = m2;
+  }
+  if (!stats) return;
+  // 32-lane reductions (one channel per half-wave and iteration), all iterations interleaved:
+  // xor 1, xor 2 (quad_perm), 8-lane and 16-lane mirrors (DPP), then xor 16 (bpermute)
+#pragma unroll
+  for (int it = 0; it < kIt; ++it)
+    merge_stats(mm[it], qq[it], dpp_f<0xB1>(mm[it]), dpp_f<0xB1>(qq[it]), 4.f);
+#pragma unroll
+  for (int it = 0; it < kIt; ++it)
+    merge_stats(mm[it], qq[it], dpp_f<0x4E>(mm[it]), dpp_f<0x4E>(qq[it]), 8.f);
+#pragma unroll
+  for (int it = 0; it < kIt; ++it)
+    merge_stats(mm[it], qq[it], dpp_f<0x141>(mm[it]), dpp_f<0x141>(qq[it]), 16.f);
+#pragma unroll
+  for (int it = 0; it < kIt; ++it)
+    merge_stats(mm[it], qq[it], dpp_f<0x140>(mm[it]), dpp_f<0x140>(qq[it]), 32.f);
+#pragma unroll
+  for (int it = 0; it < kIt; ++it)
+    merge_stats(mm[it], qq[it], __shfl_xor(mm[it], 16, 64), __shfl_xor(qq[it], 16, 64), 64.f);
+  const int R = g.regions_x * g.regions_y;
+  const int region = (oy0 / kOutRows) * g.regions_x + ox0 / kOutCols;
+  if ((lane & 31) == 0) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int co = (it * 64 + lane) >> 5;
+      stats[((int64_t)n * g.Cout + cout_w + co) * R + region] = make_float2(mm[it], qq[it]);
+    }
+  }
+}
+
 template <int NB, bool PRE>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ U,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ skip,
                                                           const float2* __restrict__ pre,
-                                                          float* __restrict__ y, WinoGeo g,
+                                                          float* __restrict__ y,
+                                                          float2* __restrict__ stats, WinoGeo g,
                                                           int xcd_remap) {
   __shared__ float2 s_ss[2][kCK];  // PRE: (s, t) of the chunk's input channels
   // patch [cin][row][col] + a tail that absorbs the writes of out-of-patch slots (so the
@@ -304,22 +382,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
   }
   __syncthreads();
   // 6. coalesced stores: per wave kWN couts x 8 rows x 16 cols = 32 kWN float4
-#pragma unroll
-  for (int it = 0; it < kWN / 2; ++it) {
-    const int q = it * 64 + lane;
-    const int co = q >> 5;                 // 32 float4 per cout (8 rows x 4)
-    const int rem = q & 31;
-    const int row = rem >> 2, c4 = rem & 3;
-    f4 v = *reinterpret_cast<const f4*>(&s_out[(wave * kWN + co) * kOS + row * kOutCols + 4 * c4]);
-    const int64_t o = (int64_t)n * g.Cout * plane + (int64_t)(cout_w + co) * plane +
-                      (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
-    if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
-      const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
-      v = f4{(sk[0] + v[0]) / g.div, (sk[1] + v[1]) / g.div, (sk[2] + v[2]) / g.div,
-             (sk[3] + v[3]) / g.div};
-    }
-    *reinterpret_cast<f4*>(&y[o]) = v;
-  }
+  store_tile<kWN>(&s_out[wave * kWN * kOS], skip, y, stats, g, n, cout_w, oy0, ox0, lane);
 }
 
 // Software-pipelined form (one workgroup per CU, 4 waves x 32 couts = 128 couts, 32 tiles).
@@ -335,7 +398,7 @@ template <int NB, bool PRE>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    WinoGeo g, int xcd_remap) {
+    float2* __restrict__ stats, WinoGeo g, int xcd_remap) {
   constexpr int kWN = 16 * NB;  // couts per wave
   constexpr int kPatch = kCK * kPR * kPCp;
   __shared__ float s_patch_raw[2][kPatch];                                  // 2 x 5.9 KB
@@ -571,21 +634,291 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
     }
   }
   __syncthreads();
+  store_tile<kWN>(&s_out[wave * kWN * kOS], skip, y, stats, g, n, cout_w, oy0, ox0, lane);
+}
+
+// Persistent form of the pipelined kernel (NB = 1: 4 waves x 16 couts = 64 couts, 32
+// tiles, two workgroups per CU).  The grid holds exactly as many workgroups as fit on the
+// chip at once; workgroup l processes the work items l, l + G, l + 2G, ... (an item = one
+// 8 x 16 pixel region x 64 output channels) as ONE continuous chunk stream: the patch
+// loads, the patch stores, the V transform and the U loads of an item's first chunks run
+// inside the previous item's last chunks exactly as between the chunks of one item, so the
+// per-workgroup prologue (one memory latency + a transform) and the launch / drain of a
+// workgroup are paid once per workgroup instead of once per item.  The output transform
+// stores straight from registers (each lane owns 2 rows x 8 pixels of one channel per
+// M-block: two 16-B stores per row) so the V buffers stay live across the item boundary.
+// The GroupNorm prologue's (s, t) pairs are read per chunk with the patch (uniform loads),
+// since consecutive items of a workgroup belong to different images.
+struct WinoItem {
+  int n, oy0, ox0, cout0;
+};
+
+template <bool PRE>
+__global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
+    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
+    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
+    WinoGeo g, int64_t items, int xcd_remap) {
+  constexpr int kPatch = kCK * kPR * kPCp;
+  constexpr int kVBuf = kCK * kM * kVS;
+  __shared__ float s_patch_raw[2][kPatch];                                   // 2 x 5.9 KB
+  __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];               // 2 x 20.5 KB
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, jj = lane & 15;
+  const int64_t G = gridDim.x;
+  int64_t l = blockIdx.x;
+  // workgroups on one XCD (blockIdx % 8 under round-robin placement) take consecutive
+  // logical indices, i.e. neighbouring items (the cout halves of one region) at a time
+  if (xcd_remap) l = (l % 8) * (G / 8) + l / 8;
+  const int cnt = (int)((items - l + G - 1) / G);  // items of this workgroup (>= 1)
+  const int nch = g.Cin / kCK;
+  const int64_t plane = (int64_t)g.H * g.W;
+
+  // item -> geometry; 32-bit (the host guarantees items < 2^31) and forced scalar, so the
+  // buffer descriptors built from it stay in SGPRs (no waterfall loops)
+  auto decode = [&](int i) {
+    const unsigned it = (unsigned)(l + (int64_t)min(i, cnt - 1) * G);
+    const unsigned cbs = (unsigned)g.cout_blocks, rxs = (unsigned)g.regions_x,
+                   rys = (unsigned)g.regions_y;
+    const unsigned r0 = it / cbs, r1 = r0 / rxs;
+    WinoItem w;
+    w.cout0 = __builtin_amdgcn_readfirstlane((int)(it - r0 * cbs) * 64);
+    w.ox0 = __builtin_amdgcn_readfirstlane((int)(r0 - r1 * rxs) * kOutCols);
+    w.oy0 = __builtin_amdgcn_readfirstlane((int)(r1 % rys) * kOutRows);
+    w.n = __builtin_amdgcn_readfirstlane((int)(r1 / rys));
+    return w;
+  };
+
+  f4 acc[16][2];
 #pragma unroll
-  for (int it = 0; it < kWN / 2; ++it) {
-    const int q = it * 64 + lane;
-    const int co = q >> 5;
-    const int rem = q & 31;
-    const int row = rem >> 2, c4 = rem & 3;
-    f4 v = *reinterpret_cast<const f4*>(&s_out[(wave * kWN + co) * kOS + row * kOutCols + 4 * c4]);
-    const int64_t o = (int64_t)n * g.Cout * plane + (int64_t)(cout_w + co) * plane +
-                      (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
-    if (skip) {
-      const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
-      v = f4{(sk[0] + v[0]) / g.div, (sk[1] + v[1]) / g.div, (sk[2] + v[2]) / g.div,
-             (sk[3] + v[3]) / g.div};
+  for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
+
+  // ---- load cursor: the chunk whose patch is loaded next (item li, chunk lk)
+  constexpr int kPos = kPR * kPC;  // 180
+  const int pt = tid < kPos ? tid : 0;
+  const int ppy = pt / kPC, ppx = pt - ppy * kPC;
+  const int pdst = ppy * kPCp + ppx;
+  int li = 0, lk = 0;
+  WinoItem lit = decode(0);
+  __amdgpu_buffer_rsrc_t xrs;
+  int poff;
+  bool pin_cur;
+  auto set_load_item = [&]() {
+    const float* xn = x + (int64_t)lit.n * g.Cin * plane;
+    xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xn), 0, (int)(g.Cin * plane * 4),
+                                            0x00020000);
+    const int iy = lit.oy0 - 1 + ppy, ix = lit.ox0 - 1 + ppx;
+    pin_cur = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+    const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
+    poff = (cy * g.W + cx) * 4;
+  };
+  set_load_item();
+  // loaded values and what the store needs of them: in-image bit and the chunk's (s, t)
+  float pv[kCK];
+  bool pin_ld;
+  float2 ss_ld[kCK];
+  auto load_patch = [&]() {
+    const int k = li < cnt ? lk : nch - 1;  // past the end: re-load the last chunk
+    const int soff = k * kCK * (int)plane * 4;
+#pragma unroll
+    for (int c = 0; c < kCK; ++c)
+      pv[c] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(xrs, poff, soff + c * (int)plane * 4, 0));
+    pin_ld = pin_cur;
+    if (PRE) {
+      const float2* ps = pre + (int64_t)lit.n * g.Cin + k * kCK;
+#pragma unroll
+      for (int c = 0; c < kCK; ++c) ss_ld[c] = ps[c];
     }
-    *reinterpret_cast<f4*>(&y[o]) = v;
+    if (li < cnt && ++lk == nch) {
+      lk = 0;
+      ++li;
+      lit = decode(li);
+      set_load_item();
+    }
+  };
+  auto store_patch_from = [&](const float* src, const float2* ss, bool pin, float* sp) {
+#pragma unroll
+    for (int c = 0; c < kCK; ++c) {
+      float v = src[c];
+      if (PRE) v = silu_f(v * ss[c].x + ss[c].y);
+      sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
+    }
+  };
+
+  // ---- U cursor: the chunk whose B operands are loaded next
+  int ui = 0, uk = 0;
+  int uoff;
+  auto set_u_item = [&]() {
+    const WinoItem w = decode(ui);
+    uoff = ((kq * g.Cout + w.cout0 + wave * 16 + jj) * 16) * 4;
+  };
+  set_u_item();
+  f4 uo[2][4];
+  auto u_soff = [&](int ks) {
+    const int k = ui < cnt ? uk : nch - 1;
+    return ((k * kCK + 4 * ks) * g.Cout) * 64;
+  };
+  auto load_u_half = [&](int ks, int q) {
+    using u4 = __attribute__((ext_vector_type(4))) unsigned;
+    const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, u_soff(ks), 0);
+    uo[ks][q] = __builtin_bit_cast(f4, w);
+  };
+  auto advance_u = [&]() {
+    if (ui < cnt && ++uk == nch) {
+      uk = 0;
+      ++ui;
+      set_u_item();
+    }
+  };
+
+  const int tc = tid >> 5, tm = tid & 31;
+  const int tty = tm / kTC, ttx = tm - tty * kTC;
+  float d[4][4];
+  auto read_d = [&](const float* sp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[i][j] = sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j];
+  };
+  auto write_v = [&](float* sv) {
+    float t[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[0][j] = d[0][j] - d[2][j];
+      t[1][j] = d[1][j] + d[2][j];
+      t[2][j] = d[2][j] - d[1][j];
+      t[3][j] = d[1][j] - d[3][j];
+    }
+    f4* dst = reinterpret_cast<f4*>(&sv[(tc * kM + tm) * kVS]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
+  };
+
+  // ---- prologue: chunks 0-2 and U(0) issued before the first wait
+  float pv0[kCK], pv1[kCK];
+  float2 ss0[kCK], ss1[kCK];
+  bool pin0, pin1;
+  load_patch();
+#pragma unroll
+  for (int c = 0; c < kCK; ++c) { pv0[c] = pv[c]; ss0[c] = ss_ld[c]; }
+  pin0 = pin_ld;
+  load_patch();
+#pragma unroll
+  for (int c = 0; c < kCK; ++c) { pv1[c] = pv[c]; ss1[c] = ss_ld[c]; }
+  pin1 = pin_ld;
+  load_patch();
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) load_u_half(ks, q);
+  advance_u();
+  store_patch_from(pv0, ss0, pin0, s_patch_raw[0]);
+  store_patch_from(pv1, ss1, pin1, s_patch_raw[1]);
+  __syncthreads();
+  read_d(s_patch_raw[0]);
+  write_v(s_v[0]);
+  __syncthreads();
+
+  f4 a[4];
+  auto a_src = [&](const float* sv, int grp) {
+    const int ks = grp >> 1, mb = grp & 1;
+    return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
+  };
+  {
+    const f4* src = a_src(s_v[0], 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = src[q];
+  }
+
+  // ---- epilogue of one item: output transform straight to global memory, one 16-B
+  // strip (2 tiles x 2 pixels of one row) at a time to keep few temporaries live
+  int ci = 0;  // compute cursor (item)
+  auto epilogue = [&]() {
+    const WinoItem w = decode(ci);
+    const int co = w.cout0 + wave * 16 + jj;
+    const float bv = bias ? bias[co] : 0.f;
+    const int64_t obase = ((int64_t)w.n * g.Cout + co) * plane;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      // tiles m = 16 mb + 4 kq + rg: tile row 2 mb + kq / 2, tile cols 4 (kq & 1) + rg
+      const int oy = w.oy0 + 2 * (2 * mb + (kq >> 1));
+      const int ox = w.ox0 + 8 * (kq & 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {      // output row 2 ty + h
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {    // tiles rg = 2e, 2e + 1
+          f4 v;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int rg = 2 * e + u;
+            float t[4];  // row h of A^T M, A^T = [[1,1,1,0],[0,1,-1,-1]]
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              t[j] = h == 0 ? acc[j][mb][rg] + acc[4 + j][mb][rg] + acc[8 + j][mb][rg]
+                            : acc[4 + j][mb][rg] - acc[8 + j][mb][rg] - acc[12 + j][mb][rg];
+            v[2 * u] = t[0] + t[1] + t[2] + bv;
+            v[2 * u + 1] = t[1] - t[2] - t[3] + bv;
+          }
+          const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
+          if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
+            const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = (sk[c] + v[c]) / g.div;
+          }
+          *reinterpret_cast<f4*>(&y[o]) = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  auto step = [&](auto sb_c) {
+    constexpr int SB = decltype(sb_c)::value;
+    const float* sv = s_v[SB];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      const int ks = grp >> 1, mb = grp & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                          // patch(q+1)
+      if (grp == 1) write_v(s_v[SB ^ 1]);                                 // V(q+1)
+      if (grp == 2) store_patch_from(pv, ss_ld, pin_ld, s_patch_raw[SB]);  // patch(q+2)
+      if (grp == 3) load_patch();                                         // patch(q+3)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp)
+          acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              a[q][pp], uo[ks][q][pp], acc[4 * q + pp][mb], 0, 0, 0);
+        if (grp < 3) a[q] = a_src(sv, grp + 1)[q];
+        if (mb == 1) load_u_half(ks, q);  // U(q+1)
+      }
+    }
+    advance_u();
+    __syncthreads();
+  };
+  auto read_a0 = [&](const float* sv) {
+    const f4* src = a_src(sv, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = src[q];
+  };
+  // nch is even (host check), so every item starts on LDS buffer 0
+  for (; ci < cnt; ++ci) {
+    for (int k = 0; k < nch; k += 2) {
+      step(std::integral_constant<int, 0>{});
+      read_a0(s_v[1]);
+      step(std::integral_constant<int, 1>{});
+      if (k + 2 < nch) read_a0(s_v[0]);
+    }
+    epilogue();  // before the next item's A reads, so those registers are free here
+    read_a0(s_v[0]);
   }
 }
 
@@ -610,9 +943,11 @@ extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W
          W % kOutCols == 0;
 }
 
-extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U,
-                                        const float* bias, const float* skip, float div, float* y,
-                                        int N, int Cin, int Cout, int H, int W, void* stream) {
+extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const float* U,
+                                       const float* bias, const float* skip, float div, float* y,
+                                       float* stats, int N, int Cin, int Cout, int H, int W,
+                                       void* stream) {
+  float2* stats2 = reinterpret_cast<float2*>(stats);
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
               "Cout %% 64, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
@@ -627,6 +962,40 @@ extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const 
     const char* e = getenv("BPK_WINO_PIPE");
     return e ? atoi(e) : 1;
   }();
+  // BPK_WINO_PERSIST=1: the persistent form for the GroupNorm-prologue convs (=2: for every
+  // conv).  Opt-in: it removes the per-workgroup fixed cost (~2 chunks) but its main loop runs
+  // ~9 % slower, a net loss for Cin >= 256 (profiles/r01_conv_persist_sweep.txt).
+  static const int persist_env = [] {
+    const char* e = getenv("BPK_WINO_PERSIST");
+    return e ? atoi(e) : 0;
+  }();
+  if (pipe_env == 1 && (persist_env == 2 || (persist_env == 1 && pre)) && Cin % (2 * kCK) == 0 &&
+      !stats) {
+    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div};
+    const int64_t items = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
+    // as many workgroups as are resident at once (2 per CU): more would run as a second,
+    // mostly idle wave of workgroups
+    static int slots = 0;
+    if (slots == 0) {
+      int dev = 0, cus = 0, occ = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wino_f23_persist_kernel<true>, 256, 0);
+      slots = std::max(8, cus * std::max(1, occ));
+    }
+    const int64_t G = std::min<int64_t>(items, slots);
+    const int remap = (G % 8 == 0) ? 1 : 0;
+    const float2* pre2 = reinterpret_cast<const float2*>(pre);
+    hipStream_t st = bpk::as_stream(stream);
+    if (pre)
+      hipLaunchKernelGGL((wino_f23_persist_kernel<true>), dim3((unsigned)G), dim3(256), 0, st, x,
+                         U, bias, skip, pre2, y, g, items, remap);
+    else
+      hipLaunchKernelGGL((wino_f23_persist_kernel<false>), dim3((unsigned)G), dim3(256), 0, st, x,
+                         U, bias, skip, pre2, y, g, items, remap);
+    BPK_LAUNCH_CHECK("conv3x3_wino_persist");
+    return BPK_OK;
+  }
   if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
     // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup
     const int pnb = (pipe_env == 2 && Cout % 128 == 0) ? 2 : 1;
@@ -638,7 +1007,7 @@ extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const 
     hipStream_t st = bpk::as_stream(stream);
 #define WINO_PIPE(NB_, PRE_)                                                                  \
   hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, \
-                     x, U, bias, skip, pre2, y, g, remap)
+                     x, U, bias, skip, pre2, y, stats2, g, remap)
     if (pnb == 2) {
       if (pre) WINO_PIPE(2, true); else WINO_PIPE(2, false);
     } else {
@@ -657,7 +1026,7 @@ extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const 
   hipStream_t st = bpk::as_stream(stream);
 #define WINO_LAUNCH(NB_, PRE_)                                                                 \
   hipLaunchKernelGGL((wino_f23_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, x, \
-                     U, bias, skip, pre2, y, g, remap)
+                     U, bias, skip, pre2, y, stats2, g, remap)
   if (nb == 2) {
     if (pre) WINO_LAUNCH(2, true); else WINO_LAUNCH(2, false);
   } else {
@@ -666,6 +1035,13 @@ extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const 
 #undef WINO_LAUNCH
   BPK_LAUNCH_CHECK("conv3x3_wino");
   return BPK_OK;
+}
+
+extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U,
+                                        const float* bias, const float* skip, float div, float* y,
+                                        int N, int Cin, int Cout, int H, int W, void* stream) {
+  return bpk_conv3x3_wino_ex_f32(x, pre, U, bias, skip, div, y, nullptr, N, Cin, Cout, H, W,
+                                 stream);
 }
 
 extern "C" int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,

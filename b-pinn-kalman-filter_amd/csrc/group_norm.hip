@@ -659,3 +659,63 @@ extern "C" int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, c
   BPK_LAUNCH_CHECK("group_norm_affine");
   return BPK_OK;
 }
+
+// ---------------------------------------------------------------- statistics from partials
+// GroupNorm (s, t) from per-(n, channel, region) partial statistics written by the producer
+// of x (the Winograd conv's epilogue, bpk_conv3x3_wino_ex_f32): part[n][c][r] = (mean, M2) of
+// `cnt` values each.  Equal counts, so the group mean is the mean of the partial means
+// (+ the per-channel bias) and M2 = sum(M2_i + cnt (mean_i + b_c - mean)^2) -- two passes
+// over the partials, fixed reduction order (deterministic).
+namespace {
+__global__ __launch_bounds__(256) void gn_affine_partials_kernel(
+    const float2* __restrict__ part, int R, float cnt, const float* __restrict__ bias_nc,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float2* __restrict__ ss,
+    int C, int G, float eps) {
+  __shared__ float sbuf[256 / kWave];
+  __shared__ float s_stat[2];
+  const int ng = blockIdx.x;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const int K = cpg * R;
+  const float2* pg = part + ((int64_t)n * C + (int64_t)g * cpg) * R;
+  const float* bn = bias_nc ? bias_nc + (int64_t)n * C + g * cpg : nullptr;
+  float ls = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) ls += pg[i].x + (bn ? bn[i / R] : 0.f);
+  const float mean = block_sum<256>(ls, sbuf) / (float)K;
+  float lm2 = 0.f;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) {
+    const float2 p = pg[i];
+    const float d = p.x + (bn ? bn[i / R] : 0.f) - mean;
+    lm2 += p.y + cnt * d * d;
+  }
+  const float m2 = block_sum<256>(lm2, sbuf);
+  if (threadIdx.x == 0) {
+    s_stat[0] = mean;
+    s_stat[1] = 1.f / sqrtf(m2 / ((float)K * cnt) + eps);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < cpg; j += blockDim.x) {
+    const int c = g * cpg + j;
+    const float sc = s_stat[1] * (gamma ? gamma[c] : 1.f);
+    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+    ss[(int64_t)n * C + c] = make_float2(sc, (beta ? beta[c] : 0.f) + (b - s_stat[0]) * sc);
+  }
+}
+}  // namespace
+
+extern "C" int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt,
+                                                  const float* bias_nc, const float* gamma,
+                                                  const float* beta, float* scale_shift, int N,
+                                                  int C, int G, float eps, void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && G > 0 && R > 0 && cnt > 0,
+              "group_norm_affine_partials: bad shape");
+  BPK_REQUIRE(C % G == 0, "group_norm_affine_partials: C (%d) not divisible by G (%d)", C, G);
+  BPK_REQUIRE((int64_t)(C / G) * R < (1ll << 31), "group_norm_affine_partials: too many partials");
+  if (N == 0) return BPK_OK;
+  hipLaunchKernelGGL(gn_affine_partials_kernel, dim3(N * G), dim3(256), 0, bpk::as_stream(stream),
+                     reinterpret_cast<const float2*>(part), R, (float)cnt, bias_nc, gamma, beta,
+                     reinterpret_cast<float2*>(scale_shift), C, G, eps);
+  BPK_LAUNCH_CHECK("group_norm_affine_partials");
+  return BPK_OK;
+}

@@ -73,6 +73,8 @@ def ddpm_conv1x1(in_planes, out_planes, stride=1, bias=True, init_scale=1., padd
 
 
 _WINO_ENABLED = os.environ.get("BPK_CONV", "winograd") != "miopen"
+# GroupNorm partial statistics from the producing conv's epilogue (BPK_GN_STATS=0: off)
+_GN_STATS = os.environ.get("BPK_GN_STATS", "1") != "0"
 
 
 def _wino_eligible(x, conv: nn.Conv2d):
@@ -110,15 +112,28 @@ def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=N
     if conv_op.small_supported(x, conv.weight) and conv.out_channels > 4:
         return None  # the small-Cin kernel has no GroupNorm prologue
     ss = group_norm_affine(x, gn, bias_nc)
-    return conv_op.conv3x3(x, conv.weight, conv_bias, skip=skip, div=div, pre=ss)
+    return conv_op.conv3x3(x, conv.weight, conv_bias, skip=skip, div=div, pre=ss,
+                           stats=_GN_STATS and conv_op.wino_supported(x, conv.weight))
 
 
-def conv_residual(h, conv: nn.Conv2d, bias, skip, div):
+def conv_residual(h, conv: nn.Conv2d, bias, skip, div, stats=False):
     """(skip + (conv(h) + bias)) / div -- the tail of every residual block -- as ONE
-    Winograd launch when the conv qualifies, else conv + the fused residual kernel."""
+    Winograd launch when the conv qualifies, else conv + the fused residual kernel.
+    stats=True (inference): the output carries GroupNorm partial statistics."""
     if _wino_eligible(h, conv) and skip.shape[1] == conv.out_channels:
-        return conv_op.conv3x3(h, conv.weight, bias, skip=skip, div=div)
+        return conv_op.conv3x3(h, conv.weight, bias, skip=skip, div=div,
+                               stats=_GN_STATS and stats and conv_op.wino_supported(h, conv.weight))
     return residual_rescale(skip, conv2d(h, conv, bias=False), bias, div)
+
+
+def cat_channels(a, b):
+    """torch.cat([a, b], 1); GroupNorm partial statistics carried by both inputs are
+    concatenated too (per-channel partials over the same regions)."""
+    y = torch.cat([a, b], dim=1)
+    pa, pb = conv_op.gn_partials(a), conv_op.gn_partials(b)
+    if pa is not None and pb is not None and pa[1:] == pb[1:]:
+        conv_op.attach_gn_partials(y, torch.cat([pa[0], pb[0]], dim=1), pa[1], pa[2])
+    return y
 
 
 class Conv2d(nn.Conv2d):

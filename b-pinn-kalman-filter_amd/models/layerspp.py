@@ -238,4 +238,4 @@ class ResnetBlockBigGANpp(nn.Module):
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
         h = self.Dropout_0(h)
-        return layers.conv_residual(h, self.Conv_1, bias, x, div)
+        return layers.conv_residual(h, self.Conv_1, bias, x, div, stats=fused)

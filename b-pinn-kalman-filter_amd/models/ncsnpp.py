@@ -240,7 +240,7 @@ class NCSNpp(nn.Module):
             elif kind == "h_from_top":
                 h = hs[-1]
             elif kind == "res_cat":
-                h = mods[step[1]](torch.cat([h, hs.pop()], dim=1), temb)
+                h = mods[step[1]](layers.cat_channels(h, hs.pop()), temb)
             elif kind == "pyr_head":
                 pyramid = self._gn_act_conv(h, mods[step[1]], mods[step[2]])
             elif kind == "pyr_out_skip":

@@ -60,9 +60,28 @@ def filter_transform(weight):
     return U
 
 
-def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None):
+GN_PART_COUNT = 128  # pixels per partial-statistics region (8 x 16)
+
+
+def gn_partials(t):
+    """(part [N, C, R, 2], R, count) attached to `t` by a stats-producing conv, or None if
+    absent or stale (t modified in place since)."""
+    p = getattr(t, "_bpk_gn_part", None)
+    if p is None or p[3] != t._version:
+        return None
+    return p[:3]
+
+
+def attach_gn_partials(t, part, R, cnt=GN_PART_COUNT):
+    t._bpk_gn_part = (part, R, cnt, t._version)
+    return t
+
+
+def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
     """conv(a, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch),
-    where a = x, or silu(x * s + t) with pre[n, c] = (s, t) (GroupNorm+SiLU fused in)."""
+    where a = x, or silu(x * s + t) with pre[n, c] = (s, t) (GroupNorm+SiLU fused in).
+    stats=True also writes the GroupNorm partial statistics of the output (attached to it,
+    see gn_partials) so the next GroupNorm skips its statistics pass."""
     x = x.contiguous()
     N, C, H, W = x.shape
     Cout = weight.shape[0]
@@ -75,10 +94,17 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None):
     pr = None if pre is None else pre.contiguous()
     if pr is not None and tuple(pr.shape) != (N, C, 2):
         raise RuntimeError(f"conv3x3: pre must be [N, Cin, 2], got {tuple(pr.shape)}")
-    check(lib.bpk_conv3x3_wino_pre_f32(
+    part = None
+    if stats:
+        R = (H // 8) * (W // 16)
+        part = torch.empty((N, Cout, R, 2), dtype=torch.float32, device=x.device)
+    check(lib.bpk_conv3x3_wino_ex_f32(
         x.data_ptr(), None if pr is None else pr.data_ptr(), U.data_ptr(),
         None if b is None else b.data_ptr(), None if sk is None else sk.data_ptr(), float(div),
-        y.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)), "conv3x3_wino")
+        y.data_ptr(), None if part is None else part.data_ptr(), N, C, Cout, H, W,
+        stream_ptr(x.device)), "conv3x3_wino")
+    if part is not None:
+        attach_gn_partials(y, part, R)
     return y
 
 
@@ -191,14 +217,19 @@ class _Conv3x3(torch.autograd.Function):
         return gx, gw, gb, gs, None
 
 
+def _needs_grad(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
 def _inference_only(*ts):
-    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
+    if _needs_grad(*ts):
         raise RuntimeError("conv3x3(pre=...) is inference-only")
 
 
-def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None):
+def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
     """F.conv2d(x, weight, bias, padding=1), or the residual-block tail
-    (skip + conv2d(x, weight, bias)) / div fused into the same launch.  With `pre`
+    (skip + conv2d(x, weight, bias)) / div fused into the same launch.  stats=True (inference,
+    Winograd path): GroupNorm partial statistics of the output ride along (gn_partials).  With `pre`
     ([N, Cin, 2] from op.norm_act.group_norm_affine) the convolved tensor is
     silu(x * s + t) = act(GroupNorm(x + b)) -- inference only (no autograd)."""
     require_hip(x, weight, bias, skip, pre, what="conv3x3")
@@ -214,7 +245,7 @@ def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None):
         return y
     if not wino_supported(x, weight):
         raise RuntimeError(f"conv3x3: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
-    if pre is not None:
+    if pre is not None or (stats and not _needs_grad(x, weight, bias, skip)):
         _inference_only(x, weight, bias, skip)
-        return conv3x3_fwd_raw(x, weight, bias, skip, div, pre)
+        return conv3x3_fwd_raw(x, weight, bias, skip, div, pre, stats)
     return _Conv3x3.apply(x, weight, bias, skip, div)

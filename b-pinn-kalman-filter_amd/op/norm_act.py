@@ -88,6 +88,21 @@ def group_norm_affine(x, gn: torch.nn.GroupNorm, bias_nc=None):
     the statistics pass of GroupNorm alone (one read of x), for convolutions that apply the
     normalization in their input load (op.conv.conv3x3(..., pre=)).  Inference only."""
     require_hip(x, bias_nc, what="group_norm_affine")
+    from .conv import gn_partials
+    part = gn_partials(x)
+    if part is not None:  # statistics from the producing conv's epilogue: no pass over x
+        pt, R, cnt = part
+        N, C = x.shape[:2]
+        ss = torch.empty((N, C, 2), device=x.device, dtype=torch.float32)
+        bnc = bias_nc.contiguous() if bias_nc is not None else None
+        w = gn.weight if gn.affine else None
+        b = gn.bias if gn.affine else None
+        check(lib.bpk_group_norm_affine_partials_f32(
+            pt.data_ptr(), R, cnt, bnc.data_ptr() if bnc is not None else None,
+            w.detach().data_ptr() if w is not None else None,
+            b.detach().data_ptr() if b is not None else None, ss.data_ptr(), N, C,
+            gn.num_groups, float(gn.eps), stream_ptr(x.device)), "group_norm_affine_partials")
+        return ss
     x = x.contiguous()
     N, C = x.shape[:2]
     HW = x.numel() // max(N * C, 1)

@@ -194,6 +194,12 @@ int bpk_group_norm_fwd_f32(const float* x, const float* bias_nc, const float* ga
 int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float* gamma,
                               const float* beta, float* scale_shift, void* workspace, int N, int C,
                               int64_t HW, int G, float eps, void* stream);
+/* The same affine form from per-(n, channel, region) partial statistics written by the
+ * producer of x (bpk_conv3x3_wino_ex_f32): part [N, C, R, 2] = (mean, M2) of cnt values
+ * each; no pass over x.  Deterministic (fixed reduction order). */
+int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt, const float* bias_nc,
+                                       const float* gamma, const float* beta, float* scale_shift,
+                                       int N, int C, int G, float eps, void* stream);
 int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
                            const float* gamma, const float* beta, const float* mean,
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,
@@ -310,6 +316,13 @@ int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* b
 int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U, const float* bias,
                              const float* skip, float div, float* y, int N, int Cin, int Cout,
                              int H, int W, void* stream);
+/* Same, and -- stats != NULL -- the GroupNorm partial statistics of the stored output:
+ * stats [N, Cout, (H/8) * (W/16), 2] = (mean, M2) of each channel over each 8 x 16 pixel
+ * region (bpk_group_norm_affine_partials_f32 turns them into the next GroupNorm's affine
+ * form without a statistics pass over y). */
+int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const float* U, const float* bias,
+                            const float* skip, float div, float* y, float* stats, int N, int Cin,
+                            int Cout, int H, int W, void* stream);
 /* Weight gradient of the same conv (the backward-filter convolution cuDNN / MIOpen runs
  * for nn.Conv2d's autograd): dw [Cout, Cin, 3, 3] = d(sum y * gy)/dw for x [N, Cin, H, W],
  * gy [N, Cout, H, W].  Winograd F(2x2,3x3): per transform position a split-K GEMM

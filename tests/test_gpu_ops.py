@@ -238,7 +238,8 @@ def test_grid_sample_double_backward_gradgradcheck(hip):
 
 # ------------------------------------------------------------------ Winograd conv3x3
 @pytest.mark.parametrize("N,cin,cout,hw", [(1, 8, 128, 16), (3, 24, 128, 32), (2, 128, 256, 64),
-                                           (2, 256, 128, 16), (1, 512, 256, 32)])
+                                           (2, 256, 128, 16), (1, 512, 256, 32),
+                                           (9, 64, 128, 64), (16, 16, 64, 96)])
 @pytest.mark.parametrize("with_bias", [True, False])
 def test_conv3x3_winograd_matches_fp32_reference(hip, N, cin, cout, hw, with_bias):
     """Fused Winograd F(2x2,3x3) MFMA conv vs a float64 direct convolution; the fp32 MIOpen
@@ -404,3 +405,64 @@ def test_conv3x3_small_channel_groupnorm_prologue_and_skip(hip):
         assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
         tail = conv3x3(x, w, b, skip=skip, div=2.0, pre=group_norm_affine(x, gn))
         assert (tail - (skip + ref) / 2.0).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_conv3x3_winograd_persistent_many_items(hip):
+    """The persistent Winograd kernel streams several work items per workgroup (more items
+    than resident workgroups, uneven split): GroupNorm prologue + residual tail at that size
+    vs the unfused composition in float64 (1e-5 relative)."""
+    from op.conv import conv3x3
+    from op.norm_act import group_norm_affine
+    g = torch.Generator().manual_seed(11)
+    N, C, Co, H, W = 11, 64, 128, 48, 80   # 11 * 6 * 5 * 2 = 660 items
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.3)
+    gn = torch.nn.GroupNorm(16, C, eps=1e-6)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(C, generator=g))
+    w = torch.randn(Co, C, 3, 3, generator=g) * 0.05
+    b = torch.randn(Co, generator=g)
+    skip = torch.randn(N, Co, H, W, generator=g)
+    a = F.silu(F.group_norm(x.double(), 16, gn.weight.double(), gn.bias.double(), 1e-6))
+    ref = (skip.double() + F.conv2d(a, w.double(), b.double(), padding=1)) / 2 ** 0.5
+    gnd = gn.to(hip)
+    with torch.no_grad():
+        xd = x.to(hip)
+        out = conv3x3(xd, w.to(hip), b.to(hip), skip=skip.to(hip), div=2 ** 0.5,
+                      pre=group_norm_affine(xd, gnd)).double().cpu()
+    assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("with_bias_nc", [False, True])
+def test_conv3x3_winograd_gn_partial_statistics(hip, with_bias_nc):
+    """GroupNorm partial statistics from the Winograd epilogue (stats=True, incl. the residual
+    tail) and through a channel concat: the affine form built from them equals the one from
+    the full statistics pass (1e-5 relative), and the conv output itself is unchanged."""
+    from models.layers import cat_channels
+    from op.conv import conv3x3, gn_partials
+    from op.norm_act import group_norm_affine
+    g = torch.Generator().manual_seed(21)
+    N, C, Co, H, W = 3, 64, 128, 32, 48
+    x = torch.randn(N, C, H, W, generator=g).to(hip)
+    w = (torch.randn(Co, C, 3, 3, generator=g) * 0.05).to(hip)
+    b = torch.randn(Co, generator=g).to(hip)
+    skip = (torch.randn(N, Co, H, W, generator=g) * 3 + 1).to(hip)
+    other = (torch.randn(N, Co, H, W, generator=g) * 0.5 - 2).to(hip)
+    bnc = torch.randn(N, 2 * Co, generator=g).to(hip) if with_bias_nc else None
+    gn = torch.nn.GroupNorm(32, 2 * Co, eps=1e-6).to(hip)
+    with torch.no_grad():
+        gn.weight.copy_((torch.rand(2 * Co, generator=g) + 0.5).to(hip))
+        gn.bias.copy_(torch.randn(2 * Co, generator=g).to(hip))
+        y = conv3x3(x, w, b, skip=skip, div=2 ** 0.5, stats=True)
+        y2 = conv3x3(skip, w.new_zeros(Co, Co, 3, 3) + 0.01, None, skip=other, div=1.0, stats=True)
+        assert gn_partials(y) is not None and gn_partials(y2) is not None
+        plain = conv3x3(x, w, b, skip=skip, div=2 ** 0.5)
+        assert torch.equal(y, plain)
+        cat = cat_channels(y, y2)
+        assert gn_partials(cat) is not None
+        got = group_norm_affine(cat, gn, bnc)
+        ref = group_norm_affine(cat.clone(), gn, bnc)   # clone: no partials -> full pass
+        assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+        # an in-place update invalidates the attached statistics
+        y.add_(1.0)
+        assert gn_partials(y) is None

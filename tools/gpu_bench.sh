@@ -1,7 +1,6 @@
 #!/bin/bash
 # bench (N=1) with the MIOpen kernel cache written under gpurun_out/ (so it comes back and
-# can be kept in-tree), then the rocprofv3 kernel trace of the sampler phase and the
-# Winograd NB=2 A/B.  Each GPU step has its own limit; stop at the first failure.
+# can be kept in-tree), then the rocprofv3 kernel trace of the sampler phase.  Each GPU step has its own limit; stop at the first failure.
 mkdir -p gpurun_out/miopen_cache/kernels gpurun_out/miopen_cache/db
 export TMPDIR=/tmp
 if [ -d b-pinn-kalman-filter_amd/miopen_cache ]; then cp -r b-pinn-kalman-filter_amd/miopen_cache/. gpurun_out/miopen_cache/; fi
@@ -11,5 +10,3 @@ cat gpurun_out/bench.log
 [ "$1" = "noprof" ] && exit 0
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 5 --warmup 2 --no-train --no-cpu-baseline --no-pinn --no-dps > gpurun_out/prof.log 2>&1 || exit 1
 echo PROF_OK
-BPK_WINO_PIPE=2 timeout -k 10 300 python tools/bench_conv.py > gpurun_out/conv_pipe2.log 2>&1 || exit 1
-cat gpurun_out/conv_pipe2.log
