@@ -21,6 +21,8 @@
 #include "bpk_common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -194,6 +196,262 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restr
     }
 }
 
+// Software-pipelined weight gradient (default).  Same decomposition as wino_wgrad_kernel
+// (workgroup = 32 cin x 64 cout over a K-range of 8-tile chunks), reorganized like the
+// forward pipe kernel:
+//   * the B operands (Gbar = A dY A^T, one (tile, cout) record per lane and k-step) are
+//     built in registers by the lane that consumes them, from a 2 x 2 gradient tile it
+//     loads itself (two 8-byte loads), one chunk ahead -- no LDS traffic for the gradient;
+//   * chunk c's input patch is loaded at step c-3 (2 x 16 B + one halo word per thread and
+//     (cin, row)), stored to LDS at step c-2, transformed into V records at step c-1 while
+//     the MFMAs of the previous chunk run (double-buffered patch and V), one barrier per chunk;
+//   * V records of tile t sit at t * 644 + cin * 20 floats: conflict-free 16-B writes,
+//     2-way 16-B operand reads.
+constexpr int kXRS = 24;                     // LDS patch row: halo at 3, interior at 4..19, halo 20
+constexpr int kXCS = kXR * kXRS + 16;        // per-cin stride (2-way transform reads)
+constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records (644)
+
+__global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ gy,
+                                                                 float* __restrict__ part,
+                                                                 WgradGeo g, int xcd_remap) {
+  __shared__ __attribute__((aligned(16))) float s_x[2][kCB * kXCS];   // 2 x 14.3 KB
+  __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 20.6 KB
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, jj = lane & 15;
+  int64_t nblk = (int64_t)gridDim.x;
+  int64_t b = blockIdx.x;
+  if (xcd_remap) b = (b % 8) * (nblk / 8) + b / 8;
+  const int ob = (int)(b % g.cout_blocks);
+  const int cbk = (int)((b / g.cout_blocks) % g.cin_blocks);
+  const int split = (int)(b / ((int64_t)g.cout_blocks * g.cin_blocks));
+  const int cin0 = cbk * kCB, cout0 = ob * kOB;
+  const int64_t k_begin = g.chunks * split / g.splits;
+  const int64_t k_end = g.chunks * (split + 1) / g.splits;
+  const int nk = (int)(k_end - k_begin);
+  const int plane = g.H * g.W;  // < 2^29 (host check)
+
+  f4 acc[16][2];
+#pragma unroll
+  for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
+  if (nk <= 0) {  // empty K-range: zero partial slab (no barrier below)
+    const int co = cout0 + 16 * wave + jj;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        f4* dst = reinterpret_cast<f4*>(
+            part + (((int64_t)split * g.Cin + cin0 + 16 * mb + 4 * kq + r) * g.Cout + co) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    return;
+  }
+
+  // chunk geometry (strip of 2 x 16 output pixels) as an incremental cursor: one division
+  // at the start, then scalar increments; past the end of the K-range a cursor stays on the
+  // last chunk (those loads are re-loads, never consumed)
+  struct Strip { int n, sy, sx, j; };
+  auto strip_at = [&](int j) {
+    const unsigned ck = (unsigned)(k_begin + min(j, nk - 1));
+    const unsigned r = ck / (unsigned)g.strips_x;
+    Strip s;
+    s.sx = __builtin_amdgcn_readfirstlane((int)(ck - r * (unsigned)g.strips_x));
+    s.sy = __builtin_amdgcn_readfirstlane((int)(r % (unsigned)g.strips_y));
+    s.n = __builtin_amdgcn_readfirstlane((int)(r / (unsigned)g.strips_y));
+    s.j = min(j, nk - 1);
+    return s;
+  };
+  auto advance = [&](Strip& s) {
+    if (s.j + 1 >= nk) return;
+    ++s.j;
+    if (++s.sx == g.strips_x) {
+      s.sx = 0;
+      if (++s.sy == g.strips_y) {
+        s.sy = 0;
+        ++s.n;
+      }
+    }
+  };
+
+  // ---- input patch: thread -> (cin c, row py, half h): 2 x f4 interior + 1 halo word
+  const int xp = tid >> 1, xh = tid & 1;
+  const int xc = xp >> 2, xpy = xp & 3;
+  float xv[9];
+  bool xrow_ok, xhalo_ok;
+  Strip xcur = strip_at(0);
+  auto load_x = [&]() {  // patch of chunk xcur, then advance
+    const Strip s = xcur;
+    advance(xcur);
+    const int oy0 = 2 * s.sy, ox0 = 16 * s.sx;
+    const float* base = x + ((int64_t)s.n * g.Cin + cin0) * plane;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base), 0, kCB * plane * 4, 0x00020000);
+    const int iy = oy0 - 1 + xpy;
+    xrow_ok = iy >= 0 && iy < g.H;
+    const int iyc = min(max(iy, 0), g.H - 1);
+    const int hx = xh ? ox0 + 16 : ox0 - 1;
+    xhalo_ok = hx >= 0 && hx < g.W;
+    const int hxc = min(max(hx, 0), g.W - 1);
+    const int rowoff = (xc * plane + iyc * g.W) * 4;
+    using u4 = __attribute__((ext_vector_type(4))) unsigned;
+    const u4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, rowoff + (ox0 + 8 * xh) * 4, 0, 0);
+    const u4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, rowoff + (ox0 + 8 * xh + 4) * 4, 0, 0);
+    const unsigned hv = __builtin_amdgcn_raw_buffer_load_b32(rs, rowoff + hxc * 4, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xv[e] = __uint_as_float(a[e]);
+      xv[4 + e] = __uint_as_float(c[e]);
+    }
+    xv[8] = __uint_as_float(hv);
+  };
+  auto store_x = [&](float* sx) {
+    float* row = sx + xc * kXCS + xpy * kXRS;
+    const float z = xrow_ok ? 1.f : 0.f;
+    *reinterpret_cast<f4*>(row + 4 + 8 * xh) = f4{xv[0] * z, xv[1] * z, xv[2] * z, xv[3] * z};
+    *reinterpret_cast<f4*>(row + 8 + 8 * xh) = f4{xv[4] * z, xv[5] * z, xv[6] * z, xv[7] * z};
+    row[xh ? 20 : 3] = (xrow_ok && xhalo_ok) ? xv[8] : 0.f;
+  };
+
+  // ---- V = B^T d B of one (tile, cin) per thread: c = tid >> 3, tile = tid & 7
+  const int vc = tid >> 3, vt = tid & 7;
+  float d[4][4];
+  auto read_d = [&](const float* sx) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[i][j] = sx[vc * kXCS + i * kXRS + 3 + 2 * vt + j];
+  };
+  auto write_v = [&](float* sv) {
+    float t[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[0][j] = d[0][j] - d[2][j];
+      t[1][j] = d[1][j] + d[2][j];
+      t[2][j] = d[2][j] - d[1][j];
+      t[3][j] = d[1][j] - d[3][j];
+    }
+    f4* dst = reinterpret_cast<f4*>(&sv[vt * kVT + vc * kRec]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
+  };
+
+  // ---- gradient tiles: lane (kq, jj) of wave w needs, per k-step ks, the 2 x 2 tile
+  // (4 ks + kq) of channel cout0 + 16 w + jj
+  const int gco = cout0 + 16 * wave + jj;
+  float2 gq[2][2];  // [ks][row], one chunk ahead
+  Strip gcur = strip_at(0);
+  auto load_g = [&](float2 (&dst)[2][2]) {  // gradient tiles of chunk gcur, then advance
+    const Strip s = gcur;
+    advance(gcur);
+    const float* src = gy + ((int64_t)s.n * g.Cout + gco) * plane + (int64_t)(2 * s.sy) * g.W +
+                       16 * s.sx;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float* p = src + 2 * (4 * ks + kq);
+      dst[ks][0] = *reinterpret_cast<const float2*>(p);
+      dst[ks][1] = *reinterpret_cast<const float2*>(p + g.W);
+    }
+  };
+  // Gbar = A dY A^T with A = [[1,0],[1,1],[1,-1],[0,-1]]: 16 values, position 4 i + j
+  auto gbar = [&](const float2 (&t)[2], f4 (&bq)[4]) {
+    const float a = t[0].x, bb = t[0].y, c = t[1].x, dd = t[1].y;
+    const float rows[4][2] = {{a, bb}, {a + c, bb + dd}, {a - c, bb - dd}, {-c, -dd}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = rows[i][0], q = rows[i][1];
+      bq[i] = f4{p, p + q, p - q, -q};
+    }
+  };
+
+  // ---- prologue
+  float xv0[9], xv1[9];
+  bool ok0r, ok0h, ok1r, ok1h;
+  load_x();
+#pragma unroll
+  for (int e = 0; e < 9; ++e) xv0[e] = xv[e];
+  ok0r = xrow_ok; ok0h = xhalo_ok;
+  load_x();
+#pragma unroll
+  for (int e = 0; e < 9; ++e) xv1[e] = xv[e];
+  ok1r = xrow_ok; ok1h = xhalo_ok;
+  load_x();
+  load_g(gq);
+  {
+    float keep[9];
+    bool kr = xrow_ok, kh = xhalo_ok;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) { keep[e] = xv[e]; xv[e] = xv0[e]; }
+    xrow_ok = ok0r; xhalo_ok = ok0h;
+    store_x(s_x[0]);
+#pragma unroll
+    for (int e = 0; e < 9; ++e) xv[e] = xv1[e];
+    xrow_ok = ok1r; xhalo_ok = ok1h;
+    store_x(s_x[1]);
+#pragma unroll
+    for (int e = 0; e < 9; ++e) xv[e] = keep[e];
+    xrow_ok = kr; xhalo_ok = kh;
+  }
+  __syncthreads();
+  read_d(s_x[0]);
+  write_v(s_v[0]);
+  __syncthreads();
+
+  // step j: MFMAs of chunk j (V in s_v[SB], Gbar from gq); side work: V(j+1) from
+  // s_x[SB^1], patch(j+2) -> s_x[SB], patch(j+3) and gradient(j+1) loads
+  auto step = [&](auto sb_c) {
+    constexpr int SB = decltype(sb_c)::value;
+    const float* sv = s_v[SB];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f4 bq[4];
+      gbar(gq[ks], bq);
+      if (ks == 1) load_g(gq);  // chunk j + 1 (both k-steps' tiles consumed)
+      const int tile = 4 * ks + kq;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks == 0 && mb == 0) read_d(s_x[SB ^ 1]);
+        if (ks == 0 && mb == 1) write_v(s_v[SB ^ 1]);
+        if (ks == 1 && mb == 0) store_x(s_x[SB]);
+        if (ks == 1 && mb == 1) load_x();  // chunk j + 3
+        __builtin_amdgcn_sched_barrier(0);
+        const f4* as = reinterpret_cast<const f4*>(&sv[tile * kVT + (16 * mb + jj) * kRec]);
+        f4 a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = as[q];
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+          acc[p][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p >> 2][p & 3], bq[p >> 2][p & 3],
+                                                            acc[p][mb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  };
+  int j = 0;
+  for (; j + 1 < nk; j += 2) {
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+  }
+  if (j < nk) step(std::integral_constant<int, 0>{});
+
+  const int co = cout0 + 16 * wave + jj;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ci = cin0 + 16 * mb + 4 * kq + r;
+      f4* dst = reinterpret_cast<f4*>(part + (((int64_t)split * g.Cin + ci) * g.Cout + co) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dst[q] = f4{acc[4 * q][mb][r], acc[4 * q + 1][mb][r], acc[4 * q + 2][mb][r],
+                    acc[4 * q + 3][mb][r]};
+    }
+}
+
 // dw[cout][cin] = G^T (sum_s part[s][cin][cout]) G,  G^T = [[1,.5,.5,0],[0,.5,-.5,0],[0,.5,.5,1]]
 __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __restrict__ part,
                                                                 float* __restrict__ dw, int Cin,
@@ -246,7 +504,7 @@ WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
 
 extern "C" int bpk_conv3x3_wino_wgrad_supported(int N, int Cin, int Cout, int H, int W) {
   return N > 0 && Cin > 0 && Cout > 0 && Cin % kCB == 0 && Cout % kOB == 0 && H % 2 == 0 &&
-         W % 16 == 0 && (int64_t)H * W * 4 < (1LL << 31);
+         W % 16 == 0 && (int64_t)H * W * kCB * 4 < (1LL << 31);
 }
 
 extern "C" int64_t bpk_conv3x3_wino_wgrad_workspace_bytes(int N, int Cin, int Cout, int H,
@@ -268,8 +526,17 @@ extern "C" int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino_wgrad: grid too large");
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
-  hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
-                     workspace, g, remap);
+  // the software-pipelined kernel unless BPK_WGRAD_PIPE=0
+  static const int pipe_env = [] {
+    const char* e = getenv("BPK_WGRAD_PIPE");
+    return e ? atoi(e) : 1;
+  }();
+  if (pipe_env)
+    hipLaunchKernelGGL(wino_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
+                       workspace, g, remap);
+  else
+    hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
+                       workspace, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
   hipLaunchKernelGGL(wino_wgrad_reduce_kernel,
