@@ -358,106 +358,145 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
   }
 }
 
-// split backward stage 1: chunk sums of dxhat and dxhat*xhat; dgamma/dbeta via global atomics
-template <int W>
-__global__ __launch_bounds__(256) void gn_bwd_partial(
-    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
-    const float* __restrict__ gamma, const float* __restrict__ beta,
-    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    float* __restrict__ part, float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C,
-    int HW, int G, int splits, int chunk, int act) {
-  __shared__ float sbuf[256 / kWave];
-  const int split = blockIdx.x;
-  const int ng = blockIdx.y;
-  const int n = ng / G;
-  const int g = ng - n * G;
-  const int cpg = C / G;
-  const int S = cpg * HW;
-  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
-  const float mean = mean_in[ng];
-  const float rstd = rstd_in[ng];
-  float la = 0.f, lb = 0.f;
-  const int e_end = min(S, (split + 1) * chunk);
-  int cur_c = -1;
-  float pg = 0.f, pb = 0.f;
-  for (int e = split * chunk + threadIdx.x * W; e < e_end; e += 256 * W) {
-    const int c = g * cpg + e / HW;
-    if (c != cur_c) {
-      if (cur_c >= 0) {
-        if (dgamma_nc) atomicAdd(&dgamma_nc[(int64_t)n * C + cur_c], pg);
-        if (dbeta_nc) atomicAdd(&dbeta_nc[(int64_t)n * C + cur_c], pb);
-      }
-      cur_c = c;
-      pg = 0.f;
-      pb = 0.f;
-    }
-    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
-    const float ga = gamma ? gamma[c] : 1.f;
-    const float be = beta ? beta[c] : 0.f;
-    float xv[W], gv[W];
-    Vec<W>::load(x + base + e, xv);
-    Vec<W>::load(dy + base + e, gv);
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      const float xhat = (xv[q] + b - mean) * rstd;
-      const float dz = gv[q] * act_bwd(xhat * ga + be, act);
-      pg += dz * xhat;
-      pb += dz;
-      la += dz * ga;
-      lb += dz * ga * xhat;
-    }
+// split backward (deterministic, no atomics): the blocks of a group are laid on channel
+// boundaries -- a block covers one slice of one channel plane (HW >= CH) or a run of whole
+// planes (HW < CH) -- so the channel's bias / gamma / beta are loop constants, and the
+// per-channel dgamma / dbeta sums are per-block partials reduced in a fixed order by the
+// apply kernel (float atomics into one address per channel serialise and are not
+// bit-reproducible).
+struct BwdBlk {
+  int c0, nc, h0, h1, s;
+};
+__host__ __device__ inline int bwd_spc(int HW, int CH) { return HW >= CH ? (HW + CH - 1) / CH : 1; }
+__host__ __device__ inline int bwd_bpg(int HW, int cpg, int CH) {
+  if (HW >= CH) return cpg * bwd_spc(HW, CH);
+  const int cpb = CH / HW;
+  return (cpg + cpb - 1) / cpb;
+}
+__device__ inline BwdBlk bwd_block(int bi, int HW, int cpg, int CH) {
+  BwdBlk r;
+  if (HW >= CH) {
+    const int spc = bwd_spc(HW, CH);
+    r.c0 = bi / spc;
+    r.s = bi - r.c0 * spc;
+    r.nc = 1;
+    r.h0 = r.s * CH;
+    r.h1 = min(HW, r.h0 + CH);
+  } else {
+    const int cpb = CH / HW;
+    r.c0 = bi * cpb;
+    r.nc = min(cpb, cpg - r.c0);
+    r.s = 0;
+    r.h0 = 0;
+    r.h1 = HW;
   }
-  if (cur_c >= 0) {
-    if (dgamma_nc) atomicAdd(&dgamma_nc[(int64_t)n * C + cur_c], pg);
-    if (dbeta_nc) atomicAdd(&dbeta_nc[(int64_t)n * C + cur_c], pb);
-  }
-  const float A = block_sum<256>(la, sbuf);
-  const float B = block_sum<256>(lb, sbuf);
-  if (threadIdx.x == 0) {
-    part[((int64_t)ng * splits + split) * 2] = A;
-    part[((int64_t)ng * splits + split) * 2 + 1] = B;
-  }
+  return r;
 }
 
 template <int W>
-__global__ __launch_bounds__(256) void gn_bwd_apply(
+__global__ __launch_bounds__(256) void gn_bwd_partial2(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
     const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    const float* __restrict__ part, float* __restrict__ dx, int C, int HW, int G, int splits,
-    int chunk, int act) {
-  const int split = blockIdx.x;
+    float2* __restrict__ part_ab, float2* __restrict__ part_c, int want_c, int C, int HW, int G,
+    int CH, int act) {
+  __shared__ float sbuf[256 / kWave];
+  const int bi = blockIdx.x, bpg = gridDim.x;
   const int ng = blockIdx.y;
   const int n = ng / G;
   const int g = ng - n * G;
   const int cpg = C / G;
-  const int S = cpg * HW;
-  const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
+  const BwdBlk blk = bwd_block(bi, HW, cpg, CH);
+  const int spc = bwd_spc(HW, CH);
   const float mean = mean_in[ng];
   const float rstd = rstd_in[ng];
-  float A = 0.f, B = 0.f;
-  for (int s = 0; s < splits; ++s) {
-    A += part[((int64_t)ng * splits + s) * 2];
-    B += part[((int64_t)ng * splits + s) * 2 + 1];
-  }
-  A /= (float)S;
-  B /= (float)S;
-  const int e_end = min(S, (split + 1) * chunk);
-  for (int e = split * chunk + threadIdx.x * W; e < e_end; e += 256 * W) {
-    const int c = g * cpg + e / HW;
+  float la = 0.f, lb = 0.f;
+  for (int k = 0; k < blk.nc; ++k) {
+    const int c = g * cpg + blk.c0 + k;
     const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
     const float ga = gamma ? gamma[c] : 1.f;
     const float be = beta ? beta[c] : 0.f;
-    float xv[W], gv[W], o[W];
-    Vec<W>::load(x + base + e, xv);
-    Vec<W>::load(dy + base + e, gv);
+    const int64_t base = ((int64_t)n * C + c) * HW;
+    float pg = 0.f, pb = 0.f;
+    for (int e = blk.h0 + threadIdx.x * W; e < blk.h1; e += 256 * W) {
+      float xv[W], gv[W];
+      Vec<W>::load(x + base + e, xv);
+      Vec<W>::load(dy + base + e, gv);
 #pragma unroll
-    for (int q = 0; q < W; ++q) {
-      const float xhat = (xv[q] + b - mean) * rstd;
-      const float dxhat = gv[q] * act_bwd(xhat * ga + be, act) * ga;
-      o[q] = rstd * (dxhat - A - xhat * B);
+      for (int q = 0; q < W; ++q) {
+        const float xhat = (xv[q] + b - mean) * rstd;
+        const float dz = gv[q] * act_bwd(xhat * ga + be, act);
+        pg += dz * xhat;
+        pb += dz;
+      }
     }
-    Vec<W>::store(dx + base + e, o);
+    la += pb * ga;
+    lb += pg * ga;
+    if (want_c) {
+      const float PG = block_sum<256>(pg, sbuf);
+      const float PB = block_sum<256>(pb, sbuf);
+      if (threadIdx.x == 0) part_c[((int64_t)n * C + c) * spc + blk.s] = make_float2(PG, PB);
+    }
+  }
+  const float A = block_sum<256>(la, sbuf);
+  const float B = block_sum<256>(lb, sbuf);
+  if (threadIdx.x == 0) part_ab[(int64_t)ng * bpg + bi] = make_float2(A, B);
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void gn_bwd_apply2(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const float2* __restrict__ part_ab, const float2* __restrict__ part_c, float* __restrict__ dx,
+    float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C, int HW, int G, int CH,
+    int act) {
+  const int bi = blockIdx.x, bpg = gridDim.x;
+  const int ng = blockIdx.y;
+  const int n = ng / G;
+  const int g = ng - n * G;
+  const int cpg = C / G;
+  const BwdBlk blk = bwd_block(bi, HW, cpg, CH);
+  const int spc = bwd_spc(HW, CH);
+  const float mean = mean_in[ng];
+  const float rstd = rstd_in[ng];
+  float A = 0.f, B = 0.f;
+  for (int i = 0; i < bpg; ++i) {
+    const float2 p = part_ab[(int64_t)ng * bpg + i];
+    A += p.x;
+    B += p.y;
+  }
+  const float S = (float)cpg * (float)HW;
+  A /= S;
+  B /= S;
+  for (int k = 0; k < blk.nc; ++k) {
+    const int c = g * cpg + blk.c0 + k;
+    const float b = bias_nc ? bias_nc[(int64_t)n * C + c] : 0.f;
+    const float ga = gamma ? gamma[c] : 1.f;
+    const float be = beta ? beta[c] : 0.f;
+    const int64_t base = ((int64_t)n * C + c) * HW;
+    for (int e = blk.h0 + threadIdx.x * W; e < blk.h1; e += 256 * W) {
+      float xv[W], gv[W], o[W];
+      Vec<W>::load(x + base + e, xv);
+      Vec<W>::load(dy + base + e, gv);
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const float xhat = (xv[q] + b - mean) * rstd;
+        const float dxhat = gv[q] * act_bwd(xhat * ga + be, act) * ga;
+        o[q] = rstd * (dxhat - A - xhat * B);
+      }
+      Vec<W>::store(dx + base + e, o);
+    }
+    if (blk.s == 0 && threadIdx.x == 0 && (dgamma_nc || dbeta_nc)) {
+      float pg = 0.f, pb = 0.f;
+      for (int i = 0; i < spc; ++i) {
+        const float2 p = part_c[((int64_t)n * C + c) * spc + i];
+        pg += p.x;
+        pb += p.y;
+      }
+      if (dgamma_nc) dgamma_nc[(int64_t)n * C + c] = pg;
+      if (dbeta_nc) dbeta_nc[(int64_t)n * C + c] = pb;
+    }
   }
 }
 
@@ -544,7 +583,10 @@ extern "C" int64_t bpk_group_norm_workspace_bytes(int N, int C, int64_t HW, int 
   if (N <= 0 || G <= 0 || C % G != 0) return 0;
   const int64_t S = (int64_t)(C / G) * HW;
   const int64_t splits = bpk::ceil_div(S, kSplitChunk / 4);  // worst case W = 1
-  return (int64_t)N * G * splits * 3 * (int64_t)sizeof(float);
+  // backward split path: per-block (A, B) partials + per-(channel, slice) (dgamma, dbeta)
+  const int64_t bpg = splits + C / G, spc = bpk::ceil_div(HW, kSplitChunk / 4);
+  const int64_t bwd = ((int64_t)N * G * bpg + (int64_t)N * C * spc) * 2;
+  return std::max<int64_t>((int64_t)N * G * splits * 3, bwd) * (int64_t)sizeof(float);
 }
 
 extern "C" int bpk_group_norm_fwd_f32(const float* x, const float* bias_nc, const float* gamma,
@@ -610,24 +652,27 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
                                     dbeta_nc, N, C, (int)HW, G, act, st);
   }
   BPK_REQUIRE(workspace != nullptr, "group_norm_bwd: split path needs a workspace");
-  float* part = static_cast<float*>(workspace);
-  if (dgamma_nc) (void)hipMemsetAsync(dgamma_nc, 0, sizeof(float) * (size_t)N * C, st);
-  if (dbeta_nc) (void)hipMemsetAsync(dbeta_nc, 0, sizeof(float) * (size_t)N * C, st);
-  dim3 grid(p.splits, N * G);
+  const int cpg = C / G;
+  const int CH = p.chunk;
+  const int bpg = bwd_bpg((int)HW, cpg, CH);
+  float2* part_ab = static_cast<float2*>(workspace);
+  float2* part_c = part_ab + (int64_t)N * G * bpg;
+  const int want_c = (dgamma_nc || dbeta_nc) ? 1 : 0;
+  dim3 grid(bpg, N * G);
   if (p.W == 4) {
-    hipLaunchKernelGGL(gn_bwd_partial<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
-                       mean, rstd, part, dgamma_nc, dbeta_nc, C, (int)HW, G, p.splits, p.chunk,
-                       act);
+    hipLaunchKernelGGL(gn_bwd_partial2<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
+                       mean, rstd, part_ab, part_c, want_c, C, (int)HW, G, CH, act);
     BPK_LAUNCH_CHECK("group_norm_bwd_partial");
-    hipLaunchKernelGGL(gn_bwd_apply<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta, mean,
-                       rstd, part, dx, C, (int)HW, G, p.splits, p.chunk, act);
+    hipLaunchKernelGGL(gn_bwd_apply2<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
+                       mean, rstd, part_ab, part_c, dx, dgamma_nc, dbeta_nc, C, (int)HW, G, CH,
+                       act);
   } else {
-    hipLaunchKernelGGL(gn_bwd_partial<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
-                       mean, rstd, part, dgamma_nc, dbeta_nc, C, (int)HW, G, p.splits, p.chunk,
-                       act);
+    hipLaunchKernelGGL(gn_bwd_partial2<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
+                       mean, rstd, part_ab, part_c, want_c, C, (int)HW, G, CH, act);
     BPK_LAUNCH_CHECK("group_norm_bwd_partial");
-    hipLaunchKernelGGL(gn_bwd_apply<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta, mean,
-                       rstd, part, dx, C, (int)HW, G, p.splits, p.chunk, act);
+    hipLaunchKernelGGL(gn_bwd_apply2<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
+                       mean, rstd, part_ab, part_c, dx, dgamma_nc, dbeta_nc, C, (int)HW, G, CH,
+                       act);
   }
   BPK_LAUNCH_CHECK("group_norm_bwd_apply");
   return BPK_OK;

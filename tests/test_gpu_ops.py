@@ -95,7 +95,8 @@ def test_fused_leaky_relu_grads_f64(hip):
 
 # ------------------------------------------------------------------ GroupNorm + SiLU
 @pytest.mark.parametrize("N,C,H,G", [(2, 64, 16, 16), (3, 128, 32, 32), (2, 256, 64, 32),
-                                      (2, 384, 64, 32), (1, 8, 5, 2), (2, 32, 128, 8)])
+                                      (2, 384, 64, 32), (1, 8, 5, 2), (2, 32, 128, 8),
+                                      (1, 16, 256, 4), (1, 64, 151, 4)])
 @pytest.mark.parametrize("act", [0, 1])
 def test_group_norm_act_fwd_bwd_vs_torch(hip, N, C, H, G, act):
     from op.norm_act import group_norm_act_f
