@@ -103,9 +103,10 @@ def time_kernel(fn, stream, reps=10):
 
 
 def conv_roofline(dev, batch):
-    """Dominant kernel of the score net (74 % of a PC step): the fused Winograd F(2x2,3x3)
-    MFMA conv3x3 (csrc/conv_winograd.hip), measured on its most frequent shape, 128 -> 128
-    channels @ 128x128 (13 per forward).  MFMA-bound.
+    """Dominant kernel of the score net (~75 % of a PC step): the fused, software-pipelined
+    Winograd F(2x2,3x3) MFMA conv3x3 (csrc/conv_winograd.hip wino_f23_pipe_kernel), measured
+    on its most frequent shape, 128 -> 128 channels @ 128x128 (13 per forward, SURVEY 8(a)
+    a11).  MFMA-bound.
 
     achieved = the kernel's algorithmic MFMA FLOPs per launch -- Winograd F(2,3) multiplies
     16 transformed values per 2x2 output tile per (cin, cout), i.e. 4/9 of the direct
@@ -126,10 +127,10 @@ def conv_roofline(dev, batch):
     ach = wino / t / 1e12
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": _pmc_traffic("wino_f23_kernel conv3x3 128->128 @128x128 B=64")
+            "traffic": _pmc_traffic("wino_f23_pipe_kernel conv3x3 128->128 @128x128 B=64")
             if batch == 64 else None,
             "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-            "kernel": "wino_f23_kernel conv3x3 128->128 @128x128 fp32 (hand-written, f32 MFMA)",
+            "kernel": "wino_f23_pipe_kernel conv3x3 128->128 @128x128 fp32 (hand-written, f32 MFMA)",
             "ms_per_launch": round(t * 1e3, 4), "flop_per_launch": wino,
             "direct_equivalent_tflops": round(direct / t / 1e12, 2),
             "miopen_ms_per_launch": round(tm * 1e3, 4),
