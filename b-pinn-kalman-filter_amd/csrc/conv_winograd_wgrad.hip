@@ -214,6 +214,7 @@ constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records
 __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ gy,
                                                                  float* __restrict__ part,
+                                                                 float* __restrict__ part_b,
                                                                  WgradGeo g, int xcd_remap) {
   __shared__ __attribute__((aligned(16))) float s_x[2][kCB * kXCS];   // 2 x 14.3 KB
   __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 20.6 KB
@@ -236,8 +237,13 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
   f4 acc[16][2];
 #pragma unroll
   for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
-  if (nk <= 0) {  // empty K-range: zero partial slab (no barrier below)
+  // bias gradient (sum of dy over n, h, w): the cin-block-0 workgroups add up the gradient
+  // tiles they load anyway; per-(split, cout) partials, reduced with dw
+  const bool want_b = part_b != nullptr && cbk == 0;
+  float bsum = 0.f;
+  if (nk <= 0) {  // empty K-range: zero partial slabs (no barrier below)
     const int co = cout0 + 16 * wave + jj;
+    if (want_b && kq == 0) part_b[(int64_t)split * g.Cout + co] = 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -409,6 +415,7 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
     for (int ks = 0; ks < 2; ++ks) {
       f4 bq[4];
       gbar(gq[ks], bq);
+      if (want_b) bsum += (gq[ks][0].x + gq[ks][0].y) + (gq[ks][1].x + gq[ks][1].y);
       if (ks == 1) load_g(gq);  // chunk j + 1 (both k-steps' tiles consumed)
       const int tile = 4 * ks + kq;
 #pragma unroll
@@ -439,6 +446,11 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
   if (j < nk) step(std::integral_constant<int, 0>{});
 
   const int co = cout0 + 16 * wave + jj;
+  if (want_b) {  // lanes jj, jj + 16, jj + 32, jj + 48 hold one channel's tiles
+    bsum += __shfl_xor(bsum, 16, 64);
+    bsum += __shfl_xor(bsum, 32, 64);
+    if (kq == 0) part_b[(int64_t)split * g.Cout + co] = bsum;
+  }
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -454,9 +466,19 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
 
 // dw[cout][cin] = G^T (sum_s part[s][cin][cout]) G,  G^T = [[1,.5,.5,0],[0,.5,-.5,0],[0,.5,.5,1]]
 __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __restrict__ part,
-                                                                float* __restrict__ dw, int Cin,
+                                                                float* __restrict__ dw,
+                                                                const float* __restrict__ part_b,
+                                                                float* __restrict__ db, int Cin,
                                                                 int Cout, int splits) {
   const int64_t pairs = (int64_t)Cin * Cout;
+  if (db) {  // db[cout] = sum over splits, fixed order
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < Cout;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      float acc = 0.f;
+      for (int sp = 0; sp < splits; ++sp) acc += part_b[(int64_t)sp * Cout + i];
+      db[i] = acc;
+    }
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pairs;
        i += (int64_t)gridDim.x * blockDim.x) {
     f4 u[4] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f},
@@ -511,12 +533,19 @@ extern "C" int64_t bpk_conv3x3_wino_wgrad_workspace_bytes(int N, int Cin, int Co
                                                           int W) {
   if (!bpk_conv3x3_wino_wgrad_supported(N, Cin, Cout, H, W)) return 0;
   const WgradGeo g = make_geo(N, Cin, Cout, H, W);
-  return (int64_t)g.splits * Cin * Cout * 16 * (int64_t)sizeof(float);
+  return ((int64_t)g.splits * Cin * Cout * 16 + (int64_t)g.splits * Cout) * (int64_t)sizeof(float);
 }
 
 extern "C" int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float* dw,
                                           float* workspace, int N, int Cin, int Cout, int H,
                                           int W, void* stream) {
+  return bpk_conv3x3_wino_wgrad_bias_f32(x, gy, dw, nullptr, workspace, N, Cin, Cout, H, W,
+                                         stream);
+}
+
+extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, float* dw,
+                                               float* db, float* workspace, int N, int Cin,
+                                               int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_wgrad_supported(N, Cin, Cout, H, W),
               "conv3x3_wino_wgrad: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin "
               "%% 32, Cout %% 64, H %% 2, W %% 16 == 0)", N, Cin, Cout, H, W);
@@ -531,9 +560,11 @@ extern "C" int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float
     const char* e = getenv("BPK_WGRAD_PIPE");
     return e ? atoi(e) : 1;
   }();
+  float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
+  BPK_REQUIRE(pipe_env || !db, "conv3x3_wino_wgrad: the bias gradient needs the pipelined kernel");
   if (pipe_env)
     hipLaunchKernelGGL(wino_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
-                       workspace, g, remap);
+                       workspace, part_b, g, remap);
   else
     hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
                        workspace, g, remap);
@@ -541,7 +572,7 @@ extern "C" int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float
   const int64_t pairs = (int64_t)Cin * Cout;
   hipLaunchKernelGGL(wino_wgrad_reduce_kernel,
                      dim3((unsigned)std::min<int64_t>(bpk::ceil_div(pairs, 256), 4096)),
-                     dim3(256), 0, st, workspace, dw, Cin, Cout, g.splits);
+                     dim3(256), 0, st, workspace, dw, part_b, db, Cin, Cout, g.splits);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad_reduce");
   return BPK_OK;
 }

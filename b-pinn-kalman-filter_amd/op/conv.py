@@ -109,6 +109,7 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=Fa
 
 
 _WGRAD = os.environ.get("BPK_WINO_WGRAD", "1") != "0"
+_WGRAD_PIPE = os.environ.get("BPK_WGRAD_PIPE", "1") != "0"  # the kernel with the bias gradient
 
 
 def wgrad_supported(x, weight):
@@ -120,9 +121,10 @@ def wgrad_supported(x, weight):
     return bool(lib.bpk_conv3x3_wino_wgrad_supported(N, C, weight.shape[0], H, W))
 
 
-def conv3x3_wgrad_raw(x, gy, wshape):
+def conv3x3_wgrad_raw(x, gy, wshape, bias_grad=False):
     """dw [Cout, Cin, 3, 3] of conv3x3(x, w) for the output gradient gy (Winograd split-K,
-    csrc/conv_winograd_wgrad.hip); == torch.nn.grad.conv2d_weight(x, wshape, gy, padding=1)."""
+    csrc/conv_winograd_wgrad.hip); == torch.nn.grad.conv2d_weight(x, wshape, gy, padding=1).
+    bias_grad=True: returns (dw, db) with db = gy.sum((0, 2, 3)) from the same kernel."""
     x = x.detach().contiguous()
     gy = gy.detach().contiguous()
     N, C, H, W = x.shape
@@ -133,10 +135,11 @@ def conv3x3_wgrad_raw(x, gy, wshape):
     nbytes = lib.bpk_conv3x3_wino_wgrad_workspace_bytes(N, C, Cout, H, W)
     ws = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
     dw = torch.empty((Cout, C, 3, 3), dtype=torch.float32, device=x.device)
-    check(lib.bpk_conv3x3_wino_wgrad_f32(x.data_ptr(), gy.data_ptr(), dw.data_ptr(),
-                                         ws.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)),
-          "conv3x3_wgrad")
-    return dw
+    db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if bias_grad else None
+    check(lib.bpk_conv3x3_wino_wgrad_bias_f32(
+        x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None if db is None else db.data_ptr(),
+        ws.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)), "conv3x3_wgrad")
+    return (dw, db) if bias_grad else dw
 
 
 def conv3x3_small_raw(x, weight, bias=None, pre=None):
@@ -207,12 +210,17 @@ class _Conv3x3(torch.autograd.Function):
                 gx = conv3x3_fwd_raw(gy, wt)
             else:
                 gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            if not torch.is_grad_enabled() and wgrad_supported(x, weight):
+            if not torch.is_grad_enabled() and wgrad_supported(x, weight) and _WGRAD_PIPE:
+                gw, gb = conv3x3_wgrad_raw(x, gy, weight.shape, bias_grad=True)
+                if not want_b:
+                    gb = None
+            elif not torch.is_grad_enabled() and wgrad_supported(x, weight):
                 gw = conv3x3_wgrad_raw(x, gy, weight.shape)
             else:
                 gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if want_b and gb is None:
             gb = gy.sum((0, 2, 3))
         return gx, gw, gb, gs, None
 

@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=6)
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--cifar-steps", type=int, default=6,
+                    help="configs[1] train steps (NCSN++ CIFAR-10 32x32x3, batch 128/GPU); 0: skip")
     ap.add_argument("--pinn-steps", type=int, default=5)
     ap.add_argument("--pinn-warmup", type=int, default=2)
     ap.add_argument("--no-pinn", action="store_true")
@@ -199,6 +201,52 @@ def pinn_batch(c, B, dev, seed=0):
     target = torch.randn(B, 3, n, n, device=dev, generator=g) * 0.5
     return (f1, f2, x.contiguous().requires_grad_(), y.contiguous().requires_grad_(),
             t.requires_grad_(), target)
+
+
+def bench_cifar_train(args, ctx, dev):
+    """configs[1]: NCSN++ continuous VP-SDE CIFAR-10 training (configs/vp/
+    cifar10_ncsnpp_continuous.py: 32x32x3, nf 128, ch_mult (1,2,2,2), 4 res blocks, attention
+    at 16^2), batch 128/GPU, synthetic data; DDP (RCCL gradient all-reduce) for N > 1."""
+    import losses
+    import models  # noqa: F401
+    import sde_lib
+    from configs.vp import cifar10_ncsnpp_continuous
+    from models import utils as mutils
+    from models.ema import ExponentialMovingAverage
+    c = cifar10_ncsnpp_continuous.get_config()
+    c.device = dev
+    c.model.dropout = 0.0
+    torch.manual_seed(0)
+    model = mutils.create_model(c, wrap=False).train()
+    tmodel = model
+    if ctx.world_size > 1:
+        tmodel = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
+                                                           bucket_cap_mb=100)
+    sde = sde_lib.VPSDE(c.model.beta_min, c.model.beta_max, c.model.num_scales)
+    opt = losses.get_optimizer(c, tmodel.parameters())
+    ema = ExponentialMovingAverage(tmodel.parameters(), decay=c.model.ema_rate)
+    state = dict(optimizer=opt, model=tmodel, ema=ema, step=0)
+    step_fn = losses.get_step_fn(sde, train=True, optimize_fn=losses.optimization_manager(c),
+                                 reduce_mean=True, continuous=True)
+    B = c.training.batch_size
+    batch = torch.rand(B, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(ctx.rank))
+    for _ in range(2):
+        step_fn(state, batch)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.cifar_steps):
+        loss = step_fn(state, batch)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
+    return {"cifar_train_steps_per_s": round(args.cifar_steps / dt, 3),
+            "cifar_train_ms_per_step": round(dt / args.cifar_steps * 1e3, 2),
+            "cifar_train_global_batch": B * ctx.world_size,
+            "cifar_train_loss": round(float(loss.item()), 5),
+            "cifar_config": "configs[1]: cifar10_ncsnpp_continuous 32x32x3, batch 128/GPU"}
 
 
 def bench_pinn(args, ctx, dev):
@@ -390,6 +438,11 @@ def main():
                  "train_tflops": round(args.train_steps * B * world * NCSNPP_GFLOP_PER_TRAIN_SAMPLE
                                        / tdt / 1e3, 2)}
 
+    cifar = None
+    if args.cifar_steps > 0 and not args.no_train:
+        log("configs[1] train steps (CIFAR-10 32x32, batch 128)")
+        cifar = bench_cifar_train(args, ctx, dev)
+
     pinn = None
     if not args.no_pinn:
         log("PINN train steps")
@@ -425,6 +478,8 @@ def main():
         }
         if train:
             result.update(train)
+        if cifar:
+            result.update(cifar)
         if pinn:
             result.update(pinn)
         if dps:

@@ -333,6 +333,12 @@ int bpk_conv3x3_wino_wgrad_supported(int N, int Cin, int Cout, int H, int W);
 int64_t bpk_conv3x3_wino_wgrad_workspace_bytes(int N, int Cin, int Cout, int H, int W);
 int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float* dw, float* workspace,
                                int N, int Cin, int Cout, int H, int W, void* stream);
+/* Same, plus the bias gradient db [Cout] = sum of gy over (n, h, w), accumulated from the
+ * gradient tiles the weight-gradient kernel loads anyway (replaces a separate reduction of
+ * gy; deterministic). */
+int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, float* dw, float* db,
+                                    float* workspace, int N, int Cin, int Cout, int H, int W,
+                                    void* stream);
 
 /* 3x3 / stride 1 / pad 1 conv with a small channel count on one side (VALU, HBM-bound):
  * the score networks' conv_in (Cin = image channels, models/ncsnpp.py) and output_skip

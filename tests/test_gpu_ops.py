@@ -306,6 +306,11 @@ def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
     # deterministic: the same inputs give the same bits
     again = conv3x3_wgrad_raw(x.to(hip), gy.to(hip), wt.shape).double().cpu()
     assert torch.equal(out, again)
+    # the bias gradient from the same kernel: dw unchanged, db = sum of gy over (n, h, w)
+    dw2, db = conv3x3_wgrad_raw(x.to(hip), gy.to(hip), wt.shape, bias_grad=True)
+    assert torch.equal(dw2.double().cpu(), out)
+    dref = gy.double().sum((0, 2, 3))
+    assert (db.double().cpu() - dref).abs().max().item() <= 1e-5 * max(1.0, dref.abs().max().item())
     del F
 
 
