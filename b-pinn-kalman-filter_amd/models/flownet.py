@@ -62,7 +62,9 @@ def _lrelu():
 
 
 def _conv3(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1)
+    # layers.Conv2d: nn.Conv2d parameters / state-dict keys, forward dispatched to the native
+    # conv kernels where the shape qualifies (small-channel heads, Winograd), MIOpen otherwise
+    return layers.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1)
 
 
 def _chain(widths, last_act=False):

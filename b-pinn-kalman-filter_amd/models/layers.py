@@ -309,8 +309,8 @@ def ncsn_conv1x1(in_planes, out_planes, stride=1, bias=True, dilation=1, init_sc
 def ncsn_conv3x3(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=1):
     """3x3 conv, PyTorch default init scaled by init_scale (reference layers.py:104-110)."""
     scale = 1e-10 if init_scale == 0 else init_scale
-    conv = nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, bias=bias,
-                     dilation=dilation, padding=padding)
+    conv = Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, bias=bias,
+                  dilation=dilation, padding=padding)
     conv.weight.data *= scale
     if bias:
         conv.bias.data *= scale

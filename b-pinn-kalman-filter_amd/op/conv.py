@@ -173,12 +173,21 @@ class _Conv3x3Small(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             # backward-data = forward conv of gy with the flipped, transposed filter (the
-            # small side moves from Cout to Cin or back: the same kernel pair)
-            wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
-            if not torch.is_grad_enabled() and small_supported(gy, wt):
-                gx = conv3x3_small_raw(gy, wt)
+            # small side moves from Cout to Cin or back: the same kernel pair).  Under
+            # create_graph (the PINN residual's second derivatives) the same op is recorded
+            # with autograd, so higher derivatives stay on these kernels.
+            if torch.is_grad_enabled():
+                wt = weight.flip(2, 3).transpose(0, 1)
+                if small_supported(gy, wt):
+                    gx = _Conv3x3Small.apply(gy, wt.contiguous(), None)
+                else:
+                    gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
             else:
-                gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+                wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
+                if small_supported(gy, wt):
+                    gx = conv3x3_small_raw(gy, wt)
+                else:
+                    gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
         if ctx.needs_input_grad[1]:
             gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:

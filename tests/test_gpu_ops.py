@@ -472,3 +472,27 @@ def test_conv3x3_winograd_gn_partial_statistics(hip, with_bias_nc):
         # an in-place update invalidates the attached statistics
         y.add_(1.0)
         assert gn_partials(y) is None
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 2), (4, 64)])
+def test_conv3x3_small_channel_double_backward(hip, cin, cout):
+    """Second derivatives through the small-channel conv (the PINN residual differentiates
+    the networks twice): grad of <d out/d x . v> w.r.t. x and w vs MIOpen's (2e-5 relative)."""
+    from op.conv import conv3x3
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x0 = torch.randn(2, cin, 16, 24, generator=g)
+    w0 = torch.randn(cout, cin, 3, 3, generator=g) * 0.2
+    go = torch.randn(2, cout, 16, 24, generator=g).to(hip)
+    v = torch.randn(2, cin, 16, 24, generator=g).to(hip)
+
+    def second(fn):
+        x = x0.to(hip).requires_grad_()
+        w = w0.to(hip).requires_grad_()
+        y = fn(x, w)
+        (gx,) = torch.autograd.grad(y, x, go, create_graph=True)
+        return torch.autograd.grad((gx * v).sum() + (gx * gx).sum(), (x, w))
+
+    got = second(lambda x, w: conv3x3(torch.tanh(x), w))
+    ref = second(lambda x, w: F.conv2d(torch.tanh(x), w, padding=1))
+    for a, r in zip(got, ref):
+        assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
