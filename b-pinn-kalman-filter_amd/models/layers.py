@@ -77,17 +77,22 @@ _WINO_ENABLED = os.environ.get("BPK_CONV", "winograd") != "miopen"
 _GN_STATS = os.environ.get("BPK_GN_STATS", "1") != "0"
 
 
-def _wino_eligible(x, conv: nn.Conv2d):
+def _is_3x3(x, conv: nn.Conv2d):
     return (_WINO_ENABLED and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
-            and x.is_cuda and conv_op.supported(x, conv.weight))
+            and x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32)
+
+
+def _wino_eligible(x, conv: nn.Conv2d):
+    """a 3x3 conv one of the native kernels (Winograd MFMA, small-channel) runs"""
+    return _is_3x3(x, conv) and conv_op.supported(x, conv.weight)
 
 
 def conv2d(x, conv: nn.Conv2d, bias=True):
     """conv(x) -- the fused Winograd F(2x2,3x3) MFMA kernel (op.conv) for every 3x3 /
     stride-1 / pad-1 conv whose shape it supports, MIOpen (F.conv2d) otherwise."""
     b = conv.bias if bias else None
-    if _wino_eligible(x, conv):
+    if _is_3x3(x, conv):  # native kernels where they fit; every derivative order on 3x3 ops
         return conv_op.conv3x3(x, conv.weight, b)
     return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 import os
 
 import torch
+import torch.nn.functional as F
 
 from ._lib import check, lib, require_hip, stream_ptr
 
@@ -160,48 +161,64 @@ def conv3x3_small_raw(x, weight, bias=None, pre=None):
     return y
 
 
-class _Conv3x3Small(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
-        return conv3x3_small_raw(x, weight, bias)
+def _flip_t(w):
+    """[Cout, Cin, 3, 3] -> the flipped, transposed filter [Cin, Cout, 3, 3]: backward-data of
+    a 3x3 / stride-1 / pad-1 conv is the forward conv of the output gradient with it."""
+    return w.flip(2, 3).transpose(0, 1)
 
-    @staticmethod
-    def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            # backward-data = forward conv of gy with the flipped, transposed filter (the
-            # small side moves from Cout to Cin or back: the same kernel pair).  Under
-            # create_graph (the PINN residual's second derivatives) the same op is recorded
-            # with autograd, so higher derivatives stay on these kernels.
-            if torch.is_grad_enabled():
-                wt = weight.flip(2, 3).transpose(0, 1)
-                if small_supported(gy, wt):
-                    gx = _Conv3x3Small.apply(gy, wt.contiguous(), None)
-                else:
-                    gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
-            else:
-                wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
-                if small_supported(gy, wt):
-                    gx = conv3x3_small_raw(gy, wt)
-                else:
-                    gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
-        if ctx.needs_input_grad[1]:
-            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = gy.sum((0, 2, 3))
-        return gx, gw, gb
+
+def _fwd_impl(x, w, bias=None, skip=None, div=1.0):
+    """conv(x, w) + bias [-> (skip + .) / div] without autograd: Winograd MFMA kernel,
+    small-channel kernel, or MIOpen for the other shapes."""
+    w = w.detach().contiguous()
+    if wino_supported(x, w):
+        return conv3x3_fwd_raw(x.detach(), w, bias, skip, div)
+    with torch.no_grad():
+        if small_supported(x, w):
+            y = conv3x3_small_raw(x.detach(), w, bias)
+        else:
+            y = F.conv2d(x.detach(), w, None if bias is None else bias.detach(), padding=1)
+        if skip is not None:
+            from .norm_act import residual_rescale
+            y = residual_rescale(skip.detach(), y, None, div)
+    return y
+
+
+def _wgrad_impl(x, gy, wshape, want_b):
+    """(dw, db or None) without autograd: the Winograd weight gradient (+ bias) when the
+    shape qualifies, MIOpen backward-weights otherwise."""
+    if wgrad_supported(x, gy.new_empty(wshape)):
+        if _WGRAD_PIPE:
+            dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
+            return dw, (db if want_b else None)
+        dw = conv3x3_wgrad_raw(x, gy, wshape)
+    else:
+        with torch.no_grad():
+            dw = torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), padding=1)
+    return dw, (gy.detach().sum((0, 2, 3)) if want_b else None)
+
+
+def _conv_any(x, w):
+    """conv3x3(x, w) recorded for autograd when grad mode is on (higher derivatives), else
+    the raw kernels."""
+    if torch.is_grad_enabled():
+        return _Conv3x3.apply(x, w.contiguous(), None, None, 1.0)
+    return _fwd_impl(x, w)
 
 
 class _Conv3x3(torch.autograd.Function):
+    """y = (skip + conv3x3(x, w) + bias) / div (skip optional).  Its backward is written in
+    terms of this op and _Wgrad3x3, both differentiable again, so second and higher
+    derivatives (the PINN residual, create_graph=True) stay on 3x3 convs and weight
+    gradients -- never on the batch/channel-swapped 'convolutions' with H x W kernels that
+    a generic double backward of a convolution produces."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, skip, div):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.div = float(div)
-        return conv3x3_fwd_raw(x, weight, bias, skip, div)
+        return _fwd_impl(x, weight, bias, skip, div)
 
     @staticmethod
     def backward(ctx, gy):
@@ -211,27 +228,39 @@ class _Conv3x3(torch.autograd.Function):
             gy = gy / ctx.div
         if ctx.needs_input_grad[3]:
             gs = gy
-        if ctx.needs_input_grad[0]:
-            # backward-data of a 3x3 / stride-1 / pad-1 conv is the forward conv of gy with
-            # the flipped, transposed filter: the Winograd kernel when the shape qualifies
-            wt = weight.detach().flip(2, 3).transpose(0, 1).contiguous()
-            if not torch.is_grad_enabled() and wino_supported(gy, wt):
-                gx = conv3x3_fwd_raw(gy, wt)
-            else:
-                gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1]:
-            if not torch.is_grad_enabled() and wgrad_supported(x, weight) and _WGRAD_PIPE:
-                gw, gb = conv3x3_wgrad_raw(x, gy, weight.shape, bias_grad=True)
-                if not want_b:
-                    gb = None
-            elif not torch.is_grad_enabled() and wgrad_supported(x, weight):
-                gw = conv3x3_wgrad_raw(x, gy, weight.shape)
-            else:
-                gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
-        if want_b and gb is None:
-            gb = gy.sum((0, 2, 3))
+        if ctx.needs_input_grad[0]:
+            gx = _conv_any(gy, _flip_t(weight))
+        if torch.is_grad_enabled():
+            if ctx.needs_input_grad[1]:
+                gw = _Wgrad3x3.apply(x, gy, tuple(weight.shape))
+            if want_b:
+                gb = gy.sum((0, 2, 3))
+        elif ctx.needs_input_grad[1] or want_b:
+            dw, gb = _wgrad_impl(x, gy, tuple(weight.shape), want_b)
+            gw = dw if ctx.needs_input_grad[1] else None
         return gx, gw, gb, gs, None
+
+
+class _Wgrad3x3(torch.autograd.Function):
+    """dw = sum over (n, p) of gy[n, co, p] x[n, ci, p + (r, s)] (the weight gradient of the
+    3x3 / pad-1 conv).  Linear in x and in gy: for an incoming ggw,
+    d/dx = conv3x3(gy, flip_t(ggw)) and d/dgy = conv3x3(x, ggw)."""
+
+    @staticmethod
+    def forward(ctx, x, gy, wshape):
+        ctx.save_for_backward(x, gy)
+        return _wgrad_impl(x, gy, wshape, False)[0]
+
+    @staticmethod
+    def backward(ctx, ggw):
+        x, gy = ctx.saved_tensors
+        gx = ggy = None
+        if ctx.needs_input_grad[0]:
+            gx = _conv_any(gy, _flip_t(ggw))
+        if ctx.needs_input_grad[1]:
+            ggy = _conv_any(x, ggw)
+        return gx, ggy, None
 
 
 def _needs_grad(*ts):
@@ -244,25 +273,28 @@ def _inference_only(*ts):
 
 
 def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
-    """F.conv2d(x, weight, bias, padding=1), or the residual-block tail
+    """F.conv2d(x, weight, bias, padding=1) for any fp32 NCHW HIP operands (native kernels
+    where the shape qualifies, MIOpen otherwise; every derivative order on 3x3 convs and
+    weight gradients), or the residual-block tail
     (skip + conv2d(x, weight, bias)) / div fused into the same launch.  stats=True (inference,
     Winograd path): GroupNorm partial statistics of the output ride along (gn_partials).  With `pre`
     ([N, Cin, 2] from op.norm_act.group_norm_affine) the convolved tensor is
     silu(x * s + t) = act(GroupNorm(x + b)) -- inference only (no autograd)."""
     require_hip(x, weight, bias, skip, pre, what="conv3x3")
-    if small_supported(x, weight) and (pre is None or weight.shape[0] <= 4):
-        if pre is not None:
-            _inference_only(x, weight, bias, skip)
-            y = conv3x3_small_raw(x, weight, bias, pre)
-        else:
-            y = _Conv3x3Small.apply(x, weight, bias)
-        if skip is not None:
-            from .norm_act import residual_rescale
-            y = residual_rescale(skip, y, None, div)
-        return y
-    if not wino_supported(x, weight):
-        raise RuntimeError(f"conv3x3: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
-    if pre is not None or (stats and not _needs_grad(x, weight, bias, skip)):
+    if not _shape_ok(x, weight):
+        raise RuntimeError(f"conv3x3: bad operands {tuple(x.shape)} x {tuple(weight.shape)}")
+    if pre is not None:
         _inference_only(x, weight, bias, skip)
+        if small_supported(x, weight) and weight.shape[0] <= 4:
+            y = conv3x3_small_raw(x, weight, bias, pre)
+            if skip is not None:
+                from .norm_act import residual_rescale
+                y = residual_rescale(skip, y, None, div)
+            return y
+        if not wino_supported(x, weight):
+            raise RuntimeError(f"conv3x3(pre=...): unsupported shape {tuple(x.shape)} x "
+                               f"{tuple(weight.shape)}")
         return conv3x3_fwd_raw(x, weight, bias, skip, div, pre, stats)
+    if stats and wino_supported(x, weight) and not _needs_grad(x, weight, bias, skip):
+        return conv3x3_fwd_raw(x, weight, bias, skip, div, None, stats)
     return _Conv3x3.apply(x, weight, bias, skip, div)

@@ -496,3 +496,35 @@ def test_conv3x3_small_channel_double_backward(hip, cin, cout):
     ref = second(lambda x, w: F.conv2d(torch.tanh(x), w, padding=1))
     for a, r in zip(got, ref):
         assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(64, 128, (16, 32)), (16, 32, (12, 20)), (64, 32, (16, 16))])
+def test_conv3x3_double_backward_any_shape(hip, cin, cout, hw):
+    """Second derivatives through conv3x3 for Winograd-eligible (64 -> 128) and MIOpen-fallback
+    shapes: the backward is expressed in conv3x3 / weight-gradient ops that are themselves
+    differentiable; grads of a function of (dL/dx, dL/dw) w.r.t. x and w vs F.conv2d's
+    (2e-5 relative)."""
+    from op.conv import conv3x3
+    g = torch.Generator().manual_seed(cin + cout)
+    x0 = torch.randn(2, cin, *hw, generator=g)
+    w0 = torch.randn(cout, cin, 3, 3, generator=g) * 0.1
+    b0 = torch.randn(cout, generator=g)
+    go = torch.randn(2, cout, *hw, generator=g).to(hip)
+    v = torch.randn(2, cin, *hw, generator=g).to(hip)
+
+    def second(fn):
+        x = x0.to(hip).requires_grad_()
+        w = w0.to(hip).requires_grad_()
+        b = b0.to(hip).requires_grad_()
+        y = fn(torch.tanh(x), w, b)
+        gx, gw = torch.autograd.grad(y, (x, w), go, create_graph=True)
+        return torch.autograd.grad((gx * v).sum() + (gw * gw).sum() + (gx * gx).sum(), (x, w, b),
+                                   allow_unused=True)
+
+    got = second(lambda x, w, b: conv3x3(x, w, b))
+    ref = second(lambda x, w, b: F.conv2d(x, w, b, padding=1))
+    for a, r in zip(got, ref):
+        if r is None:
+            assert a is None or a.abs().max().item() == 0
+            continue
+        assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
