@@ -78,6 +78,7 @@ struct WinoGeo {
   int N, Cin, Cout, H, W;
   int regions_x, regions_y, cout_blocks;
   float div;  // fused residual: y = (skip + (conv + bias)) / div when skip != nullptr
+  int C1;     // input channels [0, C1) from x, [C1, Cin) from x2 (pipelined kernel only)
 };
 
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
@@ -398,7 +399,7 @@ template <int NB, bool PRE>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    float2* __restrict__ stats, WinoGeo g, int xcd_remap) {
+    float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2) {
   constexpr int kWN = 16 * NB;  // couts per wave
   constexpr int kPatch = kCK * kPR * kPCp;
   __shared__ float s_patch_raw[2][kPatch];                                  // 2 x 5.9 KB
@@ -433,15 +434,21 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int64_t plane = (int64_t)g.H * g.W;
-  const float* xn = x + (int64_t)n * g.Cin * plane;
+  const int C2 = g.Cin - g.C1;
+  const float* xn = x + (int64_t)n * g.C1 * plane;
   const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
   const int kq = lane >> 4, jj = lane & 15;
   const int nch = g.Cin / kCK;
 
   // Global loads go through buffer descriptors (base in SGPRs, 32-bit per-lane offsets,
   // the chunk offset in soffset): no 64-bit address registers next to the accumulators.
+  // Two sources (the up path's [h, skip] without their concatenation): channels [0, C1)
+  // from x, [C1, Cin) from x2; a chunk never straddles (C1 % 8 == 0).
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xn), 0, (int)(g.Cin * plane * 4), 0x00020000);
+      const_cast<float*>(xn), 0, (int)(g.C1 * plane * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(C2 > 0 ? x2 + (int64_t)n * C2 * plane : xn), 0,
+      (int)((C2 > 0 ? C2 : g.C1) * plane * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
 
@@ -464,11 +471,13 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   }
   float pv[kCK];
   auto load_patch = [&](int k) {
-    const int soff = (min(k, nch - 1) * kCK) * (int)plane * 4;
+    const int cc = min(k, nch - 1) * kCK;
+    const bool second = cc >= g.C1;
+    const int soff = (second ? cc - g.C1 : cc) * (int)plane * 4;
 #pragma unroll
     for (int c = 0; c < kCK; ++c)
-      pv[c] = __uint_as_float(
-          __builtin_amdgcn_raw_buffer_load_b32(xrs, poff, soff + c * (int)plane * 4, 0));
+      pv[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          second ? xrs2 : xrs, poff, soff + c * (int)plane * 4, 0));
   };
   auto store_patch_from = [&](const float* src, float* sp, int k) {
     const int c0 = min(k, nch - 1) * kCK;
@@ -943,11 +952,14 @@ extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W
          W % kOutCols == 0;
 }
 
-extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const float* U,
-                                       const float* bias, const float* skip, float div, float* y,
-                                       float* stats, int N, int Cin, int Cout, int H, int W,
-                                       void* stream) {
+extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, const float* pre,
+                                       const float* U, const float* bias, const float* skip,
+                                       float div, float* y, float* stats, int N, int Cin,
+                                       int Cout, int H, int W, void* stream) {
   float2* stats2 = reinterpret_cast<float2*>(stats);
+  if (!x2) C1 = Cin;
+  BPK_REQUIRE(C1 > 0 && C1 <= Cin && C1 % kCK == 0,
+              "conv3x3_wino: bad channel split C1=%d of Cin=%d", C1, Cin);
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
               "Cout %% 64, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
@@ -970,8 +982,8 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const f
     return e ? atoi(e) : 0;
   }();
   if (pipe_env == 1 && (persist_env == 2 || (persist_env == 1 && pre)) && Cin % (2 * kCK) == 0 &&
-      !stats) {
-    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div};
+      !stats && !x2) {
+    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div, Cin};
     const int64_t items = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
     // as many workgroups as are resident at once (2 per CU): more would run as a second,
     // mostly idle wave of workgroups
@@ -996,10 +1008,12 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const f
     BPK_LAUNCH_CHECK("conv3x3_wino_persist");
     return BPK_OK;
   }
+  BPK_REQUIRE(!x2 || (pipe_env && (!pre || Cin <= kPreMaxCin)),
+              "conv3x3_wino: a second input source needs the pipelined kernel");
   if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
     // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup
     const int pnb = (pipe_env == 2 && Cout % 128 == 0) ? 2 : 1;
-    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * pnb), div};
+    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * pnb), div, C1};
     const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
     BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
     const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -1007,7 +1021,7 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const f
     hipStream_t st = bpk::as_stream(stream);
 #define WINO_PIPE(NB_, PRE_)                                                                  \
   hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, \
-                     x, U, bias, skip, pre2, y, stats2, g, remap)
+                     x, U, bias, skip, pre2, y, stats2, g, remap, x2)
     if (pnb == 2) {
       if (pre) WINO_PIPE(2, true); else WINO_PIPE(2, false);
     } else {
@@ -1018,7 +1032,7 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const f
     return BPK_OK;
   }
   const int nb = (Cout % 128 == 0 && nb_env == 2) ? 2 : 1;
-  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div};
+  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div, Cin};
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -1040,8 +1054,8 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const f
 extern "C" int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U,
                                         const float* bias, const float* skip, float div, float* y,
                                         int N, int Cin, int Cout, int H, int W, void* stream) {
-  return bpk_conv3x3_wino_ex_f32(x, pre, U, bias, skip, div, y, nullptr, N, Cin, Cout, H, W,
-                                 stream);
+  return bpk_conv3x3_wino_ex_f32(x, nullptr, Cin, pre, U, bias, skip, div, y, nullptr, N, Cin,
+                                 Cout, H, W, stream);
 }
 
 extern "C" int bpk_conv3x3_wino_residual_f32(const float* x, const float* U, const float* bias,

@@ -210,6 +210,40 @@ class ResnetBlockBigGANpp(nn.Module):
                     else up_or_down_sampling.naive_downsample_2d(t, factor=2))
         return t
 
+    def forward_pair(self, x1, x2, temb=None):
+        """forward(torch.cat([x1, x2], 1), temb) -- the up path's skip concatenation -- at
+        inference without building the concatenation: GroupNorm_0 from the parts' partial
+        statistics, Conv_0 reading both sources (Winograd), the 1x1 skip projection as one
+        two-source MFMA GEMM.  Falls back to the concatenation when a piece does not fit."""
+        from op import conv as conv_op
+        from op.norm_act import group_norm_affine_partials
+        p1, p2 = conv_op.gn_partials(x1), conv_op.gn_partials(x2)
+        C1, C = x1.shape[1], x1.shape[1] + x2.shape[1]
+        ok = (layers.fused_inference_ok(self, x1, self.act) and not (self.up or self.down)
+              and hasattr(self, "Conv_2") and p1 is not None and p2 is not None
+              and p1[1:] == p2[1:] and C1 % 8 == 0
+              and x1.dtype == torch.float32 and self.Conv_0.weight.shape[1] == C
+              and bool(conv_op.lib.bpk_conv3x3_wino_supported(
+                  x1.shape[0], C, self.Conv_0.out_channels, x1.shape[2], x1.shape[3]))
+              and conv_op.gemm1x1_supported(x1, self.Conv_2.weight, x2))
+        if not ok:
+            return self.forward(layers.cat_channels(x1, x2), temb)
+        ss = group_norm_affine_partials((torch.cat([p1[0], p2[0]], 1), p1[1], p1[2]),
+                                        x1.shape[0], C, self.GroupNorm_0)
+        h = conv_op.conv3x3_pair(x1, x2, self.Conv_0.weight, pre=ss,
+                                 stats=layers._GN_STATS)
+        bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
+        if temb is not None:
+            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+        bias = self.Conv_1.bias + self.Conv_2.bias
+        x = conv_op.conv1x1(x1, self.Conv_2.weight, None, x2)
+        div = np.sqrt(2.) if self.skip_rescale else 1.0
+        out = layers.gn_silu_conv(h, self.GroupNorm_1, self.Conv_1, bias_nc, bias, x, div)
+        if out is not None:
+            return out
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        return layers.conv_residual(h, self.Conv_1, bias, x, div, stats=True)
+
     def forward(self, x, temb=None):
         fused = layers.fused_inference_ok(self, x, self.act)
         h = None

@@ -10,6 +10,7 @@ hipGraph.
 from __future__ import annotations
 
 import functools
+import os
 
 import numpy as np
 import torch
@@ -19,6 +20,8 @@ from op.norm_act import residual_rescale
 
 from . import layers, layerspp, utils
 
+# up-path skip concatenations read as two sources at inference (BPK_PAIR=0: torch.cat)
+_PAIR = os.environ.get("BPK_PAIR", "1") != "0"
 conv3x3 = layerspp.conv3x3
 default_initializer = layers.default_init
 _SQRT2 = np.sqrt(2.)
@@ -240,7 +243,11 @@ class NCSNpp(nn.Module):
             elif kind == "h_from_top":
                 h = hs[-1]
             elif kind == "res_cat":
-                h = mods[step[1]](layers.cat_channels(h, hs.pop()), temb)
+                blk = mods[step[1]]
+                if hasattr(blk, "forward_pair") and _PAIR:
+                    h = blk.forward_pair(h, hs.pop(), temb)
+                else:
+                    h = blk(layers.cat_channels(h, hs.pop()), temb)
             elif kind == "pyr_head":
                 pyramid = self._gn_act_conv(h, mods[step[1]], mods[step[2]])
             elif kind == "pyr_out_skip":

@@ -78,13 +78,18 @@ def attach_gn_partials(t, part, R, cnt=GN_PART_COUNT):
     return t
 
 
-def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
+def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False, x2=None):
     """conv(a, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch),
     where a = x, or silu(x * s + t) with pre[n, c] = (s, t) (GroupNorm+SiLU fused in).
     stats=True also writes the GroupNorm partial statistics of the output (attached to it,
     see gn_partials) so the next GroupNorm skips its statistics pass."""
     x = x.contiguous()
-    N, C, H, W = x.shape
+    N, C1, H, W = x.shape
+    C = C1 if x2 is None else C1 + x2.shape[1]
+    if x2 is not None:
+        x2 = x2.contiguous()
+        if x2.shape[0] != N or tuple(x2.shape[2:]) != (H, W) or C1 % 8:
+            raise RuntimeError(f"conv3x3: second source {tuple(x2.shape)} vs {tuple(x.shape)}")
     Cout = weight.shape[0]
     U = filter_transform(weight)
     y = torch.empty((N, Cout, H, W), dtype=x.dtype, device=x.device)
@@ -100,7 +105,8 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=Fa
         R = (H // 8) * (W // 16)
         part = torch.empty((N, Cout, R, 2), dtype=torch.float32, device=x.device)
     check(lib.bpk_conv3x3_wino_ex_f32(
-        x.data_ptr(), None if pr is None else pr.data_ptr(), U.data_ptr(),
+        x.data_ptr(), None if x2 is None else x2.data_ptr(), C1,
+        None if pr is None else pr.data_ptr(), U.data_ptr(),
         None if b is None else b.data_ptr(), None if sk is None else sk.data_ptr(), float(div),
         y.data_ptr(), None if part is None else part.data_ptr(), N, C, Cout, H, W,
         stream_ptr(x.device)), "conv3x3_wino")
@@ -272,6 +278,19 @@ def _inference_only(*ts):
         raise RuntimeError("conv3x3(pre=...) is inference-only")
 
 
+def conv3x3_pair(x, x2, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
+    """conv3x3 of the channel concatenation [x, x2] (inference, Winograd kernel) without
+    building it; pre / stats as conv3x3."""
+    require_hip(x, x2, weight, bias, skip, pre, what="conv3x3_pair")
+    _inference_only(x, x2, weight, bias, skip)
+    N, C1, H, W = x.shape
+    if not (_shape_ok(x, weight[:, :C1]) and C1 % 8 == 0 and bool(lib.bpk_conv3x3_wino_supported(
+            N, C1 + x2.shape[1], weight.shape[0], H, W)) and weight.shape[1] == C1 + x2.shape[1]):
+        raise RuntimeError(f"conv3x3_pair: unsupported shapes {tuple(x.shape)}, "
+                           f"{tuple(x2.shape)} x {tuple(weight.shape)}")
+    return conv3x3_fwd_raw(x, weight, bias, skip, div, pre, stats, x2=x2)
+
+
 def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
     """F.conv2d(x, weight, bias, padding=1) for any fp32 NCHW HIP operands (native kernels
     where the shape qualifies, MIOpen otherwise; every derivative order on 3x3 convs and
@@ -298,3 +317,38 @@ def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
     if stats and wino_supported(x, weight) and not _needs_grad(x, weight, bias, skip):
         return conv3x3_fwd_raw(x, weight, bias, skip, div, None, stats)
     return _Conv3x3.apply(x, weight, bias, skip, div)
+
+
+def gemm1x1_supported(x, weight, x2=None):
+    """The MFMA 1x1-conv GEMM (csrc/gemm_nchw.hip) runs conv1x1([x, x2], weight)."""
+    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4 or not x.is_cuda:
+        return False
+    N, K1, H, W = x.shape
+    K2 = 0 if x2 is None else x2.shape[1]
+    if x2 is not None and (x2.shape[0] != N or tuple(x2.shape[2:]) != (H, W)):
+        return False
+    if weight.shape[1] != K1 + K2 or weight.numel() != weight.shape[0] * (K1 + K2):
+        return False
+    return bool(lib.bpk_gemm_nchw_supported(N, weight.shape[0], H * W, K1, K2))
+
+
+def conv1x1(x, weight, bias=None, x2=None):
+    """1x1 conv of NCHW x (or of the channel concatenation [x, x2], without building it)
+    with weight [Cout, Cin(, 1, 1)] (+ bias): the MFMA GEMM kernel.  Inference only."""
+    require_hip(x, weight, bias, x2, what="conv1x1")
+    if not gemm1x1_supported(x, weight, x2):
+        raise RuntimeError(f"conv1x1: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
+    _inference_only(x, weight, bias, x2)
+    x = x.contiguous()
+    x2 = None if x2 is None else x2.contiguous()
+    N, K1, H, W = x.shape
+    K2 = 0 if x2 is None else x2.shape[1]
+    M = weight.shape[0]
+    w = weight.detach().reshape(M, K1 + K2).contiguous()
+    b = None if bias is None else bias.detach().contiguous()
+    y = torch.empty((N, M, H, W), dtype=torch.float32, device=x.device)
+    check(lib.bpk_gemm_nchw_f32(w.data_ptr(), K1 + K2, x.data_ptr(), K1,
+                                None if x2 is None else x2.data_ptr(), K2,
+                                None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
+                                stream_ptr(x.device)), "conv1x1")
+    return y

@@ -83,6 +83,22 @@ def group_norm_act_f(x, num_groups, weight, bias, eps, act=ACT_SILU, bias_nc=Non
     return _GroupNormAct.apply(x, bias_nc, weight, bias, num_groups, eps, act)
 
 
+def group_norm_affine_partials(part, N, C, gn: torch.nn.GroupNorm, bias_nc=None):
+    """(s, t) [N, C, 2] from partial statistics (part [N, C, R, 2], R, cnt) -- e.g. those of
+    a channel concatenation assembled from its parts' -- without touching the tensor."""
+    pt, R, cnt = part
+    ss = torch.empty((N, C, 2), device=pt.device, dtype=torch.float32)
+    bnc = bias_nc.contiguous() if bias_nc is not None else None
+    w = gn.weight if gn.affine else None
+    b = gn.bias if gn.affine else None
+    check(lib.bpk_group_norm_affine_partials_f32(
+        pt.data_ptr(), R, cnt, bnc.data_ptr() if bnc is not None else None,
+        w.detach().data_ptr() if w is not None else None,
+        b.detach().data_ptr() if b is not None else None, ss.data_ptr(), N, C,
+        gn.num_groups, float(gn.eps), stream_ptr(pt.device)), "group_norm_affine_partials")
+    return ss
+
+
 def group_norm_affine(x, gn: torch.nn.GroupNorm, bias_nc=None):
     """Per-(n, c) (scale, shift) [N, C, 2] with act(GN(x + bias_nc)) == act(x * s + t):
     the statistics pass of GroupNorm alone (one read of x), for convolutions that apply the
@@ -91,18 +107,7 @@ def group_norm_affine(x, gn: torch.nn.GroupNorm, bias_nc=None):
     from .conv import gn_partials
     part = gn_partials(x)
     if part is not None:  # statistics from the producing conv's epilogue: no pass over x
-        pt, R, cnt = part
-        N, C = x.shape[:2]
-        ss = torch.empty((N, C, 2), device=x.device, dtype=torch.float32)
-        bnc = bias_nc.contiguous() if bias_nc is not None else None
-        w = gn.weight if gn.affine else None
-        b = gn.bias if gn.affine else None
-        check(lib.bpk_group_norm_affine_partials_f32(
-            pt.data_ptr(), R, cnt, bnc.data_ptr() if bnc is not None else None,
-            w.detach().data_ptr() if w is not None else None,
-            b.detach().data_ptr() if b is not None else None, ss.data_ptr(), N, C,
-            gn.num_groups, float(gn.eps), stream_ptr(x.device)), "group_norm_affine_partials")
-        return ss
+        return group_norm_affine_partials(part, x.shape[0], x.shape[1], gn, bias_nc)
     x = x.contiguous()
     N, C = x.shape[:2]
     HW = x.numel() // max(N * C, 1)

@@ -319,10 +319,13 @@ int bpk_conv3x3_wino_pre_f32(const float* x, const float* pre, const float* U, c
 /* Same, and -- stats != NULL -- the GroupNorm partial statistics of the stored output:
  * stats [N, Cout, (H/8) * (W/16), 2] = (mean, M2) of each channel over each 8 x 16 pixel
  * region (bpk_group_norm_affine_partials_f32 turns them into the next GroupNorm's affine
- * form without a statistics pass over y). */
-int bpk_conv3x3_wino_ex_f32(const float* x, const float* pre, const float* U, const float* bias,
-                            const float* skip, float div, float* y, float* stats, int N, int Cin,
-                            int Cout, int H, int W, void* stream);
+ * form without a statistics pass over y).  x2 != NULL: the input is the channel
+ * concatenation [x (C1 channels), x2 (Cin - C1 channels)] without building it (C1 % 8 == 0;
+ * the up path's torch.cat([h, hs.pop()]) in models/ncsnpp.py). */
+int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, const float* pre,
+                            const float* U, const float* bias, const float* skip, float div,
+                            float* y, float* stats, int N, int Cin, int Cout, int H, int W,
+                            void* stream);
 /* Weight gradient of the same conv (the backward-filter convolution cuDNN / MIOpen runs
  * for nn.Conv2d's autograd): dw [Cout, Cin, 3, 3] = d(sum y * gy)/dw for x [N, Cin, H, W],
  * gy [N, Cout, H, W].  Winograd F(2x2,3x3): per transform position a split-K GEMM
@@ -350,6 +353,17 @@ int bpk_conv3x3_small_supported(int N, int Cin, int Cout, int H, int W);
 int bpk_conv3x3_small_f32(const float* x, const float* pre, const float* weight,
                           const float* bias, float* y, int N, int Cin, int Cout, int H, int W,
                           void* stream);
+
+/* 1x1 convolution of NCHW tensors as an f32 MFMA GEMM with an optional second source
+ * along K (the score networks' Conv_2 skip projections and attention NINs, which the
+ * reference runs through nn.Conv2d / einsum):
+ *   Y[n] (M x P) = W[:, :K1] X1[n] (K1 x P) + W[:, K1:K1+K2] X2[n] (K2 x P) + bias[M]
+ * W row-major [M, ldw], X1 [N, K1, P], X2 [N, K2, P] (NULL when K2 = 0), Y [N, M, P], P = H*W;
+ * reading [X1, X2] this way replaces the channel concatenation torch.cat([X1, X2], 1).
+ * supported(): M % 128 == 0, P % 128 == 0, K1 % 16 == 0, K2 % 16 == 0. */
+int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2);
+int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K1, const float* X2, int K2,
+                      const float* bias, float* Y, int N, int M, int P, void* stream);
 
 #ifdef __cplusplus
 }

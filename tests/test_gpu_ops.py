@@ -528,3 +528,66 @@ def test_conv3x3_double_backward_any_shape(hip, cin, cout, hw):
             assert a is None or a.abs().max().item() == 0
             continue
         assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
+
+
+@pytest.mark.parametrize("N,k1,k2,m,hw", [(2, 64, 0, 128, 16), (3, 128, 64, 256, 32),
+                                          (1, 256, 256, 128, 16), (2, 16, 48, 384, 32)])
+def test_conv1x1_gemm_matches_fp32_reference(hip, N, k1, k2, m, hw):
+    """MFMA 1x1-conv GEMM (one or two sources along K) vs float64 (1e-5 relative); the
+    two-source form equals conv1x1 of the concatenation."""
+    from op.conv import conv1x1
+    g = torch.Generator().manual_seed(k1 + k2 + m)
+    x1 = torch.randn(N, k1, hw, hw, generator=g)
+    x2 = torch.randn(N, k2, hw, hw, generator=g) if k2 else None
+    w = torch.randn(m, k1 + k2, 1, 1, generator=g) / (k1 + k2) ** 0.5
+    b = torch.randn(m, generator=g)
+    xc = x1 if x2 is None else torch.cat([x1, x2], 1)
+    ref = F.conv2d(xc.double(), w.double(), b.double())
+    with torch.no_grad():
+        out = conv1x1(x1.to(hip), w.to(hip), b.to(hip), None if x2 is None else x2.to(hip))
+    assert (out.double().cpu() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_conv3x3_winograd_two_sources(hip):
+    """The Winograd conv reading [x1, x2] as two sources equals the conv of their
+    concatenation (same kernel, same chunk order: bit-identical), incl. the GroupNorm
+    prologue and the partial statistics."""
+    from op.conv import conv3x3, conv3x3_pair, gn_partials
+    g = torch.Generator().manual_seed(31)
+    x1 = torch.randn(2, 64, 16, 32, generator=g).to(hip)
+    x2 = torch.randn(2, 128, 16, 32, generator=g).to(hip)
+    w = (torch.randn(128, 192, 3, 3, generator=g) * 0.03).to(hip)
+    b = torch.randn(128, generator=g).to(hip)
+    pre = torch.stack([torch.rand(2, 192, generator=g) + 0.5, torch.randn(2, 192, generator=g)], -1).to(hip)
+    with torch.no_grad():
+        ref = conv3x3(torch.cat([x1, x2], 1), w, b, pre=pre, stats=True)
+        out = conv3x3_pair(x1, x2, w, b, pre=pre, stats=True)
+    assert torch.equal(out, ref)
+    assert torch.equal(gn_partials(out)[0], gn_partials(ref)[0])
+
+
+def test_resblock_forward_pair_matches_concat(hip):
+    """ResnetBlockBigGANpp.forward_pair(h, hs) (no concatenation: partial-statistics
+    GroupNorm, two-source Winograd conv, two-source 1x1 GEMM) == forward(cat([h, hs]))
+    within 1e-5 relative, and the output carries partial statistics."""
+    import models.layerspp as lpp
+    from models.layers import cat_channels
+    from op.conv import conv3x3, gn_partials
+    torch.manual_seed(0)
+    blk = lpp.ResnetBlockBigGANpp(act=torch.nn.SiLU(), in_ch=256, out_ch=128, temb_dim=512,
+                                  skip_rescale=True, init_scale=0.).to(hip).eval()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn_like(p) * 0.02)
+        g = torch.Generator().manual_seed(4)
+        src = torch.randn(2, 64, 32, 32, generator=g).to(hip)
+        w1 = (torch.randn(128, 64, 3, 3, generator=g) * 0.05).to(hip)
+        w2 = (torch.randn(128, 64, 3, 3, generator=g) * 0.05).to(hip)
+        h = conv3x3(src, w1, stats=True)      # producers that attach partial statistics
+        hs = conv3x3(src, w2, stats=True)
+        assert gn_partials(h) is not None and gn_partials(hs) is not None
+        temb = torch.randn(2, 512, generator=g).to(hip)
+        out = blk.forward_pair(h, hs, temb)
+        ref = blk(cat_channels(h, hs), temb)
+    assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    assert gn_partials(out) is not None
