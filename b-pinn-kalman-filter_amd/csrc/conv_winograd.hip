@@ -647,17 +647,17 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
 }
 
 // Persistent form of the pipelined kernel (NB = 1: 4 waves x 16 couts = 64 couts, 32
-// tiles, two workgroups per CU).  The grid holds exactly as many workgroups as fit on the
-// chip at once; workgroup l processes the work items l, l + G, l + 2G, ... (an item = one
-// 8 x 16 pixel region x 64 output channels) as ONE continuous chunk stream: the patch
+// tiles, two workgroups per CU).  The grid holds at most as many workgroups as fit on the
+// chip at once; workgroup l processes `ipw` consecutive work items of ONE image (an item =
+// one 8 x 16 pixel region x 64 output channels; the cout blocks of a region adjacent) as
+// ONE continuous chunk stream: the patch
 // loads, the patch stores, the V transform and the U loads of an item's first chunks run
 // inside the previous item's last chunks exactly as between the chunks of one item, so the
 // per-workgroup prologue (one memory latency + a transform) and the launch / drain of a
 // workgroup are paid once per workgroup instead of once per item.  The output transform
 // stores straight from registers (each lane owns 2 rows x 8 pixels of one channel per
 // M-block: two 16-B stores per row) so the V buffers stay live across the item boundary.
-// The GroupNorm prologue's (s, t) pairs are read per chunk with the patch (uniform loads),
-// since consecutive items of a workgroup belong to different images.
+// One image per workgroup: the GroupNorm prologue's (s, t) table is loaded to LDS once.
 struct WinoItem {
   int n, oy0, ox0, cout0;
 };
@@ -666,11 +666,12 @@ template <bool PRE>
 __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    WinoGeo g, int64_t items, int xcd_remap) {
+    float2* __restrict__ stats, WinoGeo g, int ipw, int wpi, int xcd_remap) {
   constexpr int kPatch = kCK * kPR * kPCp;
   constexpr int kVBuf = kCK * kM * kVS;
   __shared__ float s_patch_raw[2][kPatch];                                   // 2 x 5.9 KB
   __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];               // 2 x 20.5 KB
+  __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];  // PRE: (s, t) of every input channel
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -678,24 +679,24 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
   const int64_t G = gridDim.x;
   int64_t l = blockIdx.x;
   // workgroups on one XCD (blockIdx % 8 under round-robin placement) take consecutive
-  // logical indices, i.e. neighbouring items (the cout halves of one region) at a time
+  // logical indices: the same image, neighbouring regions
   if (xcd_remap) l = (l % 8) * (G / 8) + l / 8;
-  const int cnt = (int)((items - l + G - 1) / G);  // items of this workgroup (>= 1)
+  const int n = __builtin_amdgcn_readfirstlane((int)(l / wpi));
+  const int first = __builtin_amdgcn_readfirstlane((int)(l % wpi) * ipw);
+  const int cnt = ipw;
   const int nch = g.Cin / kCK;
   const int64_t plane = (int64_t)g.H * g.W;
 
-  // item -> geometry; 32-bit (the host guarantees items < 2^31) and forced scalar, so the
-  // buffer descriptors built from it stay in SGPRs (no waterfall loops)
+  // item (within this workgroup's image) -> geometry, forced scalar
   auto decode = [&](int i) {
-    const unsigned it = (unsigned)(l + (int64_t)min(i, cnt - 1) * G);
-    const unsigned cbs = (unsigned)g.cout_blocks, rxs = (unsigned)g.regions_x,
-                   rys = (unsigned)g.regions_y;
-    const unsigned r0 = it / cbs, r1 = r0 / rxs;
+    const unsigned q = (unsigned)(first + min(i, cnt - 1));
+    const unsigned cbs = (unsigned)g.cout_blocks, rxs = (unsigned)g.regions_x;
+    const unsigned r0 = q / cbs;
     WinoItem w;
-    w.cout0 = __builtin_amdgcn_readfirstlane((int)(it - r0 * cbs) * 64);
-    w.ox0 = __builtin_amdgcn_readfirstlane((int)(r0 - r1 * rxs) * kOutCols);
-    w.oy0 = __builtin_amdgcn_readfirstlane((int)(r1 % rys) * kOutRows);
-    w.n = __builtin_amdgcn_readfirstlane((int)(r1 / rys));
+    w.n = n;
+    w.cout0 = __builtin_amdgcn_readfirstlane((int)(q - r0 * cbs) * 64);
+    w.ox0 = __builtin_amdgcn_readfirstlane((int)(r0 % rxs) * kOutCols);
+    w.oy0 = __builtin_amdgcn_readfirstlane((int)(r0 / rxs) * kOutRows);
     return w;
   };
 
@@ -713,23 +714,22 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
   const int pdst = ppy * kPCp + ppx;
   int li = 0, lk = 0;
   WinoItem lit = decode(0);
-  __amdgpu_buffer_rsrc_t xrs;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + (int64_t)n * g.Cin * plane), 0, (int)(g.Cin * plane * 4),
+      0x00020000);
   int poff;
   bool pin_cur;
   auto set_load_item = [&]() {
-    const float* xn = x + (int64_t)lit.n * g.Cin * plane;
-    xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xn), 0, (int)(g.Cin * plane * 4),
-                                            0x00020000);
     const int iy = lit.oy0 - 1 + ppy, ix = lit.ox0 - 1 + ppx;
     pin_cur = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
     const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
     poff = (cy * g.W + cx) * 4;
   };
   set_load_item();
-  // loaded values and what the store needs of them: in-image bit and the chunk's (s, t)
+  // loaded values and what the store needs of them: in-image bit and the chunk index
   float pv[kCK];
   bool pin_ld;
-  float2 ss_ld[kCK];
+  int k_ld = 0;
   auto load_patch = [&]() {
     const int k = li < cnt ? lk : nch - 1;  // past the end: re-load the last chunk
     const int soff = k * kCK * (int)plane * 4;
@@ -738,11 +738,7 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
       pv[c] = __uint_as_float(
           __builtin_amdgcn_raw_buffer_load_b32(xrs, poff, soff + c * (int)plane * 4, 0));
     pin_ld = pin_cur;
-    if (PRE) {
-      const float2* ps = pre + (int64_t)lit.n * g.Cin + k * kCK;
-#pragma unroll
-      for (int c = 0; c < kCK; ++c) ss_ld[c] = ps[c];
-    }
+    k_ld = k;
     if (li < cnt && ++lk == nch) {
       lk = 0;
       ++li;
@@ -750,11 +746,14 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
       set_load_item();
     }
   };
-  auto store_patch_from = [&](const float* src, const float2* ss, bool pin, float* sp) {
+  auto store_patch_from = [&](const float* src, int kc, bool pin, float* sp) {
 #pragma unroll
     for (int c = 0; c < kCK; ++c) {
       float v = src[c];
-      if (PRE) v = silu_f(v * ss[c].x + ss[c].y);
+      if (PRE) {
+        const float2 st = s_ss[kc * kCK + c];
+        v = silu_f(v * st.x + st.y);
+      }
       sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
     }
   };
@@ -809,26 +808,32 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
       dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
   };
 
-  // ---- prologue: chunks 0-2 and U(0) issued before the first wait
+  // ---- prologue: chunks 0-2, U(0) and the GroupNorm table issued before the first wait
   float pv0[kCK], pv1[kCK];
-  float2 ss0[kCK], ss1[kCK];
+  int k0c, k1c;
   bool pin0, pin1;
   load_patch();
 #pragma unroll
-  for (int c = 0; c < kCK; ++c) { pv0[c] = pv[c]; ss0[c] = ss_ld[c]; }
+  for (int c = 0; c < kCK; ++c) pv0[c] = pv[c];
   pin0 = pin_ld;
+  k0c = k_ld;
   load_patch();
 #pragma unroll
-  for (int c = 0; c < kCK; ++c) { pv1[c] = pv[c]; ss1[c] = ss_ld[c]; }
+  for (int c = 0; c < kCK; ++c) pv1[c] = pv[c];
   pin1 = pin_ld;
+  k1c = k_ld;
   load_patch();
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int q = 0; q < 4; ++q) load_u_half(ks, q);
   advance_u();
-  store_patch_from(pv0, ss0, pin0, s_patch_raw[0]);
-  store_patch_from(pv1, ss1, pin1, s_patch_raw[1]);
+  if (PRE) {
+    for (int c = tid; c < g.Cin; c += 256) s_ss[c] = pre[(int64_t)n * g.Cin + c];
+    __syncthreads();
+  }
+  store_patch_from(pv0, k0c, pin0, s_patch_raw[0]);
+  store_patch_from(pv1, k1c, pin1, s_patch_raw[1]);
   __syncthreads();
   read_d(s_patch_raw[0]);
   write_v(s_v[0]);
@@ -853,6 +858,10 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
     const int co = w.cout0 + wave * 16 + jj;
     const float bv = bias ? bias[co] : 0.f;
     const int64_t obase = ((int64_t)w.n * g.Cout + co) * plane;
+    // GroupNorm partial statistics of channel co over the region: this lane's 32 values
+    // (sum, then sum of squared deviations from the lane mean), merged over the 4 lanes
+    // jj + 16 kq with equal counts (symmetric butterfly: every lane gets the same bits)
+    float lm = 0.f, lm2 = 0.f, lcnt = 0.f;  // running (mean, M2, count) of this lane's values
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
       // tiles m = 16 mb + 4 kq + rg: tile row 2 mb + kq / 2, tile cols 4 (kq & 1) + rg
@@ -881,7 +890,27 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
             for (int c = 0; c < 4; ++c) v[c] = (sk[c] + v[c]) / g.div;
           }
           *reinterpret_cast<f4*>(&y[o]) = v;
+          if (stats) {  // Chan merge of this 4-value strip into the running statistics
+            const float sm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+            float sm2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sm2 = fmaf(v[c] - sm, v[c] - sm, sm2);
+            const float d = sm - lm, nt = lcnt + 4.f;
+            lm = lm + d * (4.f / nt);
+            lm2 = (lm2 + sm2) + d * d * (lcnt * 4.f / nt);
+            lcnt = nt;
+          }
         }
+      }
+    }
+    if (stats) {
+      float m = lm, m2 = lm2;
+      merge_stats(m, m2, __shfl_xor(m, 16, 64), __shfl_xor(m2, 16, 64), 32.f);
+      merge_stats(m, m2, __shfl_xor(m, 32, 64), __shfl_xor(m2, 32, 64), 64.f);
+      if (kq == 0) {
+        const int R = g.regions_x * g.regions_y;
+        const int region = (w.oy0 / kOutRows) * g.regions_x + w.ox0 / kOutCols;
+        stats[((int64_t)w.n * g.Cout + co) * R + region] = make_float2(m, m2);
       }
     }
 #pragma unroll
@@ -897,7 +926,7 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
       __builtin_amdgcn_sched_barrier(0);
       if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                          // patch(q+1)
       if (grp == 1) write_v(s_v[SB ^ 1]);                                 // V(q+1)
-      if (grp == 2) store_patch_from(pv, ss_ld, pin_ld, s_patch_raw[SB]);  // patch(q+2)
+      if (grp == 2) store_patch_from(pv, k_ld, pin_ld, s_patch_raw[SB]);  // patch(q+2)
       if (grp == 3) load_patch();                                         // patch(q+3)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -982,11 +1011,10 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     return e ? atoi(e) : 0;
   }();
   if (pipe_env == 1 && (persist_env == 2 || (persist_env == 1 && pre)) && Cin % (2 * kCK) == 0 &&
-      !stats && !x2) {
+      !x2 && (!pre || Cin <= kPreMaxCin)) {
     WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div, Cin};
-    const int64_t items = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
-    // as many workgroups as are resident at once (2 per CU): more would run as a second,
-    // mostly idle wave of workgroups
+    // as many workgroups as are resident at once (2 per CU), each on consecutive items of
+    // one image: ipw = items per workgroup divides the items of an image
     static int slots = 0;
     if (slots == 0) {
       int dev = 0, cus = 0, occ = 0;
@@ -995,16 +1023,24 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wino_f23_persist_kernel<true>, 256, 0);
       slots = std::max(8, cus * std::max(1, occ));
     }
-    const int64_t G = std::min<int64_t>(items, slots);
+    const int ipi = g.regions_x * g.regions_y * g.cout_blocks;
+    int ipw = 1;
+    while ((int64_t)N * (ipi / ipw) > slots && ipw < ipi) {
+      ++ipw;
+      while (ipi % ipw) ++ipw;
+    }
+    const int wpi = ipi / ipw;
+    const int64_t G = (int64_t)N * wpi;
+    BPK_REQUIRE(G < (1LL << 31), "conv3x3_wino: grid too large");
     const int remap = (G % 8 == 0) ? 1 : 0;
     const float2* pre2 = reinterpret_cast<const float2*>(pre);
     hipStream_t st = bpk::as_stream(stream);
     if (pre)
       hipLaunchKernelGGL((wino_f23_persist_kernel<true>), dim3((unsigned)G), dim3(256), 0, st, x,
-                         U, bias, skip, pre2, y, g, items, remap);
+                         U, bias, skip, pre2, y, stats2, g, ipw, wpi, remap);
     else
       hipLaunchKernelGGL((wino_f23_persist_kernel<false>), dim3((unsigned)G), dim3(256), 0, st, x,
-                         U, bias, skip, pre2, y, g, items, remap);
+                         U, bias, skip, pre2, y, stats2, g, ipw, wpi, remap);
     BPK_LAUNCH_CHECK("conv3x3_wino_persist");
     return BPK_OK;
   }

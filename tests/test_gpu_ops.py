@@ -563,7 +563,9 @@ def test_conv3x3_winograd_two_sources(hip):
         ref = conv3x3(torch.cat([x1, x2], 1), w, b, pre=pre, stats=True)
         out = conv3x3_pair(x1, x2, w, b, pre=pre, stats=True)
     assert torch.equal(out, ref)
-    assert torch.equal(gn_partials(out)[0], gn_partials(ref)[0])
+    # statistics: same values, merge order may differ between kernel forms
+    pa, pb = gn_partials(out)[0], gn_partials(ref)[0]
+    assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6 * pb.abs().max().item())
 
 
 def test_resblock_forward_pair_matches_concat(hip):
