@@ -245,7 +245,7 @@ def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
     return step_fn
 
 
-def get_pinn_step_fn(config, train, optimize_fn, ctx=None):
+def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
     """Schedule 2: data losses + pinn_loss_weight * Navier-Stokes residual (Re = 1e7), both
     nets trained together; a NaN gradient on PressureNet's last 1x1 conv skips the update
     (reference losses.py:332-386).  Returns step_fn(state, operator, batch) ->
@@ -273,16 +273,71 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None):
                      * config.training.pinn_loss_weight)
         return pinn_loss + data_loss, pinn_loss, data_loss
 
+    # graph=True (training): after two eager steps, the forward, the residual's first and
+    # second derivatives and the backward are captured once in a hipGraph and replayed with
+    # the step's batch / mask copied into static buffers -- the ~17k small kernel launches
+    # of a step are issued by the device instead of the host.  Gradient all-reduce, the NaN
+    # check, the optimizers and the EMA stay eager.
+    gstate = {"eager": 0}
+
+    def graph_forward_backward(model, operator, batch, opt_flow, opt_pres):
+        if gstate["eager"] < 2:
+            gstate["eager"] += 1
+            opt_flow.zero_grad(set_to_none=False)
+            opt_pres.zero_grad(set_to_none=False)
+            return loss_fn(model, operator, batch)
+        dev = batch[0].device
+        if "graph" not in gstate:
+            sb = []
+            for t in batch:
+                c = t.detach().clone()
+                sb.append(c.requires_grad_(t.requires_grad))
+            gstate["batch"] = tuple(sb)
+            gstate["mask"] = operator.mask.to(dev).clone()
+            cur = torch.cuda.current_stream(dev)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(cur)
+            real_mask = operator.mask
+            operator.mask = gstate["mask"]
+            with torch.cuda.stream(side):  # warm-up on the capture stream
+                opt_flow.zero_grad(set_to_none=False)
+                opt_pres.zero_grad(set_to_none=False)
+                l3 = loss_fn(model, operator, gstate["batch"])
+                l3[0].backward()
+            cur.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for p in model.parameters():
+                    if p.grad is not None:
+                        p.grad.zero_()
+                out = loss_fn(model, operator, gstate["batch"])
+                out[0].backward()
+            operator.mask = real_mask
+            gstate["graph"], gstate["out"] = g, out
+        with torch.no_grad():
+            for s_, t in zip(gstate["batch"], batch):
+                if s_ is not t:
+                    s_.copy_(t)
+            gstate["mask"].copy_(operator.mask, non_blocking=True)
+        gstate["graph"].replay()
+        return gstate["out"]
+
     def step_fn(state, operator, batch):
         model = state["model"]
         operator.next()
         if train:
             opt_flow, opt_pres = state["optimizer"]
             model.train()
-            opt_flow.zero_grad()
-            opt_pres.zero_grad()
-            loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
-            loss.backward()
+            if graph:
+                loss, pinn_loss, data_loss = graph_forward_backward(model, operator, batch,
+                                                                    opt_flow, opt_pres)
+                if gstate["eager"] <= 2 and "graph" not in gstate:
+                    loss.backward()
+            else:
+                opt_flow.zero_grad()
+                opt_pres.zero_grad()
+                loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
+                loss.backward()
             params = list(model.parameters())
             _sync_grads(params, ctx)
             w = model.pressurenet.end[-1].weight

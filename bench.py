@@ -53,6 +53,9 @@ def parse():
                     help="configs[1] train steps (NCSN++ CIFAR-10 32x32x3, batch 128/GPU); 0: skip")
     ap.add_argument("--pinn-steps", type=int, default=5)
     ap.add_argument("--pinn-warmup", type=int, default=2)
+    ap.add_argument("--pinn-graph", action="store_true",
+                    help="replay the PINN forward/backward from a hipGraph (measured slower than "
+                         "eager on ROCm 7: 3.66 vs 4.06 steps/s; needs --pinn-warmup >= 3)")
     ap.add_argument("--no-pinn", action="store_true")
     ap.add_argument("--dps-steps", type=int, default=2, help="accepted RK45 steps timed")
     ap.add_argument("--no-dps", action="store_true")
@@ -253,7 +256,8 @@ def bench_pinn(args, ctx, dev):
     """configs[3]: one PINN train step (get_pinn_step_fn: FlowNet + PressureNet forward,
     equation_mse with create_graph first derivatives and second derivatives -- correlation and
     grid_sample grad2 on HIP --, backward, two Adams, EMA) at pinn_pde, batch 64/GPU, 64x64;
-    gradients averaged over ranks with one coalesced RCCL all-reduce."""
+    gradients averaged over ranks with one coalesced RCCL all-reduce.  --pinn-graph replays the
+    forward/backward from a hipGraph after two eager steps (opt-in: slower here)."""
     import losses
     from configs.pinn import pinn_pde
     from inverse.operators import get_operator
@@ -268,7 +272,7 @@ def bench_pinn(args, ctx, dev):
     opt_p = losses.get_optimizer(c, model.pressurenet.parameters(), 0.005)
     state = dict(optimizer=(opt_f, opt_p), model=model, ema=ema, step=c.training.n_iters)
     step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
-                                      ctx=ctx)
+                                      ctx=ctx, graph=args.pinn_graph)
     operator = get_operator(c)
     batch = pinn_batch(c, args.batch, dev, seed=ctx.rank)
     for _ in range(args.pinn_warmup):
