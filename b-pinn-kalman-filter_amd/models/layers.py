@@ -94,6 +94,11 @@ def conv2d(x, conv: nn.Conv2d, bias=True):
     b = conv.bias if bias else None
     if _is_3x3(x, conv):  # native kernels where they fit; every derivative order on 3x3 ops
         return conv_op.conv3x3(x, conv.weight, b)
+    if (x.is_cuda and torch.is_grad_enabled() and _WINO_ENABLED and conv.padding_mode == "zeros"
+            and isinstance(conv.padding, tuple)):
+        # under autograd: higher derivatives as plain convolutions (op.conv.conv2d_general)
+        return conv_op.conv2d_general(x, conv.weight, b, conv.stride, conv.padding,
+                                      conv.dilation, conv.groups)
     return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
@@ -302,8 +307,8 @@ class ResnetBlockDDPM(nn.Module):
 
 def ncsn_conv1x1(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=0):
     """1x1 conv, PyTorch default init scaled by init_scale (reference layers.py:44-50)."""
-    conv = nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=bias,
-                     dilation=dilation, padding=padding)
+    conv = Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=bias,
+                  dilation=dilation, padding=padding)
     scale = 1e-10 if init_scale == 0 else init_scale
     conv.weight.data *= scale
     if bias:

@@ -352,3 +352,97 @@ def conv1x1(x, weight, bias=None, x2=None):
                                 None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
                                 stream_ptr(x.device)), "conv1x1")
     return y
+
+
+# ---------------------------------------------------------------- general convolutions
+# Every other Conv2d of the networks (stride-2 3x3, 1x1, ...) runs on MIOpen, but through
+# three autograd Functions -- conv, its adjoint (conv transpose) and the weight gradient --
+# whose backward passes are written in terms of each other.  Higher derivatives (the PINN
+# residual differentiates the networks twice) thus stay plain convolutions, instead of the
+# generic convolution double backward, which runs its weight terms as batch/channel-swapped
+# convolutions with H x W kernels (0.5-5 ms each on the PINN shapes).
+
+def _cfg(ctx_like):
+    return dict(stride=ctx_like[0], padding=ctx_like[1], dilation=ctx_like[2], groups=ctx_like[3])
+
+
+def _conv_fn(x, w, cfg):
+    return _ConvG.apply(x, w, cfg) if torch.is_grad_enabled() else _ConvG.forward(None, x, w, cfg)
+
+
+def _convt_fn(u, w, xshape, cfg):
+    if torch.is_grad_enabled():
+        return _ConvTG.apply(u, w, xshape, cfg)
+    return _ConvTG.forward(None, u, w, xshape, cfg)
+
+
+def _wgrad_fn(x, gy, wshape, cfg):
+    if torch.is_grad_enabled():
+        return _WgradG.apply(x, gy, wshape, cfg)
+    return _WgradG.forward(None, x, gy, wshape, cfg)
+
+
+class _ConvG(torch.autograd.Function):
+    """y = conv2d(x, w) (no bias), MIOpen forward; grads: conv transpose and weight grad."""
+
+    @staticmethod
+    def forward(ctx, x, w, cfg):
+        if ctx is not None:
+            ctx.save_for_backward(x, w)
+            ctx.cfg = cfg
+        with torch.no_grad():
+            return F.conv2d(x.detach(), w.detach(), None, **_cfg(cfg))
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = _convt_fn(gy, w, tuple(x.shape), ctx.cfg) if ctx.needs_input_grad[0] else None
+        gw = _wgrad_fn(x, gy, tuple(w.shape), ctx.cfg) if ctx.needs_input_grad[1] else None
+        return gx, gw, None
+
+
+class _ConvTG(torch.autograd.Function):
+    """z = conv2d's adjoint w.r.t. its input: z = A_w^T u (shape xshape)."""
+
+    @staticmethod
+    def forward(ctx, u, w, xshape, cfg):
+        if ctx is not None:
+            ctx.save_for_backward(u, w)
+            ctx.cfg = cfg
+        with torch.no_grad():
+            return torch.nn.grad.conv2d_input(xshape, w.detach(), u.detach(), **_cfg(cfg))
+
+    @staticmethod
+    def backward(ctx, gz):
+        u, w = ctx.saved_tensors
+        gu = _conv_fn(gz, w, ctx.cfg) if ctx.needs_input_grad[0] else None
+        gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg) if ctx.needs_input_grad[1] else None
+        return gu, gw, None, None
+
+
+class _WgradG(torch.autograd.Function):
+    """dw = d<conv2d(x, w), gy>/dw; linear in x and gy."""
+
+    @staticmethod
+    def forward(ctx, x, gy, wshape, cfg):
+        if ctx is not None:
+            ctx.save_for_backward(x, gy)
+            ctx.cfg = cfg
+        with torch.no_grad():
+            return torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), **_cfg(cfg))
+
+    @staticmethod
+    def backward(ctx, ggw):
+        x, gy = ctx.saved_tensors
+        gx = _convt_fn(gy, ggw, tuple(x.shape), ctx.cfg) if ctx.needs_input_grad[0] else None
+        ggy = _conv_fn(x, ggw, ctx.cfg) if ctx.needs_input_grad[1] else None
+        return gx, ggy, None, None
+
+
+def conv2d_general(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
+    """F.conv2d with every derivative order expressed as convolutions / conv transposes /
+    weight gradients (see above).  MIOpen kernels underneath."""
+    pair = lambda v: (v, v) if isinstance(v, int) else tuple(v)
+    cfg = (pair(stride), pair(padding), pair(dilation), int(groups))
+    y = _conv_fn(x, weight, cfg)
+    return y if bias is None else y + bias.view(1, -1, 1, 1)

@@ -593,3 +593,35 @@ def test_resblock_forward_pair_matches_concat(hip):
         ref = blk(cat_channels(h, hs), temb)
     assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
     assert gn_partials(out) is not None
+
+
+@pytest.mark.parametrize("k,stride,pad,cin,cout", [(3, 2, 1, 1, 16), (3, 2, 1, 16, 32), (1, 1, 0, 64, 128)])
+def test_conv2d_general_double_backward(hip, k, stride, pad, cin, cout):
+    """conv2d_general (MIOpen kernels, derivatives of every order as convolutions / conv
+    transposes / weight gradients) vs F.conv2d: forward, and second derivatives w.r.t. x, w, b
+    of a function of (dL/dx, dL/dw) (2e-5 relative)."""
+    from op.conv import conv2d_general
+    g = torch.Generator().manual_seed(k * 100 + stride * 10 + cin)
+    x0 = torch.randn(2, cin, 16, 20, generator=g)
+    w0 = torch.randn(cout, cin, k, k, generator=g) * 0.2
+    b0 = torch.randn(cout, generator=g)
+    ho, wo = (16 + 2 * pad - k) // stride + 1, (20 + 2 * pad - k) // stride + 1
+    go = torch.randn(2, cout, ho, wo, generator=g).to(hip)
+    v = torch.randn(2, cin, 16, 20, generator=g).to(hip)
+
+    def second(fn):
+        x = x0.to(hip).requires_grad_()
+        w = w0.to(hip).requires_grad_()
+        b = b0.to(hip).requires_grad_()
+        y = fn(torch.tanh(x), w, b)
+        gx, gw = torch.autograd.grad(y, (x, w), go, create_graph=True)
+        return (y.detach(),) + torch.autograd.grad(
+            (gx * v).sum() + (gw * gw).sum() + (gx * gx).sum(), (x, w, b), allow_unused=True)
+
+    got = second(lambda x, w, b: conv2d_general(x, w, b, stride, pad))
+    ref = second(lambda x, w, b: F.conv2d(x, w, b, stride, pad))
+    for a, r in zip(got, ref):
+        if r is None:
+            assert a is None or a.abs().max().item() == 0
+            continue
+        assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
