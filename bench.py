@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--no-dps", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-samples", type=int, default=4)
+    ap.add_argument("--cpu-samples", type=int, default=8,
+                    help="CPU-baseline sample: 1 PC step on this many samples (~10 s on 16 cores)")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="1: MIOpen exhaustive find (cudnn.benchmark); immediate mode (0) picks "
                          "the same fp32 Winograd kernels for the forward and avoids minutes of "
