@@ -1018,9 +1018,9 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     static int slots = 0;
     if (slots == 0) {
       int dev = 0, cus = 0, occ = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wino_f23_persist_kernel<true>, 256, 0);
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wino_f23_persist_kernel<true>, 256, 0);
       slots = std::max(8, cus * std::max(1, occ));
     }
     const int ipi = g.regions_x * g.regions_y * g.cout_blocks;

@@ -133,6 +133,152 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
     }
 }
 
+
+// ---------------------------------------------------------------- weight gradient
+// dW (M x K) = sum_n GY[n] (M x P) X[n]^T (P x K)  and  db[m] = sum_{n,p} GY[n][m][p]:
+// the 1x1 conv's weight / bias gradient.  The reduction runs over the N * P pixels in
+// chunks of 16; both operands keep pixels contiguous, so both tiles sit in LDS as
+// [row][pixel] at stride 20 and every lane reads its four k-step values with one 16-byte
+// read.  Split-K over pixel ranges (deterministic: per-split partial slabs, summed in a
+// fixed order by gemm_wgrad_reduce_kernel).
+struct WgGeo {
+  int N, M, K, P;
+  int tiles_m, tiles_k, splits, cps;  // chunks per split
+};
+
+__global__ __launch_bounds__(256, 2) void gemm_nchw_wgrad_kernel(
+    const float* __restrict__ GY, const float* __restrict__ X, float* __restrict__ part,
+    float* __restrict__ part_b, WgGeo g, int xcd_remap) {
+  __shared__ __attribute__((aligned(16))) float sA[2][kBM * kAS];  // GY tile [m][p]
+  __shared__ __attribute__((aligned(16))) float sB[2][kBM * kAS];  // X tile  [k][p]
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, jj = lane & 15;
+  const int wm = wave >> 1, wk = wave & 1;
+  int b = blockIdx.x;
+  const int nblk = gridDim.x;
+  if (xcd_remap) b = (b % 8) * (nblk / 8) + b / 8;
+  const int tiles = g.tiles_m * g.tiles_k;
+  const int s = b / tiles, t = b % tiles;
+  const int tm = t / g.tiles_k, tk = t % g.tiles_k;
+  const int m0 = tm * kBM, k0 = tk * kBM;
+  const int cpi = g.P / kKC;                           // chunks per image
+  const int c0 = s * g.cps;
+  const int nch = min(g.cps, g.N * cpi - c0);          // >= 1 by construction
+
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  // loads: rows r, r + 64 of both tiles, pixels 4 (tid & 3) .. + 3 of the chunk
+  const int lr = tid >> 2, lp = (tid & 3) * 4;
+  int ln = c0 / cpi, lpc = c0 % cpi, left = nch;       // load cursor (image, chunk in image)
+  f4 ra[2], rb[2];
+  auto load = [&]() {
+    const float* gy = GY + ((int64_t)ln * g.M + m0 + lr) * g.P + lpc * kKC + lp;
+    const float* xx = X + ((int64_t)ln * g.K + k0 + lr) * g.P + lpc * kKC + lp;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ra[i] = *reinterpret_cast<const f4*>(gy + (int64_t)(64 * i) * g.P);
+      rb[i] = *reinterpret_cast<const f4*>(xx + (int64_t)(64 * i) * g.P);
+    }
+    if (--left > 0 && ++lpc == cpi) { lpc = 0; ++ln; }  // past the end: re-load the last chunk
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<f4*>(&sA[buf][(lr + 64 * i) * kAS + lp]) = ra[i];
+      *reinterpret_cast<f4*>(&sB[buf][(lr + 64 * i) * kAS + lp]) = rb[i];
+    }
+  };
+
+  load();
+  store(0);
+  load();
+  __syncthreads();
+
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    f4 a[4], bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = *reinterpret_cast<const f4*>(&sA[buf][(64 * wm + 16 * i + jj) * kAS + 4 * kq]);
+      bv[i] = *reinterpret_cast<const f4*>(&sB[buf][(64 * wk + 16 * i + jj) * kAS + 4 * kq]);
+    }
+    if (c + 1 < nch) store(buf ^ 1);
+    load();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][ks], bv[j][ks], acc[i][j], 0, 0,
+                                                           0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bsum[i] += (a[i].x + a[i].y) + (a[i].z + a[i].w);
+    __syncthreads();
+  }
+
+  // acc[i][j][rr] = dW[m0 + 64 wm + 16 i + 4 kq + rr][k0 + 64 wk + 16 j + jj]
+  float* ps = part + (int64_t)s * g.M * g.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = m0 + 64 * wm + 16 * i + 4 * kq + rr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ps[(int64_t)m * g.K + k0 + 64 * wk + 16 * j + jj] = acc[i][j][rr];
+    }
+  if (part_b != nullptr && tk == 0 && wk == 0) {  // bias: rows of this wave, summed over kq
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = bsum[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (kq == 0) part_b[(int64_t)s * g.M + m0 + 64 * wm + 16 * i + jj] = v;
+    }
+  }
+}
+
+// out[i] = sum_s part[s][i] for i < n4 float4s (fixed order; 4 split groups per column,
+// combined through LDS), and ob[m] = sum_s part_b[s][m].
+__global__ __launch_bounds__(256) void gemm_wgrad_reduce_kernel(
+    const f4* __restrict__ part, f4* __restrict__ out, const float* __restrict__ part_b,
+    float* __restrict__ ob, int64_t n4, int M, int splits) {
+  __shared__ f4 red[4][64];
+  const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + col;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  if (i < n4)
+    for (int s = grp; s < splits; s += 4) acc += part[(int64_t)s * n4 + i];
+  red[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && i < n4) out[i] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+  if (ob != nullptr && blockIdx.x == 0)
+    for (int m = threadIdx.x; m < M; m += 256) {
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s) v += part_b[(int64_t)s * M + m];
+      ob[m] = v;
+    }
+}
+
+WgGeo wgrad_geo(int N, int M, int K, int P) {
+  WgGeo g{N, M, K, P, M / kBM, K / kBM, 1, 0};
+  const int64_t chunks = (int64_t)N * (P / kKC);
+  const int tiles = g.tiles_m * g.tiles_k;
+  // ~1024 workgroups (4 per CU), at least 64 chunks (1024 pixels) per split
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(bpk::ceil_div(1024, tiles),
+                                                          chunks / 64));
+  g.cps = (int)bpk::ceil_div(chunks, splits);
+  g.splits = (int)bpk::ceil_div(chunks, (int64_t)g.cps);  // every split non-empty
+  return g;
+}
+
 }  // namespace
 
 extern "C" int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2) {
@@ -156,5 +302,44 @@ extern "C" int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K
                      bpk::as_stream(stream), W, X1, K2 ? W + K1 : W, K2 ? X2 : X1, bias, Y, g,
                      remap);
   BPK_LAUNCH_CHECK("gemm_nchw");
+  return BPK_OK;
+}
+
+extern "C" int bpk_gemm_nchw_wgrad_supported(int N, int M, int K, int P) {
+  return N > 0 && M > 0 && K > 0 && P > 0 && M % kBM == 0 && K % kBM == 0 && P % kKC == 0 &&
+         (int64_t)N * (P / kKC) < (1LL << 31);
+}
+
+extern "C" int64_t bpk_gemm_nchw_wgrad_workspace_bytes(int N, int M, int K, int P) {
+  if (!bpk_gemm_nchw_wgrad_supported(N, M, K, P)) return 0;
+  const WgGeo g = wgrad_geo(N, M, K, P);
+  if (g.splits == 1) return 0;
+  return (int64_t)g.splits * ((int64_t)M * K + M) * (int64_t)sizeof(float);
+}
+
+extern "C" int bpk_gemm_nchw_wgrad_f32(const float* GY, const float* X, float* dW, float* db,
+                                       void* workspace, int N, int M, int K, int P,
+                                       void* stream) {
+  BPK_REQUIRE(bpk_gemm_nchw_wgrad_supported(N, M, K, P),
+              "gemm_nchw_wgrad: unsupported shape N=%d M=%d K=%d P=%d (need M %% 128, K %% 128, "
+              "P %% 16 == 0)", N, M, K, P);
+  const WgGeo g = wgrad_geo(N, M, K, P);
+  BPK_REQUIRE(g.splits == 1 || workspace != nullptr, "gemm_nchw_wgrad: workspace required");
+  const int64_t blocks = (int64_t)g.splits * g.tiles_m * g.tiles_k;
+  BPK_REQUIRE(blocks < (1LL << 31), "gemm_nchw_wgrad: grid too large");
+  float* part = g.splits == 1 ? dW : static_cast<float*>(workspace);
+  float* part_b = db == nullptr ? nullptr
+                  : g.splits == 1 ? db : part + (int64_t)g.splits * M * K;
+  hipStream_t st = bpk::as_stream(stream);
+  hipLaunchKernelGGL(gemm_nchw_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, GY, X,
+                     part, part_b, g, (blocks % 8 == 0) ? 1 : 0);
+  BPK_LAUNCH_CHECK("gemm_nchw_wgrad");
+  if (g.splits > 1) {
+    const int64_t n4 = (int64_t)M * K / 4;
+    hipLaunchKernelGGL(gemm_wgrad_reduce_kernel, dim3((unsigned)bpk::ceil_div(n4, 64)),
+                       dim3(256), 0, st, reinterpret_cast<const f4*>(part),
+                       reinterpret_cast<f4*>(dW), part_b, db, n4, M, g.splits);
+    BPK_LAUNCH_CHECK("gemm_nchw_wgrad_reduce");
+  }
   return BPK_OK;
 }

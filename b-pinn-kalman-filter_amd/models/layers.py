@@ -75,12 +75,18 @@ def ddpm_conv1x1(in_planes, out_planes, stride=1, bias=True, init_scale=1., padd
 _WINO_ENABLED = os.environ.get("BPK_CONV", "winograd") != "miopen"
 # GroupNorm partial statistics from the producing conv's epilogue (BPK_GN_STATS=0: off)
 _GN_STATS = os.environ.get("BPK_GN_STATS", "1") != "0"
+_GEMM1X1 = os.environ.get("BPK_GEMM1X1", "1") != "0"  # 1x1 convs on the MFMA GEMM kernels
 
 
 def _is_3x3(x, conv: nn.Conv2d):
     return (_WINO_ENABLED and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
             and x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32)
+
+
+def _is_1x1(x, conv: nn.Conv2d):
+    return (_WINO_ENABLED and _GEMM1X1 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.groups == 1 and x.is_cuda)
 
 
 def _wino_eligible(x, conv: nn.Conv2d):
@@ -94,6 +100,8 @@ def conv2d(x, conv: nn.Conv2d, bias=True):
     b = conv.bias if bias else None
     if _is_3x3(x, conv):  # native kernels where they fit; every derivative order on 3x3 ops
         return conv_op.conv3x3(x, conv.weight, b)
+    if _is_1x1(x, conv) and conv_op.conv1x1_train_supported(x, conv.weight):
+        return conv_op.conv1x1_ad(x, conv.weight, b)  # MFMA GEMMs, every derivative order
     if (x.is_cuda and torch.is_grad_enabled() and _WINO_ENABLED and conv.padding_mode == "zeros"
             and isinstance(conv.padding, tuple)):
         # under autograd: higher derivatives as plain convolutions (op.conv.conv2d_general)

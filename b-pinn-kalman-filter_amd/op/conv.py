@@ -354,6 +354,116 @@ def conv1x1(x, weight, bias=None, x2=None):
     return y
 
 
+def conv1x1_train_supported(x, weight):
+    """The 1x1 GEMM kernels cover conv1x1(x, weight) and all of its derivatives: the forward
+    (M = Cout), its adjoint (M = Cin) and the weight gradient (csrc/gemm_nchw.hip)."""
+    if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4
+            or not x.is_cuda or weight.dim() not in (2, 4) or tuple(weight.shape[2:]) not in ((), (1, 1))):
+        return False
+    N, C, H, W = x.shape
+    M = weight.shape[0]
+    if weight.shape[1] != C:
+        return False
+    return bool(lib.bpk_gemm_nchw_supported(N, M, H * W, C, 0)
+                and lib.bpk_gemm_nchw_supported(N, C, H * W, M, 0)
+                and lib.bpk_gemm_nchw_wgrad_supported(N, M, C, H * W))
+
+
+def _gemm1x1_raw(x, w2d, bias=None):
+    """y[n] = w2d @ x[n] (+ bias): the MFMA GEMM, no autograd."""
+    x = x.detach().contiguous()
+    w = w2d.detach().contiguous()
+    N, K, H, W = x.shape
+    M = w.shape[0]
+    b = None if bias is None else bias.detach().contiguous()
+    y = torch.empty((N, M, H, W), dtype=torch.float32, device=x.device)
+    check(lib.bpk_gemm_nchw_f32(w.data_ptr(), K, x.data_ptr(), K, None, 0,
+                                None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
+                                stream_ptr(x.device)), "conv1x1")
+    return y
+
+
+def _wgrad1x1_raw(gy, x, bias_grad):
+    """(dw [M, K], db [M] or None) = (sum_n gy[n] x[n]^T, gy.sum((0, 2, 3)))."""
+    gy = gy.detach().contiguous()
+    x = x.detach().contiguous()
+    N, K, H, W = x.shape
+    M = gy.shape[1]
+    nbytes = lib.bpk_gemm_nchw_wgrad_workspace_bytes(N, M, K, H * W)
+    ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=x.device)
+    dw = torch.empty((M, K), dtype=torch.float32, device=x.device)
+    db = torch.empty((M,), dtype=torch.float32, device=x.device) if bias_grad else None
+    check(lib.bpk_gemm_nchw_wgrad_f32(gy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                      None if db is None else db.data_ptr(), ws.data_ptr(),
+                                      N, M, K, H * W, stream_ptr(x.device)), "conv1x1_wgrad")
+    return dw, db
+
+
+def _c1_fn(x, w2d, bias=None):
+    if torch.is_grad_enabled():
+        return _Conv1x1.apply(x, w2d, bias)
+    return _gemm1x1_raw(x, w2d, bias)
+
+
+def _w1_fn(gy, x, bias_grad):
+    if torch.is_grad_enabled():
+        return _Wgrad1x1.apply(gy, x, bias_grad)
+    return _wgrad1x1_raw(gy, x, bias_grad)
+
+
+class _Conv1x1(torch.autograd.Function):
+    """y = w2d @ x[n] + bias.  Backward: the adjoint is the 1x1 conv with w2d^T, the weight
+    and bias gradients one split-K GEMM; all three are differentiable again (PINN residuals
+    take second derivatives through the networks)."""
+
+    @staticmethod
+    def forward(ctx, x, w2d, bias):
+        ctx.save_for_backward(x, w2d)
+        return _gemm1x1_raw(x, w2d, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w2d = ctx.saved_tensors
+        gx = _c1_fn(gy, w2d.t()) if ctx.needs_input_grad[0] else None
+        gw = gb = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            gw, gb = _w1_fn(gy, x, bool(ctx.needs_input_grad[2]))
+            if not ctx.needs_input_grad[1]:
+                gw = None
+        return gx, gw, gb
+
+
+class _Wgrad1x1(torch.autograd.Function):
+    """(dw, db) = (sum_n gy[n] x[n]^T, gy.sum((0, 2, 3))); bilinear in (gy, x)."""
+
+    @staticmethod
+    def forward(ctx, gy, x, bias_grad):
+        ctx.save_for_backward(gy, x)
+        return _wgrad1x1_raw(gy, x, bias_grad)
+
+    @staticmethod
+    def backward(ctx, ggw, ggb):
+        gy, x = ctx.saved_tensors
+        g_gy = g_x = None
+        if ctx.needs_input_grad[0]:
+            if ggw is not None:
+                g_gy = _c1_fn(x, ggw, ggb)  # ggw x[n] + ggb
+            elif ggb is not None:
+                g_gy = ggb.view(1, -1, 1, 1).expand_as(gy)
+        if ctx.needs_input_grad[1] and ggw is not None:
+            g_x = _c1_fn(gy, ggw.t())
+        return g_gy, g_x, None
+
+
+def conv1x1_ad(x, weight, bias=None):
+    """1x1 conv with autograd on the GEMM kernels (every derivative order); shapes must pass
+    conv1x1_train_supported.  weight [Cout, Cin(, 1, 1)]."""
+    require_hip(x, weight, bias, what="conv1x1")
+    if not conv1x1_train_supported(x, weight):
+        raise RuntimeError(f"conv1x1: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
+    return _c1_fn(x, weight.reshape(weight.shape[0], weight.shape[1]), bias)
+
+
 # ---------------------------------------------------------------- general convolutions
 # Every other Conv2d of the networks (stride-2 3x3, 1x1, ...) runs on MIOpen, but through
 # three autograd Functions -- conv, its adjoint (conv transpose) and the weight gradient --

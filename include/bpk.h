@@ -365,6 +365,19 @@ int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2);
 int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K1, const float* X2, int K2,
                       const float* bias, float* Y, int N, int M, int P, void* stream);
 
+/* Weight / bias gradient of that 1x1 conv (replaces the conv2d backward-weights MIOpen
+ * runs for the reference's nn.Conv2d 1x1 layers -- ddpm_conv1x1 (models/layers.py:96), the
+ * BigGAN blocks' Conv_2 skip projection (models/layerspp.py:235) -- under loss.backward(),
+ * losses.py:210):
+ *   dW (M x K) = sum_n GY[n] (M x P) X[n]^T (P x K),   db[m] = sum_{n,p} GY[n][m][p]
+ * GY [N, M, P], X [N, K, P], dW row-major [M, K], db [M] or NULL.  Split-K over pixel
+ * ranges with per-split partial slabs summed in a fixed order (deterministic); workspace of
+ * workspace_bytes() (0: none needed).  supported(): M % 128, K % 128, P % 16 == 0. */
+int bpk_gemm_nchw_wgrad_supported(int N, int M, int K, int P);
+int64_t bpk_gemm_nchw_wgrad_workspace_bytes(int N, int M, int K, int P);
+int bpk_gemm_nchw_wgrad_f32(const float* GY, const float* X, float* dW, float* db,
+                            void* workspace, int N, int M, int K, int P, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -548,6 +548,56 @@ def test_conv1x1_gemm_matches_fp32_reference(hip, N, k1, k2, m, hw):
     assert (out.double().cpu() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("N,k,m,hw", [(1, 128, 128, 4), (2, 128, 256, 16), (3, 384, 128, 20),
+                                     (8, 256, 256, 64)])
+def test_conv1x1_wgrad_gemm_matches_fp64(hip, N, k, m, hw):
+    """1x1 weight / bias gradient GEMM (split-K over pixels, one split and many) vs float64:
+    dw = sum_n gy[n] x[n]^T, db = gy.sum((0, 2, 3)) (1e-5 relative); deterministic."""
+    from op.conv import _wgrad1x1_raw
+    g = torch.Generator().manual_seed(N * 1000 + k + m + hw)
+    x = torch.randn(N, k, hw, hw, generator=g)
+    gy = torch.randn(N, m, hw, hw, generator=g)
+    ref_w = torch.einsum("nmp,nkp->mk", gy.double().flatten(2), x.double().flatten(2))
+    ref_b = gy.double().sum((0, 2, 3))
+    dw, db = _wgrad1x1_raw(gy.to(hip), x.to(hip), True)
+    assert (dw.double().cpu() - ref_w).abs().max().item() <= 1e-5 * ref_w.abs().max().item()
+    assert (db.double().cpu() - ref_b).abs().max().item() <= 1e-5 * ref_b.abs().max().item()
+    dw2, _ = _wgrad1x1_raw(gy.to(hip), x.to(hip), False)
+    assert torch.equal(dw, dw2)
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(128, 256, 16), (256, 128, 32), (384, 128, 16)])
+def test_conv1x1_autograd_double_backward(hip, cin, cout, hw):
+    """conv1x1_ad (GEMM kernels for the forward, its adjoint and the weight / bias gradient,
+    each differentiable again) vs F.conv2d: forward, first and second derivatives w.r.t.
+    x, w, b (2e-5 relative)."""
+    from op.conv import conv1x1_ad
+    g = torch.Generator().manual_seed(cin + cout + hw)
+    x0 = torch.randn(2, cin, hw, hw, generator=g)
+    w0 = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b0 = torch.randn(cout, generator=g)
+    go = torch.randn(2, cout, hw, hw, generator=g).to(hip)
+    v = torch.randn(2, cin, hw, hw, generator=g).to(hip)
+
+    def run(fn):
+        x = x0.to(hip).requires_grad_()
+        w = w0.to(hip).requires_grad_()
+        b = b0.to(hip).requires_grad_()
+        y = fn(torch.tanh(x), w, b)
+        gx, gw, gb = torch.autograd.grad(y, (x, w, b), go, create_graph=True)
+        second = torch.autograd.grad((gx * v).sum() + (gw * gw).sum() + (gx * gx).sum()
+                                     + (gb * gb).sum(), (x, w, b), allow_unused=True)
+        return (y.detach(), gx.detach(), gw.detach(), gb.detach()) + second
+
+    got = run(conv1x1_ad)
+    ref = run(lambda x, w, b: F.conv2d(x, w, b))
+    for a, r in zip(got, ref):
+        if r is None:
+            assert a is None or a.abs().max().item() == 0
+            continue
+        assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
+
+
 def test_conv3x3_winograd_two_sources(hip):
     """The Winograd conv reading [x1, x2] as two sources equals the conv of their
     concatenation (same kernel, same chunk order: bit-identical), incl. the GroupNorm
