@@ -8,13 +8,15 @@ continuous, likelihood_weighting)` -> `step_fn(state, batch)` with
 state = {'optimizer', 'model', 'ema', 'step'}.
 
 MI355X notes: the model runs on the fused HIP block ops; Adam uses the
-multi-tensor (foreach) implementation; for batch-sharded data parallelism wrap
+fused multi-tensor implementation on the GPU (BPK_ADAM_FUSED=0: foreach); for batch-sharded data parallelism wrap
 the model in torch DistributedDataParallel (RCCL all-reduce of the gradient
 buckets, overlapped with backward) -- each rank's loss is the mean over its
 shard, so the averaged gradient equals the single-process full-batch gradient.
 The PINN step functions live in pinn_kalman/.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -24,13 +26,23 @@ from models import utils as mutils
 from sde_lib import VESDE, VPSDE
 
 
+_ADAM_FUSED = os.environ.get("BPK_ADAM_FUSED", "1") != "0"
+
+
 def get_optimizer(config, params, lr_mul=1.0, is_bpinn=False):
     lr = config.optim.bpinn_lr if is_bpinn else config.optim.lr
     decay = config.optim.bpinn_weight_decay if is_bpinn else config.optim.weight_decay
     if config.optim.optimizer != "Adam":
         raise NotImplementedError(f"Optimizer {config.optim.optimizer} not supported yet!")
+    params = list(params)
+    # on the GPU: the fused (single multi-tensor kernel per step) Adam, which also keeps the
+    # per-parameter step counts and bias corrections on the device -- the foreach form
+    # spends ~ms of host time per step on them for the ~700 NCSN++ tensors
+    fused = _ADAM_FUSED and len(params) > 0 and all(
+        (p["params"][0] if isinstance(p, dict) else p).is_cuda for p in params)
+    kind = dict(fused=True) if fused else dict(foreach=True)
     return optim.Adam(params, lr=lr * lr_mul, betas=(config.optim.beta1, 0.999),
-                      eps=config.optim.eps, weight_decay=decay, foreach=True)
+                      eps=config.optim.eps, weight_decay=decay, **kind)
 
 
 def optimization_manager(config, is_bpinn=False):
