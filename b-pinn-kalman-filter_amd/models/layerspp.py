@@ -166,7 +166,7 @@ class ResnetBlockDDPMpp(nn.Module):
         h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
         if temb is not None:
-            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+            bias_nc = bias_nc + layers.temb_proj(self.Dense_0, self.act, temb)
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
         h = self.Dropout_0(h)
         if x.shape[1] != self.out_ch:
@@ -234,7 +234,7 @@ class ResnetBlockBigGANpp(nn.Module):
                                  stats=layers._GN_STATS)
         bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
         if temb is not None:
-            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+            bias_nc = bias_nc + layers.temb_proj(self.Dense_0, self.act, temb)
         bias = self.Conv_1.bias + self.Conv_2.bias
         x = conv_op.conv1x1(x1, self.Conv_2.weight, None, x2)
         div = np.sqrt(2.) if self.skip_rescale else 1.0
@@ -257,7 +257,7 @@ class ResnetBlockBigGANpp(nn.Module):
             h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
         if temb is not None:
-            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+            bias_nc = bias_nc + layers.temb_proj(self.Dense_0, self.act, temb)
         bias = self.Conv_1.bias
         if self.in_ch != self.out_ch or self.up or self.down:
             # the 1x1 skip conv's bias joins Conv_1's in the fused residual (no separate

@@ -22,6 +22,8 @@ from . import layers, layerspp, utils
 
 # up-path skip concatenations read as two sources at inference (BPK_PAIR=0: torch.cat)
 _PAIR = os.environ.get("BPK_PAIR", "1") != "0"
+# all residual blocks' time-embedding projections as one GEMM at inference (BPK_TEMB_BANK=0: off)
+_TEMB_BANK = os.environ.get("BPK_TEMB_BANK", "1") != "0"
 conv3x3 = layerspp.conv3x3
 default_initializer = layers.default_init
 _SQRT2 = np.sqrt(2.)
@@ -182,6 +184,7 @@ class NCSNpp(nn.Module):
             plan.append(("head_pyramid",))
         self.all_modules = nn.ModuleList(mods)
         self._plan = plan
+        self._denses = None  # residual blocks' Dense_0, for layers.TembBank
 
     # ------------------------------------------------------------------
     def _time_embedding(self, time_cond):
@@ -212,6 +215,11 @@ class NCSNpp(nn.Module):
     def forward(self, x, time_cond):
         mods = self.all_modules
         temb, used_sigmas = self._time_embedding(time_cond)
+        if temb is not None and _TEMB_BANK and layers.fused_inference_ok(self, x, self.act):
+            if self._denses is None:
+                self._denses = [m.Dense_0 for m in self.all_modules
+                                if hasattr(m, "Dense_0") and isinstance(m.Dense_0, nn.Linear)]
+            temb = layers.TembBank(temb, self.act, self._denses)
         if not self.config.data.centered:
             x = 2 * x - 1.
         pyramid = x if self.progressive_input != "none" else None
