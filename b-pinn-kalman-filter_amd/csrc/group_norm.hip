@@ -713,9 +713,9 @@ extern "C" int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, c
 // over the partials, fixed reduction order (deterministic).
 namespace {
 __global__ __launch_bounds__(256) void gn_affine_partials_kernel(
-    const float2* __restrict__ part, int R, float cnt, const float* __restrict__ bias_nc,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float2* __restrict__ ss,
-    int C, int G, float eps) {
+    const float2* __restrict__ part, const float2* __restrict__ part2, int C1, int R, float cnt,
+    const float* __restrict__ bias_nc, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float2* __restrict__ ss, int C, int G, float eps) {
   __shared__ float sbuf[256 / kWave];
   __shared__ float s_stat[2];
   const int ng = blockIdx.x;
@@ -723,14 +723,21 @@ __global__ __launch_bounds__(256) void gn_affine_partials_kernel(
   const int g = ng - n * G;
   const int cpg = C / G;
   const int K = cpg * R;
-  const float2* pg = part + ((int64_t)n * C + (int64_t)g * cpg) * R;
-  const float* bn = bias_nc ? bias_nc + (int64_t)n * C + g * cpg : nullptr;
+  // partials of channel c: part [N, C1, R] for c < C1, part2 [N, C - C1, R] after (the two
+  // halves of a channel concatenation, read in place)
+  const int c0 = g * cpg;
+  auto at = [&](int i) -> float2 {
+    const int c = c0 + i / R, r = i - (i / R) * R;
+    return c < C1 ? part[((int64_t)n * C1 + c) * R + r]
+                  : part2[((int64_t)n * (C - C1) + (c - C1)) * R + r];
+  };
+  const float* bn = bias_nc ? bias_nc + (int64_t)n * C + c0 : nullptr;
   float ls = 0.f;
-  for (int i = threadIdx.x; i < K; i += blockDim.x) ls += pg[i].x + (bn ? bn[i / R] : 0.f);
+  for (int i = threadIdx.x; i < K; i += blockDim.x) ls += at(i).x + (bn ? bn[i / R] : 0.f);
   const float mean = block_sum<256>(ls, sbuf) / (float)K;
   float lm2 = 0.f;
   for (int i = threadIdx.x; i < K; i += blockDim.x) {
-    const float2 p = pg[i];
+    const float2 p = at(i);
     const float d = p.x + (bn ? bn[i / R] : 0.f) - mean;
     lm2 += p.y + cnt * d * d;
   }
@@ -759,8 +766,26 @@ extern "C" int bpk_group_norm_affine_partials_f32(const float* part, int R, int 
   BPK_REQUIRE((int64_t)(C / G) * R < (1ll << 31), "group_norm_affine_partials: too many partials");
   if (N == 0) return BPK_OK;
   hipLaunchKernelGGL(gn_affine_partials_kernel, dim3(N * G), dim3(256), 0, bpk::as_stream(stream),
-                     reinterpret_cast<const float2*>(part), R, (float)cnt, bias_nc, gamma, beta,
-                     reinterpret_cast<float2*>(scale_shift), C, G, eps);
+                     reinterpret_cast<const float2*>(part), nullptr, C, R, (float)cnt, bias_nc,
+                     gamma, beta, reinterpret_cast<float2*>(scale_shift), C, G, eps);
   BPK_LAUNCH_CHECK("group_norm_affine_partials");
+  return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_affine_partials2_f32(const float* part, int C1, const float* part2,
+                                                   int R, int cnt, const float* bias_nc,
+                                                   const float* gamma, const float* beta,
+                                                   float* scale_shift, int N, int C, int G,
+                                                   float eps, void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && G > 0 && R > 0 && cnt > 0 && C1 > 0 && C1 < C,
+              "group_norm_affine_partials2: bad shape");
+  BPK_REQUIRE(C % G == 0, "group_norm_affine_partials2: C (%d) not divisible by G (%d)", C, G);
+  BPK_REQUIRE((int64_t)(C / G) * R < (1ll << 31), "group_norm_affine_partials2: too many partials");
+  if (N == 0) return BPK_OK;
+  hipLaunchKernelGGL(gn_affine_partials_kernel, dim3(N * G), dim3(256), 0, bpk::as_stream(stream),
+                     reinterpret_cast<const float2*>(part), reinterpret_cast<const float2*>(part2),
+                     C1, R, (float)cnt, bias_nc, gamma, beta,
+                     reinterpret_cast<float2*>(scale_shift), C, G, eps);
+  BPK_LAUNCH_CHECK("group_norm_affine_partials2");
   return BPK_OK;
 }

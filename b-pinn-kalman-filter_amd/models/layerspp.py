@@ -228,8 +228,7 @@ class ResnetBlockBigGANpp(nn.Module):
               and conv_op.gemm1x1_supported(x1, self.Conv_2.weight, x2))
         if not ok:
             return self.forward(layers.cat_channels(x1, x2), temb)
-        ss = group_norm_affine_partials((torch.cat([p1[0], p2[0]], 1), p1[1], p1[2]),
-                                        x1.shape[0], C, self.GroupNorm_0)
+        ss = group_norm_affine_partials(p1, x1.shape[0], C, self.GroupNorm_0, part2=p2)
         h = conv_op.conv3x3_pair(x1, x2, self.Conv_0.weight, pre=ss,
                                  stats=layers._GN_STATS)
         bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)

@@ -83,19 +83,30 @@ def group_norm_act_f(x, num_groups, weight, bias, eps, act=ACT_SILU, bias_nc=Non
     return _GroupNormAct.apply(x, bias_nc, weight, bias, num_groups, eps, act)
 
 
-def group_norm_affine_partials(part, N, C, gn: torch.nn.GroupNorm, bias_nc=None):
-    """(s, t) [N, C, 2] from partial statistics (part [N, C, R, 2], R, cnt) -- e.g. those of
-    a channel concatenation assembled from its parts' -- without touching the tensor."""
+def group_norm_affine_partials(part, N, C, gn: torch.nn.GroupNorm, bias_nc=None, part2=None):
+    """(s, t) [N, C, 2] from partial statistics (part [N, C, R, 2], R, cnt) without touching
+    the tensor; part2 given: the tensor is the channel concatenation of two whose partials
+    are part (first C1 channels) and part2 (the rest), read in place."""
     pt, R, cnt = part
     ss = torch.empty((N, C, 2), device=pt.device, dtype=torch.float32)
     bnc = bias_nc.contiguous() if bias_nc is not None else None
     w = gn.weight if gn.affine else None
     b = gn.bias if gn.affine else None
-    check(lib.bpk_group_norm_affine_partials_f32(
-        pt.data_ptr(), R, cnt, bnc.data_ptr() if bnc is not None else None,
-        w.detach().data_ptr() if w is not None else None,
-        b.detach().data_ptr() if b is not None else None, ss.data_ptr(), N, C,
-        gn.num_groups, float(gn.eps), stream_ptr(pt.device)), "group_norm_affine_partials")
+    wp = w.detach().data_ptr() if w is not None else None
+    bp = b.detach().data_ptr() if b is not None else None
+    bncp = bnc.data_ptr() if bnc is not None else None
+    if part2 is None:
+        check(lib.bpk_group_norm_affine_partials_f32(
+            pt.data_ptr(), R, cnt, bncp, wp, bp, ss.data_ptr(), N, C, gn.num_groups,
+            float(gn.eps), stream_ptr(pt.device)), "group_norm_affine_partials")
+        return ss
+    pt2, R2, cnt2 = part2
+    C1 = pt.shape[1]
+    if (R2, cnt2) != (R, cnt) or pt.shape[0] != N or pt2.shape[:2] != (N, C - C1):
+        raise RuntimeError("group_norm_affine_partials: mismatched partials of the two parts")
+    check(lib.bpk_group_norm_affine_partials2_f32(
+        pt.data_ptr(), C1, pt2.data_ptr(), R, cnt, bncp, wp, bp, ss.data_ptr(), N, C,
+        gn.num_groups, float(gn.eps), stream_ptr(pt.device)), "group_norm_affine_partials2")
     return ss
 
 

@@ -200,6 +200,14 @@ int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float*
 int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt, const float* bias_nc,
                                        const float* gamma, const float* beta, float* scale_shift,
                                        int N, int C, int G, float eps, void* stream);
+/* Same for the channel concatenation [x1 (C1 channels), x2 (C - C1)] from the two tensors'
+ * own partials (part [N, C1, R, 2], part2 [N, C - C1, R, 2]) -- the up path's
+ * torch.cat([h, hs.pop()], 1) (reference models/ncsnpp.py:318) without concatenating
+ * either; bit-identical to the single-source entry on the concatenated partials. */
+int bpk_group_norm_affine_partials2_f32(const float* part, int C1, const float* part2, int R,
+                                        int cnt, const float* bias_nc, const float* gamma,
+                                        const float* beta, float* scale_shift, int N, int C,
+                                        int G, float eps, void* stream);
 int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
                            const float* gamma, const float* beta, const float* mean,
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,

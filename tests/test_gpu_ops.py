@@ -469,6 +469,19 @@ def test_conv3x3_winograd_gn_partial_statistics(hip, with_bias_nc):
         got = group_norm_affine(cat, gn, bnc)
         ref = group_norm_affine(cat.clone(), gn, bnc)   # clone: no partials -> full pass
         assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+        # the two parts' partials read in place == the concatenated partials (bit-identical),
+        # also when a group straddles the boundary (192 channels / 32 groups, C1 = 128)
+        from op.norm_act import group_norm_affine_partials
+        two = group_norm_affine_partials(gn_partials(y), N, 2 * Co, gn, bnc, part2=gn_partials(y2))
+        assert torch.equal(two, got)
+        y3 = conv3x3(skip, w.new_zeros(64, Co, 3, 3) + 0.02, None, stats=True)
+        gn3 = torch.nn.GroupNorm(32, Co + 64, eps=1e-6).to(hip)
+        cat3 = cat_channels(y, y3)
+        two3 = group_norm_affine_partials(gn_partials(y), N, Co + 64, gn3, None,
+                                          part2=gn_partials(y3))
+        assert torch.equal(two3, group_norm_affine(cat3, gn3))
+        ref3 = group_norm_affine(cat3.clone(), gn3)
+        assert (two3 - ref3).abs().max().item() <= 1e-5 * ref3.abs().max().item()
         # an in-place update invalidates the attached statistics
         y.add_(1.0)
         assert gn_partials(y) is None
