@@ -754,6 +754,28 @@ __global__ __launch_bounds__(256) void gn_affine_partials_kernel(
     ss[(int64_t)n * C + c] = make_float2(sc, (beta ? beta[c] : 0.f) + (b - s_stat[0]) * sc);
   }
 }
+
+// (mean, M2) of every 128 consecutive values of x: one wave per chunk, one float2 per lane.
+// For a plane of H*W % 128 == 0 pixels these are the GroupNorm partial statistics of
+// bpk_group_norm_affine_partials_f32 (R = H*W / 128 per (n, c), cnt = 128) for a tensor
+// whose producer wrote none.
+__global__ __launch_bounds__(256) void gn_chunk_partials_kernel(const float* __restrict__ x,
+                                                                float2* __restrict__ part,
+                                                                int64_t nchunks) {
+  const int64_t ch = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= nchunks) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const float2 v = reinterpret_cast<const float2*>(x + ch * 128)[lane];
+  float s = v.x + v.y;
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+  const float mean = s * (1.f / 128.f);
+  const float a = v.x - mean, b = v.y - mean;
+  float m2 = a * a + b * b;
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) m2 += __shfl_xor(m2, off, kWave);
+  if (lane == 0) part[ch] = make_float2(mean, m2);
+}
 }  // namespace
 
 extern "C" int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt,
@@ -787,5 +809,19 @@ extern "C" int bpk_group_norm_affine_partials2_f32(const float* part, int C1, co
                      C1, R, (float)cnt, bias_nc, gamma, beta,
                      reinterpret_cast<float2*>(scale_shift), C, G, eps);
   BPK_LAUNCH_CHECK("group_norm_affine_partials2");
+  return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_chunk_partials_f32(const float* x, float* part, int N, int C,
+                                                 int64_t HW, void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && HW % 128 == 0,
+              "group_norm_chunk_partials: need H*W %% 128 == 0 (got %lld)", (long long)HW);
+  const int64_t nchunks = (int64_t)N * C * (HW / 128);
+  if (nchunks == 0) return BPK_OK;
+  BPK_REQUIRE(bpk::ceil_div(nchunks, 4) < (1LL << 31), "group_norm_chunk_partials: too large");
+  hipLaunchKernelGGL(gn_chunk_partials_kernel, dim3((unsigned)bpk::ceil_div(nchunks, 4)),
+                     dim3(256), 0, bpk::as_stream(stream), x, reinterpret_cast<float2*>(part),
+                     nchunks);
+  BPK_LAUNCH_CHECK("group_norm_chunk_partials");
   return BPK_OK;
 }

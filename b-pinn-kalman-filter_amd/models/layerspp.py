@@ -217,15 +217,18 @@ class ResnetBlockBigGANpp(nn.Module):
         two-source MFMA GEMM.  Falls back to the concatenation when a piece does not fit."""
         from op import conv as conv_op
         from op.norm_act import group_norm_affine_partials
-        p1, p2 = conv_op.gn_partials(x1), conv_op.gn_partials(x2)
         C1, C = x1.shape[1], x1.shape[1] + x2.shape[1]
         ok = (layers.fused_inference_ok(self, x1, self.act) and not (self.up or self.down)
-              and hasattr(self, "Conv_2") and p1 is not None and p2 is not None
-              and p1[1:] == p2[1:] and C1 % 8 == 0
+              and hasattr(self, "Conv_2") and C1 % 8 == 0
               and x1.dtype == torch.float32 and self.Conv_0.weight.shape[1] == C
               and bool(conv_op.lib.bpk_conv3x3_wino_supported(
                   x1.shape[0], C, self.Conv_0.out_channels, x1.shape[2], x1.shape[3]))
               and conv_op.gemm1x1_supported(x1, self.Conv_2.weight, x2))
+        if ok:
+            # partial statistics of both parts (one read of a part whose producer wrote
+            # none: still cheaper than concatenating and reading the concatenation)
+            p1, p2 = conv_op.ensure_gn_partials(x1), conv_op.ensure_gn_partials(x2)
+            ok = p1 is not None and p2 is not None and p1[1:] == p2[1:]
         if not ok:
             return self.forward(layers.cat_channels(x1, x2), temb)
         ss = group_norm_affine_partials(p1, x1.shape[0], C, self.GroupNorm_0, part2=p2)

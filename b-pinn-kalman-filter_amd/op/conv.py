@@ -78,6 +78,24 @@ def attach_gn_partials(t, part, R, cnt=GN_PART_COUNT):
     return t
 
 
+def ensure_gn_partials(t):
+    """gn_partials(t), computing them with one read of t (bpk_group_norm_chunk_partials_f32)
+    when its producer attached none; None when the shape has no partials form."""
+    p = gn_partials(t)
+    if p is not None:
+        return p
+    if (t.dim() != 4 or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous()
+            or (t.shape[2] * t.shape[3]) % GN_PART_COUNT != 0):
+        return None
+    N, C, H, W = t.shape
+    R = H * W // GN_PART_COUNT
+    part = torch.empty((N, C, R, 2), dtype=torch.float32, device=t.device)
+    check(lib.bpk_group_norm_chunk_partials_f32(t.data_ptr(), part.data_ptr(), N, C, H * W,
+                                                stream_ptr(t.device)), "gn_partials")
+    attach_gn_partials(t, part, R)
+    return part, R, GN_PART_COUNT
+
+
 def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False, x2=None):
     """conv(a, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch),
     where a = x, or silu(x * s + t) with pre[n, c] = (s, t) (GroupNorm+SiLU fused in).

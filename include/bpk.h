@@ -208,6 +208,11 @@ int bpk_group_norm_affine_partials2_f32(const float* part, int C1, const float* 
                                         int cnt, const float* bias_nc, const float* gamma,
                                         const float* beta, float* scale_shift, int N, int C,
                                         int G, float eps, void* stream);
+/* Partial statistics for a tensor whose producer wrote none: part [N, C, HW / 128, 2] =
+ * (mean, M2) of each run of 128 consecutive pixels (HW % 128 == 0), the form both entries
+ * above consume (R = HW / 128, cnt = 128).  One read of x. */
+int bpk_group_norm_chunk_partials_f32(const float* x, float* part, int N, int C, int64_t HW,
+                                      void* stream);
 int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
                            const float* gamma, const float* beta, const float* mean,
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,

@@ -482,6 +482,12 @@ def test_conv3x3_winograd_gn_partial_statistics(hip, with_bias_nc):
         assert torch.equal(two3, group_norm_affine(cat3, gn3))
         ref3 = group_norm_affine(cat3.clone(), gn3)
         assert (two3 - ref3).abs().max().item() <= 1e-5 * ref3.abs().max().item()
+        # partials computed from a plain tensor (one pass) give the same affine form
+        from op.conv import ensure_gn_partials
+        plain2 = cat.clone()
+        assert gn_partials(plain2) is None and ensure_gn_partials(plain2) is not None
+        got2 = group_norm_affine(plain2, gn, bnc)
+        assert (got2 - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
         # an in-place update invalidates the attached statistics
         y.add_(1.0)
         assert gn_partials(y) is None
@@ -631,10 +637,12 @@ def test_conv3x3_winograd_two_sources(hip):
     assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6 * pb.abs().max().item())
 
 
-def test_resblock_forward_pair_matches_concat(hip):
+@pytest.mark.parametrize("hs_stats", [True, False])
+def test_resblock_forward_pair_matches_concat(hip, hs_stats):
     """ResnetBlockBigGANpp.forward_pair(h, hs) (no concatenation: partial-statistics
     GroupNorm, two-source Winograd conv, two-source 1x1 GEMM) == forward(cat([h, hs]))
-    within 1e-5 relative, and the output carries partial statistics."""
+    within 1e-5 relative, and the output carries partial statistics.  hs_stats=False: hs
+    comes without partials (they are computed from it in one pass)."""
     import models.layerspp as lpp
     from models.layers import cat_channels
     from op.conv import conv3x3, gn_partials
@@ -649,8 +657,8 @@ def test_resblock_forward_pair_matches_concat(hip):
         w1 = (torch.randn(128, 64, 3, 3, generator=g) * 0.05).to(hip)
         w2 = (torch.randn(128, 64, 3, 3, generator=g) * 0.05).to(hip)
         h = conv3x3(src, w1, stats=True)      # producers that attach partial statistics
-        hs = conv3x3(src, w2, stats=True)
-        assert gn_partials(h) is not None and gn_partials(hs) is not None
+        hs = conv3x3(src, w2, stats=hs_stats)
+        assert gn_partials(h) is not None and (gn_partials(hs) is not None) == hs_stats
         temb = torch.randn(2, 512, generator=g).to(hip)
         out = blk.forward_pair(h, hs, temb)
         ref = blk(cat_channels(h, hs), temb)
