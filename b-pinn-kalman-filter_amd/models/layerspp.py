@@ -11,6 +11,9 @@ Per block the arithmetic is re-scheduled for the GPU:
 """
 from __future__ import annotations
 
+import math
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -19,6 +22,9 @@ import torch.nn.functional as F
 from op.norm_act import residual_rescale
 
 from . import layers, up_or_down_sampling
+
+# attention at inference: q, k, v as one GEMM over the stacked NIN weights (BPK_ATTN_QKV=0: off)
+_ATTN_QKV = os.environ.get("BPK_ATTN_QKV", "1") != "0"
 
 conv1x1 = layers.ddpm_conv1x1
 conv3x3 = layers.ddpm_conv3x3
@@ -72,8 +78,38 @@ class AttnBlockpp(nn.Module):
 
     def forward(self, x):
         h = gn_act(x, self.GroupNorm_0, None)
+        div = np.sqrt(2.) if self.skip_rescale else 1.0
+        if _ATTN_QKV and not torch.is_grad_enabled() and self._qkv_ok(h):
+            return residual_rescale(x, self._forward_qkv(h), None, div)
         h = self.NIN_3(layers._attention(h, self.NIN_0, self.NIN_1, self.NIN_2))
-        return residual_rescale(x, h, None, np.sqrt(2.) if self.skip_rescale else 1.0)
+        return residual_rescale(x, h, None, div)
+
+    def _qkv_ok(self, h):
+        from op import conv as conv_op
+        N, C, H, W = h.shape
+        return (h.is_cuda and h.dtype == torch.float32
+                and bool(conv_op.lib.bpk_gemm_nchw_supported(N, 3 * C, H * W, C, 0))
+                and bool(conv_op.lib.bpk_gemm_nchw_supported(N, C, H * W, C, 0)))
+
+    def _forward_qkv(self, h):
+        """Inference: q, k, v as ONE MFMA GEMM over the stacked NIN weights, NIN_3 as another
+        (op.conv.conv1x1), the 1/sqrt(C) scale folded into q's weights when it is a power of
+        two (exact: C = 4^k, e.g. 256) and applied to the logits otherwise."""
+        from op import conv as conv_op
+        B, C, H, W = h.shape
+        s = float(int(C) ** (-0.5))
+        fold = math.frexp(s)[0] == 0.5  # s is a power of two
+        sq = s if fold else 1.0
+        wqkv = torch.cat([self.NIN_0.W.t() * sq, self.NIN_1.W.t(), self.NIN_2.W.t()], 0)
+        bqkv = torch.cat([self.NIN_0.b * sq, self.NIN_1.b, self.NIN_2.b], 0)
+        qkv = conv_op.conv1x1(h, wqkv, bqkv).reshape(B, 3, C, H * W)
+        q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
+        w = torch.bmm(q.transpose(1, 2), k)
+        if not fold:
+            w = w * s
+        w = torch.softmax(w, dim=-1)
+        out = torch.bmm(v, w.transpose(1, 2)).reshape(B, C, H, W)
+        return conv_op.conv1x1(out, self.NIN_3.W.t(), self.NIN_3.b)
 
 
 class Upsample(nn.Module):

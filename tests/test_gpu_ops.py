@@ -696,3 +696,25 @@ def test_conv2d_general_double_backward(hip, k, stride, pad, cin, cout):
             assert a is None or a.abs().max().item() == 0
             continue
         assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
+
+
+@pytest.mark.parametrize("C,hw", [(256, 16), (128, 16)])
+def test_attention_qkv_gemm_matches_unfused(hip, C, hw):
+    """AttnBlockpp at inference (q, k, v as one GEMM over the stacked NIN weights, scale
+    folded into q when 1/sqrt(C) is a power of two) == the per-NIN composition (1e-5 rel)."""
+    import models.layerspp as lpp
+    from models import layers
+    torch.manual_seed(C)
+    blk = lpp.AttnBlockpp(channels=C, skip_rescale=True, init_scale=0.).to(hip).eval()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn_like(p) * 0.1)
+        x = torch.randn(2, C, hw, hw, device=hip)
+        h = layers.gn_act(x, blk.GroupNorm_0, None)
+        assert blk._qkv_ok(h)
+        got = blk._forward_qkv(h)
+        ref = blk.NIN_3(layers._attention(h, blk.NIN_0, blk.NIN_1, blk.NIN_2))
+        assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+        out = blk(x)
+        assert (out - lpp.residual_rescale(x, ref, None, 2 ** 0.5)).abs().max().item() <= \
+            1e-5 * out.abs().max().item()
