@@ -44,14 +44,22 @@ constexpr int kOutRows = 2 * kTR, kOutCols = 2 * kTC;  // 8 x 16 pixels
 // U[cin][cout][pos] = (G g G^T)[pos] with G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
 // (the 16 positions of one (cin, cout) pair are contiguous: one lane of the GEMM loads
 // its B operands for all positions with four 16-B loads)
+// Cout not a multiple of 64: U is laid out for CoutP = Cout rounded up to 64 couts, the
+// extra couts zero (the conv computes them and never stores them).
 __global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restrict__ w,
                                                           float* __restrict__ U, int Cin,
-                                                          int Cout) {
-  const int64_t total = (int64_t)Cin * Cout;
+                                                          int Cout, int CoutP) {
+  const int64_t total = (int64_t)Cin * CoutP;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int co = (int)(i % Cout);
-    const int ci = (int)(i / Cout);
+    const int co = (int)(i % CoutP);
+    const int ci = (int)(i / CoutP);
+    if (co >= Cout) {
+      f4* u = reinterpret_cast<f4*>(U + ((int64_t)ci * CoutP + co) * 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) u[r] = f4{0.f, 0.f, 0.f, 0.f};
+      continue;
+    }
     const float* g = w + ((int64_t)co * Cin + ci) * 9;
     float t[4][3];  // G g
 #pragma unroll
@@ -62,7 +70,7 @@ __global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restric
       t[2][c] = 0.5f * (g0 - g1 + g2);
       t[3][c] = g2;
     }
-    float* u = U + ((int64_t)ci * Cout + co) * 16;
+    float* u = U + ((int64_t)ci * CoutP + co) * 16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float a0 = t[r][0], a1 = t[r][1], a2 = t[r][2];
@@ -79,6 +87,7 @@ struct WinoGeo {
   int regions_x, regions_y, cout_blocks;
   float div;  // fused residual: y = (skip + (conv + bias)) / div when skip != nullptr
   int C1;     // input channels [0, C1) from x, [C1, Cin) from x2 (pipelined kernel only)
+  int CoutS;  // couts stored (y, skip, stats channel count); Cout = CoutS rounded up to 64
 };
 
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
@@ -118,6 +127,7 @@ template <int kWN>
 __device__ inline void store_tile(const float* s_w, const float* __restrict__ skip,
                                   float* __restrict__ y, float2* __restrict__ stats,
                                   const WinoGeo& g, int n, int cout_w, int oy0, int ox0, int lane) {
+  if (cout_w >= g.CoutS) return;  // padded couts (wave-uniform: CoutS % 16 == 0)
   const int64_t plane = (int64_t)g.H * g.W;
   constexpr int kIt = kWN / 2;
   float mm[kIt], qq[kIt];
@@ -128,7 +138,7 @@ __device__ inline void store_tile(const float* s_w, const float* __restrict__ sk
     const int rem = q & 31;
     const int row = rem >> 2, c4 = rem & 3;
     f4 v = *reinterpret_cast<const f4*>(&s_w[co * kOS + row * kOutCols + 4 * c4]);
-    const int64_t o = (int64_t)n * g.Cout * plane + (int64_t)(cout_w + co) * plane +
+    const int64_t o = (int64_t)n * g.CoutS * plane + (int64_t)(cout_w + co) * plane +
                       (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
     if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
       const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
@@ -166,7 +176,7 @@ __device__ inline void store_tile(const float* s_w, const float* __restrict__ sk
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
       const int co = (it * 64 + lane) >> 5;
-      stats[((int64_t)n * g.Cout + cout_w + co) * R + region] = make_float2(mm[it], qq[it]);
+      stats[((int64_t)n * g.CoutS + cout_w + co) * R + region] = make_float2(mm[it], qq[it]);
     }
   }
 }
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     float* so = &s_out[(wave * kWN + 16 * nb + jj) * kOS];
-    const float bv = bias ? bias[cout_w + 16 * nb + jj] : 0.f;
+    const float bv = (bias && cout_w + 16 * nb + jj < g.CoutS) ? bias[cout_w + 16 * nb + jj] : 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
@@ -622,7 +632,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     float* so = &s_out[(wave * kWN + 16 * nb + jj) * kOS];
-    const float bv = bias ? bias[cout_w + 16 * nb + jj] : 0.f;
+    const float bv = (bias && cout_w + 16 * nb + jj < g.CoutS) ? bias[cout_w + 16 * nb + jj] : 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
@@ -962,23 +972,36 @@ __global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
 
 }  // namespace
 
+static int cout_padded(int Cout) { return (Cout + 63) / 64 * 64; }
+
+// the software-pipelined kernel (=2: 128 couts per workgroup) unless BPK_WINO_PIPE=0
+static int wino_pipe_env() {
+  static const int v = [] {
+    const char* e = getenv("BPK_WINO_PIPE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
-  return (int64_t)16 * Cin * Cout * (int64_t)sizeof(float);
+  return (int64_t)16 * Cin * cout_padded(Cout) * (int64_t)sizeof(float);
 }
 
 extern "C" int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout,
                                            void* stream) {
   BPK_REQUIRE(Cin > 0 && Cout > 0, "conv3x3_wino_filter: bad channels %d -> %d", Cin, Cout);
-  const int64_t total = (int64_t)Cin * Cout;
+  const int64_t total = (int64_t)Cin * cout_padded(Cout);
   hipLaunchKernelGGL(wino_filter_kernel, dim3((unsigned)std::min<int64_t>(bpk::ceil_div(total, 256), 4096)),
-                     dim3(256), 0, bpk::as_stream(stream), weight, U, Cin, Cout);
+                     dim3(256), 0, bpk::as_stream(stream), weight, U, Cin, Cout,
+                     cout_padded(Cout));
   BPK_LAUNCH_CHECK("conv3x3_wino_filter");
   return BPK_OK;
 }
 
 extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W) {
-  return N > 0 && Cin > 0 && Cin % kCK == 0 && Cout % 64 == 0 && H % kOutRows == 0 &&
-         W % kOutCols == 0;
+  // Cout % 64 != 0 (multiples of 16): padded to 64 couts, software-pipelined kernel only
+  return N > 0 && Cin > 0 && Cin % kCK == 0 && Cout % 16 == 0 && H % kOutRows == 0 &&
+         W % kOutCols == 0 && (Cout % 64 == 0 || wino_pipe_env() != 0);
 }
 
 extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, const float* pre,
@@ -991,18 +1014,15 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
               "conv3x3_wino: bad channel split C1=%d of Cin=%d", C1, Cin);
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
-              "Cout %% 64, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
+              "Cout %% 16, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
   // NB = 1 (64 couts per workgroup, two workgroups per CU: 2-4 % faster on the NCSN++
   // shapes than NB = 2) unless BPK_WINO_NB=2 asks for the one-workgroup-per-CU form
   static const int nb_env = [] {
     const char* e = getenv("BPK_WINO_NB");
     return e ? atoi(e) : 1;
   }();
-  // the software-pipelined kernel (128 couts per workgroup) unless BPK_WINO_PIPE=0
-  static const int pipe_env = [] {
-    const char* e = getenv("BPK_WINO_PIPE");
-    return e ? atoi(e) : 1;
-  }();
+  const int pipe_env = wino_pipe_env();
+  const int CoutP = cout_padded(Cout);
   // BPK_WINO_PERSIST=1: the persistent form for the GroupNorm-prologue convs (=2: for every
   // conv).  Opt-in: it removes the per-workgroup fixed cost (~2 chunks) but its main loop runs
   // ~9 % slower, a net loss for Cin >= 256 (profiles/r01_conv_persist_sweep.txt).
@@ -1011,8 +1031,8 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     return e ? atoi(e) : 0;
   }();
   if (pipe_env == 1 && (persist_env == 2 || (persist_env == 1 && pre)) && Cin % (2 * kCK) == 0 &&
-      !x2 && (!pre || Cin <= kPreMaxCin)) {
-    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div, Cin};
+      !x2 && (!pre || Cin <= kPreMaxCin) && Cout == CoutP) {
+    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div, Cin, Cout};
     // as many workgroups as are resident at once (2 per CU), each on consecutive items of
     // one image: ipw = items per workgroup divides the items of an image
     static int slots = 0;
@@ -1046,10 +1066,14 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
   }
   BPK_REQUIRE(!x2 || (pipe_env && (!pre || Cin <= kPreMaxCin)),
               "conv3x3_wino: a second input source needs the pipelined kernel");
+  BPK_REQUIRE(Cout == CoutP || (pipe_env && (!pre || Cin <= kPreMaxCin)),
+              "conv3x3_wino: Cout %% 64 != 0 needs the pipelined kernel (Cin <= %d with pre)",
+              kPreMaxCin);
   if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
     // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup
     const int pnb = (pipe_env == 2 && Cout % 128 == 0) ? 2 : 1;
-    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * pnb), div, C1};
+    WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * pnb), div, C1,
+              Cout};
     const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
     BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
     const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -1068,7 +1092,7 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     return BPK_OK;
   }
   const int nb = (Cout % 128 == 0 && nb_env == 2) ? 2 : 1;
-  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div, Cin};
+  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div, Cin, Cout};
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;

@@ -48,13 +48,16 @@ def supported(x, weight):
 
 
 def filter_transform(weight):
-    """U [Cin, Cout, 16], cached on `weight` while its version counter is unchanged."""
+    """U [Cin, CoutP, 16] (CoutP = Cout rounded up to 64), cached on `weight` while its
+    version counter is unchanged."""
     cached = getattr(weight, "_bpk_wino_u", None)
     if cached is not None and cached[0] == weight._version:
         return cached[1]
     w = weight.detach().contiguous()
     Cout, Cin = w.shape[:2]
-    U = torch.empty((Cin, Cout, 16), dtype=torch.float32, device=w.device)
+    # Cout % 64 != 0: U is laid out for Cout rounded up to 64 (zero couts, never stored)
+    CoutP = lib.bpk_conv3x3_wino_filter_bytes(Cin, Cout) // (16 * 4 * Cin)
+    U = torch.empty((Cin, CoutP, 16), dtype=torch.float32, device=w.device)
     check(lib.bpk_conv3x3_wino_filter_f32(w.data_ptr(), U.data_ptr(), Cin, Cout,
                                           stream_ptr(w.device)), "conv3x3 filter")
     weight._bpk_wino_u = (weight._version, U)

@@ -308,9 +308,12 @@ int bpk_correlation_bwd_f32(const float* first, const float* second, const float
  * 3x3 / stride 1 / pad 1 convolution, fused Winograd F(2x2,3x3) on the f32 MFMA
  * (the score networks' conv3x3: models/layers.py ddpm_conv3x3 / layerspp conv3x3,
  * which the reference runs as torch.nn.Conv2d -> cuDNN).
- *   filter: U [Cin, Cout, 16] = G w G^T of w [Cout, Cin, 3, 3] (cache while w is fixed)
+ *   filter: U [Cin, CoutP, 16] = G w G^T of w [Cout, Cin, 3, 3] (cache while w is fixed);
+ *           CoutP = Cout rounded up to 64, the extra couts zero (filter_bytes() sizes it)
  *   conv  : y [N, Cout, H, W] = conv(x [N, Cin, H, W], w) (+ bias[Cout], may be NULL)
- * supported(): Cin % 8 == 0, Cout % 64 == 0, H % 8 == 0, W % 16 == 0.
+ * supported(): Cin % 8 == 0, Cout % 16 == 0, H % 8 == 0, W % 16 == 0 (Cout % 64 != 0: the
+ * pipelined kernel computes CoutP couts and stores Cout -- the PINN networks' 16 / 32 / 96 /
+ * 192-channel convs).
  * ------------------------------------------------------------------------- */
 int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout);
 int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout, void* stream);

@@ -240,7 +240,9 @@ def test_grid_sample_double_backward_gradgradcheck(hip):
 # ------------------------------------------------------------------ Winograd conv3x3
 @pytest.mark.parametrize("N,cin,cout,hw", [(1, 8, 128, 16), (3, 24, 128, 32), (2, 128, 256, 64),
                                            (2, 256, 128, 16), (1, 512, 256, 32),
-                                           (9, 64, 128, 64), (16, 16, 64, 96)])
+                                           (9, 64, 128, 64), (16, 16, 64, 96),
+                                           (2, 16, 16, 64), (3, 32, 32, 32), (2, 64, 96, 16),
+                                           (1, 96, 192, 32)])
 @pytest.mark.parametrize("with_bias", [True, False])
 def test_conv3x3_winograd_matches_fp32_reference(hip, N, cin, cout, hw, with_bias):
     """Fused Winograd F(2x2,3x3) MFMA conv vs a float64 direct convolution; the fp32 MIOpen
@@ -718,3 +720,45 @@ def test_attention_qkv_gemm_matches_unfused(hip, C, hw):
         out = blk(x)
         assert (out - lpp.residual_rescale(x, ref, None, 2 ** 0.5)).abs().max().item() <= \
             1e-5 * out.abs().max().item()
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 16), (16, 32), (64, 96), (32, 192)])
+def test_conv3x3_winograd_padded_cout_fused_variants(hip, cin, cout):
+    """Cout % 64 != 0 (computed for Cout rounded up to 64, Cout stored): GroupNorm+SiLU
+    prologue, residual tail and the output's GroupNorm partial statistics vs the unfused
+    torch composition (2e-5 relative); first and second derivatives vs F.conv2d."""
+    from op.conv import conv3x3, gn_partials
+    from op.norm_act import group_norm_affine
+    g = torch.Generator().manual_seed(cin * 31 + cout)
+    N, H, W = 2, 16, 32
+    x = torch.randn(N, cin, H, W, generator=g).to(hip)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(hip)
+    b = torch.randn(cout, generator=g).to(hip)
+    skip = torch.randn(N, cout, H, W, generator=g).to(hip)
+    pre = torch.stack([torch.rand(N, cin, generator=g) + 0.5,
+                       torch.randn(N, cin, generator=g)], -1).to(hip)
+    with torch.no_grad():
+        a = F.silu(x * pre[..., 0, None, None] + pre[..., 1, None, None])
+        ref = (skip + F.conv2d(a, w, b, padding=1)) / 2 ** 0.5
+        out = conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre, stats=True)
+        assert (out - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+        assert gn_partials(out) is not None
+        gn = torch.nn.GroupNorm(min(cout // 4, 32), cout, eps=1e-6).to(hip)
+        got = group_norm_affine(out, gn)
+        full = group_norm_affine(out.clone(), gn)
+        assert (got - full).abs().max().item() <= 1e-5 * full.abs().max().item()
+    go = torch.randn(N, cout, H, W, generator=g).to(hip)
+    v = torch.randn(N, cin, H, W, generator=g).to(hip)
+
+    def second(fn):
+        xx = x.clone().requires_grad_()
+        ww = w.clone().requires_grad_()
+        y = fn(torch.tanh(xx), ww)
+        gx, gw = torch.autograd.grad(y, (xx, ww), go, create_graph=True)
+        return (gx.detach(), gw.detach()) + torch.autograd.grad(
+            (gx * v).sum() + (gw * gw).sum(), (xx, ww))
+
+    got = second(lambda t, ww: conv3x3(t, ww, b))
+    refs = second(lambda t, ww: F.conv2d(t, ww, b, padding=1))
+    for a_, r_ in zip(got, refs):
+        assert (a_ - r_).abs().max().item() <= 2e-5 * max(1e-6, r_.abs().max().item())

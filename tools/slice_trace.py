@@ -1,7 +1,7 @@
 """Steady-state kernel breakdown from a rocprofv3 kernel trace: drop everything up to the
 end of the warm-up, located as occurrence (per_step * warmup) of a marker kernel that runs a
 fixed number of times per step.
-usage: slice_trace.py trace.csv marker per_step warmup steps [top]"""
+usage: slice_trace.py trace.csv marker per_step warmup steps [top]  (per_step 0: inferred)"""
 import csv
 import sys
 from collections import defaultdict
@@ -11,6 +11,8 @@ per_step, warmup, steps = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
 top = int(sys.argv[6]) if len(sys.argv) > 6 else 25
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+if per_step == 0:  # infer: the marker's total count over warmup + steps
+    per_step = len(idx) // (warmup + steps)
 assert len(idx) == per_step * (warmup + steps), (len(idx), per_step * (warmup + steps))
 lo = idx[per_step * warmup - 1] + 1
 sel = rows[lo:]
