@@ -48,7 +48,7 @@ constexpr int kOutRows = 2 * kTR, kOutCols = 2 * kTC;  // 8 x 16 pixels
 // extra couts zero (the conv computes them and never stores them).
 __global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restrict__ w,
                                                           float* __restrict__ U, int Cin,
-                                                          int Cout, int CoutP) {
+                                                          int Cout, int CoutP, int ft) {
   const int64_t total = (int64_t)Cin * CoutP;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -60,11 +60,14 @@ __global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restric
       for (int r = 0; r < 4; ++r) u[r] = f4{0.f, 0.f, 0.f, 0.f};
       continue;
     }
-    const float* g = w + ((int64_t)co * Cin + ci) * 9;
+    // ft: the filter is flip_t(w) for w [Cin, Cout, 3, 3] (backward-data of the conv with
+    // w): element (co, ci, r, s) = w[ci][co][2 - r][2 - s], read in place
+    const float* g = ft ? w + ((int64_t)ci * Cout + co) * 9 : w + ((int64_t)co * Cin + ci) * 9;
+    auto gv = [&](int k) { return ft ? g[8 - k] : g[k]; };
     float t[4][3];  // G g
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const float g0 = g[c], g1 = g[3 + c], g2 = g[6 + c];
+      const float g0 = gv(c), g1 = gv(3 + c), g2 = gv(6 + c);
       t[0][c] = g0;
       t[1][c] = 0.5f * (g0 + g1 + g2);
       t[2][c] = 0.5f * (g0 - g1 + g2);
@@ -987,15 +990,25 @@ extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
   return (int64_t)16 * Cin * cout_padded(Cout) * (int64_t)sizeof(float);
 }
 
-extern "C" int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout,
-                                           void* stream) {
+static int wino_filter(const float* weight, float* U, int Cin, int Cout, int ft,
+                       void* stream) {
   BPK_REQUIRE(Cin > 0 && Cout > 0, "conv3x3_wino_filter: bad channels %d -> %d", Cin, Cout);
   const int64_t total = (int64_t)Cin * cout_padded(Cout);
   hipLaunchKernelGGL(wino_filter_kernel, dim3((unsigned)std::min<int64_t>(bpk::ceil_div(total, 256), 4096)),
                      dim3(256), 0, bpk::as_stream(stream), weight, U, Cin, Cout,
-                     cout_padded(Cout));
+                     cout_padded(Cout), ft);
   BPK_LAUNCH_CHECK("conv3x3_wino_filter");
   return BPK_OK;
+}
+
+extern "C" int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout,
+                                           void* stream) {
+  return wino_filter(weight, U, Cin, Cout, 0, stream);
+}
+
+extern "C" int bpk_conv3x3_wino_filter_ft_f32(const float* weight, float* U, int Cin, int Cout,
+                                              void* stream) {
+  return wino_filter(weight, U, Cin, Cout, 1, stream);
 }
 
 extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W) {

@@ -47,20 +47,22 @@ def supported(x, weight):
     return small_supported(x, weight) or wino_supported(x, weight)
 
 
-def filter_transform(weight):
+def filter_transform(weight, ft=False):
     """U [Cin, CoutP, 16] (CoutP = Cout rounded up to 64), cached on `weight` while its
-    version counter is unchanged."""
-    cached = getattr(weight, "_bpk_wino_u", None)
+    version counter is unchanged.  ft=True: the transform of _flip_t(weight) (the filter of
+    the backward-data conv, Cin = weight.shape[0]), read from `weight` in place."""
+    attr = "_bpk_wino_u_ft" if ft else "_bpk_wino_u"
+    cached = getattr(weight, attr, None)
     if cached is not None and cached[0] == weight._version:
         return cached[1]
     w = weight.detach().contiguous()
-    Cout, Cin = w.shape[:2]
+    Cout, Cin = (w.shape[1], w.shape[0]) if ft else (w.shape[0], w.shape[1])
     # Cout % 64 != 0: U is laid out for Cout rounded up to 64 (zero couts, never stored)
     CoutP = lib.bpk_conv3x3_wino_filter_bytes(Cin, Cout) // (16 * 4 * Cin)
     U = torch.empty((Cin, CoutP, 16), dtype=torch.float32, device=w.device)
-    check(lib.bpk_conv3x3_wino_filter_f32(w.data_ptr(), U.data_ptr(), Cin, Cout,
-                                          stream_ptr(w.device)), "conv3x3 filter")
-    weight._bpk_wino_u = (weight._version, U)
+    fn = lib.bpk_conv3x3_wino_filter_ft_f32 if ft else lib.bpk_conv3x3_wino_filter_f32
+    check(fn(w.data_ptr(), U.data_ptr(), Cin, Cout, stream_ptr(w.device)), "conv3x3 filter")
+    setattr(weight, attr, (weight._version, U))
     return U
 
 
@@ -99,11 +101,13 @@ def ensure_gn_partials(t):
     return part, R, GN_PART_COUNT
 
 
-def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False, x2=None):
+def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False, x2=None,
+                    ft=False):
     """conv(a, weight) + bias, or with `skip`: (skip + (conv + bias)) / div (one launch),
     where a = x, or silu(x * s + t) with pre[n, c] = (s, t) (GroupNorm+SiLU fused in).
     stats=True also writes the GroupNorm partial statistics of the output (attached to it,
-    see gn_partials) so the next GroupNorm skips its statistics pass."""
+    see gn_partials) so the next GroupNorm skips its statistics pass.  ft=True: the filter
+    is _flip_t(weight) (backward-data), without materialising it."""
     x = x.contiguous()
     N, C1, H, W = x.shape
     C = C1 if x2 is None else C1 + x2.shape[1]
@@ -111,8 +115,8 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=Fa
         x2 = x2.contiguous()
         if x2.shape[0] != N or tuple(x2.shape[2:]) != (H, W) or C1 % 8:
             raise RuntimeError(f"conv3x3: second source {tuple(x2.shape)} vs {tuple(x.shape)}")
-    Cout = weight.shape[0]
-    U = filter_transform(weight)
+    Cout = weight.shape[1] if ft else weight.shape[0]
+    U = filter_transform(weight, ft)
     y = torch.empty((N, Cout, H, W), dtype=x.dtype, device=x.device)
     b = None if bias is None else bias.detach().contiguous()
     sk = None if skip is None else skip.detach().contiguous()
@@ -225,6 +229,55 @@ def _wgrad_impl(x, gy, wshape, want_b):
     return dw, (gy.detach().sum((0, 2, 3)) if want_b else None)
 
 
+def _fwd_ft_impl(x, w):
+    """conv3x3(x, _flip_t(w)) without autograd; the Winograd filter transform reads w
+    flipped and transposed in place when the shape qualifies."""
+    w = w.detach()
+    N, C, H, W = x.shape
+    if (C == w.shape[0] and x.is_cuda and x.dtype == torch.float32
+            and bool(lib.bpk_conv3x3_wino_supported(N, C, w.shape[1], H, W))):
+        return conv3x3_fwd_raw(x.detach(), w, ft=True)
+    return _fwd_impl(x, _flip_t(w))
+
+
+_FT = os.environ.get("BPK_CONV_FT", "1") != "0"  # 0: explicit flipped weight copies
+
+
+def _conv_ft_any(x, w):
+    """conv3x3(x, _flip_t(w)) -- the backward-data conv -- recorded for autograd when grad
+    mode is on, else the raw kernels."""
+    if not _FT:
+        return _conv_any(x, _flip_t(w))
+    if torch.is_grad_enabled():
+        return _Conv3x3FT.apply(x, w)
+    return _fwd_ft_impl(x, w)
+
+
+class _Conv3x3FT(torch.autograd.Function):
+    """y = conv3x3(x, _flip_t(w)) for w [Co, Ci, 3, 3] (x has Co channels).  Adjoint:
+    d/dx = conv3x3(gy, w) (flip_t is an involution); d/dw = _flip_t(wgrad(x, gy)).  Both
+    differentiable again (second derivatives of the PINN residual)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return _fwd_ft_impl(x, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = _conv_any(gy, w)
+        if ctx.needs_input_grad[1]:
+            fshape = (w.shape[1], w.shape[0], 3, 3)
+            if torch.is_grad_enabled():
+                gw = _flip_t(_Wgrad3x3.apply(x, gy, fshape))
+            else:
+                gw = _flip_t(_wgrad_impl(x, gy, fshape, False)[0])
+        return gx, gw
+
+
 def _conv_any(x, w):
     """conv3x3(x, w) recorded for autograd when grad mode is on (higher derivatives), else
     the raw kernels."""
@@ -257,7 +310,7 @@ class _Conv3x3(torch.autograd.Function):
             gs = gy
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[0]:
-            gx = _conv_any(gy, _flip_t(weight))
+            gx = _conv_ft_any(gy, weight)
         if torch.is_grad_enabled():
             if ctx.needs_input_grad[1]:
                 gw = _Wgrad3x3.apply(x, gy, tuple(weight.shape))
@@ -284,7 +337,7 @@ class _Wgrad3x3(torch.autograd.Function):
         x, gy = ctx.saved_tensors
         gx = ggy = None
         if ctx.needs_input_grad[0]:
-            gx = _conv_any(gy, _flip_t(ggw))
+            gx = _conv_ft_any(gy, ggw)
         if ctx.needs_input_grad[1]:
             ggy = _conv_any(x, ggw)
         return gx, ggy, None

@@ -317,6 +317,11 @@ int bpk_correlation_bwd_f32(const float* first, const float* second, const float
  * ------------------------------------------------------------------------- */
 int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout);
 int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout, void* stream);
+/* The same transform of flip_t(w) = w[ci][co][2 - r][2 - s] for w [Cin, Cout, 3, 3] (the
+ * weight of the conv whose backward-data this is: dx = conv(dy, flip_t(w)), the cuDNN
+ * backward-data of nn.Conv2d) -- read in place, no flipped copy of w. */
+int bpk_conv3x3_wino_filter_ft_f32(const float* weight, float* U, int Cin, int Cout,
+                                   void* stream);
 int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W);
 int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y, int N,
                          int Cin, int Cout, int H, int W, void* stream);

@@ -762,3 +762,18 @@ def test_conv3x3_winograd_padded_cout_fused_variants(hip, cin, cout):
     refs = second(lambda t, ww: F.conv2d(t, ww, b, padding=1))
     for a_, r_ in zip(got, refs):
         assert (a_ - r_).abs().max().item() <= 2e-5 * max(1e-6, r_.abs().max().item())
+
+
+@pytest.mark.parametrize("co,ci", [(64, 128), (128, 32), (32, 16), (16, 2)])
+def test_conv3x3_backward_data_flip_in_filter_transform(hip, co, ci):
+    """conv3x3(dy, flip_t(w)) with the flip / transpose read inside the Winograd filter
+    transform (no flipped copy of w; MIOpen / small kernel with an explicit flip where the
+    shape does not qualify) == F.conv2d with the flipped weight (2e-5 relative)."""
+    from op.conv import _flip_t, _fwd_ft_impl
+    g = torch.Generator().manual_seed(co + 7 * ci)
+    dy = torch.randn(2, co, 16, 32, generator=g).to(hip)
+    w = (torch.randn(co, ci, 3, 3, generator=g) / (3 * co ** 0.5)).to(hip)
+    with torch.no_grad():
+        got = _fwd_ft_impl(dy, w)
+        ref = F.conv2d(dy, _flip_t(w).contiguous(), padding=1)
+    assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
