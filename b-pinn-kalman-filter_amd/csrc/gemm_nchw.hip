@@ -73,8 +73,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
     const float* Xp = second ? X2 : X1;
     const int K = second ? g.K2 : g.K1;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      ra[i] = *reinterpret_cast<const f4*>(&Wp[(int64_t)(m0 + am + 64 * i) * g.ldw + k0 + ak]);
+    for (int i = 0; i < 2; ++i)  // rows past M (M % 128 != 0): zero
+      ra[i] = m0 + am + 64 * i < g.M
+                  ? *reinterpret_cast<const f4*>(&Wp[(int64_t)(m0 + am + 64 * i) * g.ldw + k0 + ak])
+                  : f4{0.f, 0.f, 0.f, 0.f};
     const float* xb = Xp + ((int64_t)n * K + k0) * g.P + p0 + bp;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int m = m0 + 64 * wm + 16 * i + 4 * kq + rr;
+      if (m >= g.M) continue;
       const float bb = bias ? bias[m] : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) yn[(int64_t)m * g.P + p0 + 64 * wp + 16 * j + jj] = acc[i][j][rr] + bb;
@@ -182,9 +185,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_wgrad_kernel(
     const float* gy = GY + ((int64_t)ln * g.M + m0 + lr) * g.P + lpc * kKC + lp;
     const float* xx = X + ((int64_t)ln * g.K + k0 + lr) * g.P + lpc * kKC + lp;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      ra[i] = *reinterpret_cast<const f4*>(gy + (int64_t)(64 * i) * g.P);
-      rb[i] = *reinterpret_cast<const f4*>(xx + (int64_t)(64 * i) * g.P);
+    for (int i = 0; i < 2; ++i) {  // rows past M / K: zero
+      ra[i] = m0 + lr + 64 * i < g.M ? *reinterpret_cast<const f4*>(gy + (int64_t)(64 * i) * g.P)
+                                     : f4{0.f, 0.f, 0.f, 0.f};
+      rb[i] = k0 + lr + 64 * i < g.K ? *reinterpret_cast<const f4*>(xx + (int64_t)(64 * i) * g.P)
+                                     : f4{0.f, 0.f, 0.f, 0.f};
     }
     if (--left > 0 && ++lpc == cpi) { lpc = 0; ++ln; }  // past the end: re-load the last chunk
   };
@@ -231,8 +236,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_wgrad_kernel(
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int m = m0 + 64 * wm + 16 * i + 4 * kq + rr;
+      if (m >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ps[(int64_t)m * g.K + k0 + 64 * wk + 16 * j + jj] = acc[i][j][rr];
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 64 * wk + 16 * j + jj;
+        if (k < g.K) ps[(int64_t)m * g.K + k] = acc[i][j][rr];
+      }
     }
   if (part_b != nullptr && tk == 0 && wk == 0) {  // bias: rows of this wave, summed over kq
 #pragma unroll
@@ -240,7 +249,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_wgrad_kernel(
       float v = bsum[i];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      if (kq == 0) part_b[(int64_t)s * g.M + m0 + 64 * wm + 16 * i + jj] = v;
+      if (kq == 0 && m0 + 64 * wm + 16 * i + jj < g.M)
+        part_b[(int64_t)s * g.M + m0 + 64 * wm + 16 * i + jj] = v;
     }
   }
 }
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_reduce_kernel(
 }
 
 WgGeo wgrad_geo(int N, int M, int K, int P) {
-  WgGeo g{N, M, K, P, M / kBM, K / kBM, 1, 0};
+  WgGeo g{N, M, K, P, (M + kBM - 1) / kBM, (K + kBM - 1) / kBM, 1, 0};
   const int64_t chunks = (int64_t)N * (P / kKC);
   const int tiles = g.tiles_m * g.tiles_k;
   // ~1024 workgroups (4 per CU), at least 64 chunks (1024 pixels) per split
@@ -282,7 +292,7 @@ WgGeo wgrad_geo(int N, int M, int K, int P) {
 }  // namespace
 
 extern "C" int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2) {
-  return N > 0 && M > 0 && P > 0 && K1 > 0 && K2 >= 0 && M % kBM == 0 && P % kBP == 0 &&
+  return N > 0 && M > 0 && P > 0 && K1 > 0 && K2 >= 0 && M % 16 == 0 && P % kBP == 0 &&
          K1 % kKC == 0 && K2 % kKC == 0;
 }
 
@@ -290,11 +300,11 @@ extern "C" int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K
                                  const float* X2, int K2, const float* bias, float* Y, int N,
                                  int M, int P, void* stream) {
   BPK_REQUIRE(bpk_gemm_nchw_supported(N, M, P, K1, K2),
-              "gemm_nchw: unsupported shape N=%d M=%d P=%d K1=%d K2=%d (need M %% 128, "
+              "gemm_nchw: unsupported shape N=%d M=%d P=%d K1=%d K2=%d (need M %% 16, "
               "P %% 128, K %% 16 == 0)", N, M, P, K1, K2);
   BPK_REQUIRE(ldw >= K1 + K2 && ldw % 4 == 0, "gemm_nchw: bad weight row stride %d", ldw);
   BPK_REQUIRE(K2 == 0 || X2 != nullptr, "gemm_nchw: K2 > 0 needs X2");
-  GemmGeo g{N, M, P, K1, K2, ldw, M / kBM, P / kBP};
+  GemmGeo g{N, M, P, K1, K2, ldw, (M + kBM - 1) / kBM, P / kBP};
   const int64_t blocks = (int64_t)N * g.tiles_m * g.tiles_p;
   BPK_REQUIRE(blocks < (1LL << 31), "gemm_nchw: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -306,7 +316,7 @@ extern "C" int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K
 }
 
 extern "C" int bpk_gemm_nchw_wgrad_supported(int N, int M, int K, int P) {
-  return N > 0 && M > 0 && K > 0 && P > 0 && M % kBM == 0 && K % kBM == 0 && P % kKC == 0 &&
+  return N > 0 && M > 0 && K > 0 && P > 0 && M % 16 == 0 && K % 16 == 0 && P % kKC == 0 &&
          (int64_t)N * (P / kKC) < (1LL << 31);
 }
 
@@ -321,7 +331,7 @@ extern "C" int bpk_gemm_nchw_wgrad_f32(const float* GY, const float* X, float* d
                                        void* workspace, int N, int M, int K, int P,
                                        void* stream) {
   BPK_REQUIRE(bpk_gemm_nchw_wgrad_supported(N, M, K, P),
-              "gemm_nchw_wgrad: unsupported shape N=%d M=%d K=%d P=%d (need M %% 128, K %% 128, "
+              "gemm_nchw_wgrad: unsupported shape N=%d M=%d K=%d P=%d (need M %% 16, K %% 16, "
               "P %% 16 == 0)", N, M, K, P);
   const WgGeo g = wgrad_geo(N, M, K, P);
   BPK_REQUIRE(g.splits == 1 || workspace != nullptr, "gemm_nchw_wgrad: workspace required");

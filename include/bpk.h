@@ -381,7 +381,8 @@ int bpk_conv3x3_small_f32(const float* x, const float* pre, const float* weight,
  *   Y[n] (M x P) = W[:, :K1] X1[n] (K1 x P) + W[:, K1:K1+K2] X2[n] (K2 x P) + bias[M]
  * W row-major [M, ldw], X1 [N, K1, P], X2 [N, K2, P] (NULL when K2 = 0), Y [N, M, P], P = H*W;
  * reading [X1, X2] this way replaces the channel concatenation torch.cat([X1, X2], 1).
- * supported(): M % 128 == 0, P % 128 == 0, K1 % 16 == 0, K2 % 16 == 0. */
+ * supported(): M % 16 == 0, P % 128 == 0, K1 % 16 == 0, K2 % 16 == 0 (M tiles of 128,
+ * rows past M masked). */
 int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2);
 int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K1, const float* X2, int K2,
                       const float* bias, float* Y, int N, int M, int P, void* stream);
@@ -393,7 +394,7 @@ int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K1, const fl
  *   dW (M x K) = sum_n GY[n] (M x P) X[n]^T (P x K),   db[m] = sum_{n,p} GY[n][m][p]
  * GY [N, M, P], X [N, K, P], dW row-major [M, K], db [M] or NULL.  Split-K over pixel
  * ranges with per-split partial slabs summed in a fixed order (deterministic); workspace of
- * workspace_bytes() (0: none needed).  supported(): M % 128, K % 128, P % 16 == 0. */
+ * workspace_bytes() (0: none needed).  supported(): M % 16, K % 16, P % 16 == 0. */
 int bpk_gemm_nchw_wgrad_supported(int N, int M, int K, int P);
 int64_t bpk_gemm_nchw_wgrad_workspace_bytes(int N, int M, int K, int P);
 int bpk_gemm_nchw_wgrad_f32(const float* GY, const float* X, float* dW, float* db,

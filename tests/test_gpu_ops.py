@@ -552,7 +552,8 @@ def test_conv3x3_double_backward_any_shape(hip, cin, cout, hw):
 
 
 @pytest.mark.parametrize("N,k1,k2,m,hw", [(2, 64, 0, 128, 16), (3, 128, 64, 256, 32),
-                                          (1, 256, 256, 128, 16), (2, 16, 48, 384, 32)])
+                                          (1, 256, 256, 128, 16), (2, 16, 48, 384, 32),
+                                          (2, 96, 0, 32, 16), (1, 64, 32, 80, 16)])
 def test_conv1x1_gemm_matches_fp32_reference(hip, N, k1, k2, m, hw):
     """MFMA 1x1-conv GEMM (one or two sources along K) vs float64 (1e-5 relative); the
     two-source form equals conv1x1 of the concatenation."""
@@ -570,7 +571,8 @@ def test_conv1x1_gemm_matches_fp32_reference(hip, N, k1, k2, m, hw):
 
 
 @pytest.mark.parametrize("N,k,m,hw", [(1, 128, 128, 4), (2, 128, 256, 16), (3, 384, 128, 20),
-                                     (8, 256, 256, 64)])
+                                     (8, 256, 256, 64), (2, 64, 16, 16), (3, 96, 192, 8),
+                                     (2, 448, 96, 32)])
 def test_conv1x1_wgrad_gemm_matches_fp64(hip, N, k, m, hw):
     """1x1 weight / bias gradient GEMM (split-K over pixels, one split and many) vs float64:
     dw = sum_n gy[n] x[n]^T, db = gy.sum((0, 2, 3)) (1e-5 relative); deterministic."""
@@ -587,7 +589,8 @@ def test_conv1x1_wgrad_gemm_matches_fp64(hip, N, k, m, hw):
     assert torch.equal(dw, dw2)
 
 
-@pytest.mark.parametrize("cin,cout,hw", [(128, 256, 16), (256, 128, 32), (384, 128, 16)])
+@pytest.mark.parametrize("cin,cout,hw", [(128, 256, 16), (256, 128, 32), (384, 128, 16),
+                                         (64, 16, 16), (96, 192, 16), (448, 96, 32)])
 def test_conv1x1_autograd_double_backward(hip, cin, cout, hw):
     """conv1x1_ad (GEMM kernels for the forward, its adjoint and the weight / bias gradient,
     each differentiable again) vs F.conv2d: forward, first and second derivatives w.r.t.
