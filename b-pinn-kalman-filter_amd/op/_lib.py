@@ -126,3 +126,40 @@ def require_hip(*tensors, what="bpk op"):
 
 def exported_symbols() -> list:
     return sorted(parse_header().keys())
+
+
+_PRUNE = os.environ.get("BPK_GRAD_PRUNE", "1") != "0"
+
+
+def mark_inputs(ctx, *args):
+    """Record, in a custom Function's forward, which arguments are tensors: the engine keeps
+    one next_functions edge per tensor argument only, so want_grad needs the mapping."""
+    if ctx is not None:
+        pos, k = [], 0
+        for a in args:
+            pos.append(k if isinstance(a, torch.Tensor) else None)
+            k += isinstance(a, torch.Tensor)
+        ctx._bpk_tpos = pos
+
+
+def want_grad(ctx, i: int) -> bool:
+    """ctx.needs_input_grad[i], and the autograd engine will use that gradient in the current
+    backward pass: torch.autograd.grad(out, inputs=x) -- the PINN residual's derivative
+    passes -- never runs the parameters' AccumulateGrad nodes, so the weight / bias gradients
+    of a custom Function need not be computed there (ctx.needs_input_grad is fixed at forward
+    time and would say yes).  Functions whose forward did not call mark_inputs: no pruning."""
+    if not ctx.needs_input_grad[i]:
+        return False
+    pos = getattr(ctx, "_bpk_tpos", None)
+    if not _PRUNE or pos is None or i >= len(pos) or pos[i] is None:
+        return True
+    nf = ctx.next_functions
+    if pos[i] >= len(nf):
+        return True
+    node = nf[pos[i]][0]
+    if node is None:
+        return True
+    try:
+        return bool(torch._C._will_engine_execute_node(node))
+    except RuntimeError:
+        return True

@@ -19,7 +19,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from ._lib import check, lib, require_hip, stream_ptr
+from ._lib import check, lib, require_hip, stream_ptr, mark_inputs, want_grad
 
 
 def _shape_ok(x, weight):
@@ -260,6 +260,7 @@ class _Conv3x3FT(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w):
+        mark_inputs(ctx, x, w)
         ctx.save_for_backward(x, w)
         return _fwd_ft_impl(x, w)
 
@@ -267,9 +268,9 @@ class _Conv3x3FT(torch.autograd.Function):
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gx = gw = None
-        if ctx.needs_input_grad[0]:
+        if want_grad(ctx, 0):
             gx = _conv_any(gy, w)
-        if ctx.needs_input_grad[1]:
+        if want_grad(ctx, 1):
             fshape = (w.shape[1], w.shape[0], 3, 3)
             if torch.is_grad_enabled():
                 gw = _flip_t(_Wgrad3x3.apply(x, gy, fshape))
@@ -295,6 +296,7 @@ class _Conv3x3(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, skip, div):
+        mark_inputs(ctx, x, weight, bias, skip, div)
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.div = float(div)
@@ -306,19 +308,19 @@ class _Conv3x3(torch.autograd.Function):
         gx = gw = gb = gs = None
         if ctx.div != 1.0:
             gy = gy / ctx.div
-        if ctx.needs_input_grad[3]:
+        if want_grad(ctx, 3):
             gs = gy
-        want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[0]:
+        want_b = ctx.has_bias and want_grad(ctx, 2)
+        if want_grad(ctx, 0):
             gx = _conv_ft_any(gy, weight)
         if torch.is_grad_enabled():
-            if ctx.needs_input_grad[1]:
+            if want_grad(ctx, 1):
                 gw = _Wgrad3x3.apply(x, gy, tuple(weight.shape))
             if want_b:
                 gb = gy.sum((0, 2, 3))
-        elif ctx.needs_input_grad[1] or want_b:
+        elif want_grad(ctx, 1) or want_b:
             dw, gb = _wgrad_impl(x, gy, tuple(weight.shape), want_b)
-            gw = dw if ctx.needs_input_grad[1] else None
+            gw = dw if want_grad(ctx, 1) else None
         return gx, gw, gb, gs, None
 
 
@@ -329,6 +331,7 @@ class _Wgrad3x3(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gy, wshape):
+        mark_inputs(ctx, x, gy, wshape)
         ctx.save_for_backward(x, gy)
         return _wgrad_impl(x, gy, wshape, False)[0]
 
@@ -336,9 +339,9 @@ class _Wgrad3x3(torch.autograd.Function):
     def backward(ctx, ggw):
         x, gy = ctx.saved_tensors
         gx = ggy = None
-        if ctx.needs_input_grad[0]:
+        if want_grad(ctx, 0):
             gx = _conv_ft_any(gy, ggw)
-        if ctx.needs_input_grad[1]:
+        if want_grad(ctx, 1):
             ggy = _conv_any(x, ggw)
         return gx, ggy, None
 
@@ -492,17 +495,18 @@ class _Conv1x1(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w2d, bias):
+        mark_inputs(ctx, x, w2d, bias)
         ctx.save_for_backward(x, w2d)
         return _gemm1x1_raw(x, w2d, bias)
 
     @staticmethod
     def backward(ctx, gy):
         x, w2d = ctx.saved_tensors
-        gx = _c1_fn(gy, w2d.t()) if ctx.needs_input_grad[0] else None
+        gx = _c1_fn(gy, w2d.t()) if want_grad(ctx, 0) else None
         gw = gb = None
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            gw, gb = _w1_fn(gy, x, bool(ctx.needs_input_grad[2]))
-            if not ctx.needs_input_grad[1]:
+        if want_grad(ctx, 1) or want_grad(ctx, 2):
+            gw, gb = _w1_fn(gy, x, bool(want_grad(ctx, 2)))
+            if not want_grad(ctx, 1):
                 gw = None
         return gx, gw, gb
 
@@ -512,6 +516,7 @@ class _Wgrad1x1(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, gy, x, bias_grad):
+        mark_inputs(ctx, gy, x, bias_grad)
         ctx.save_for_backward(gy, x)
         return _wgrad1x1_raw(gy, x, bias_grad)
 
@@ -519,12 +524,12 @@ class _Wgrad1x1(torch.autograd.Function):
     def backward(ctx, ggw, ggb):
         gy, x = ctx.saved_tensors
         g_gy = g_x = None
-        if ctx.needs_input_grad[0]:
+        if want_grad(ctx, 0):
             if ggw is not None:
                 g_gy = _c1_fn(x, ggw, ggb)  # ggw x[n] + ggb
             elif ggb is not None:
                 g_gy = ggb.view(1, -1, 1, 1).expand_as(gy)
-        if ctx.needs_input_grad[1] and ggw is not None:
+        if want_grad(ctx, 1) and ggw is not None:
             g_x = _c1_fn(gy, ggw.t())
         return g_gy, g_x, None
 
@@ -571,6 +576,7 @@ class _ConvG(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, cfg):
+        mark_inputs(ctx, x, w, cfg)
         if ctx is not None:
             ctx.save_for_backward(x, w)
             ctx.cfg = cfg
@@ -580,8 +586,8 @@ class _ConvG(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        gx = _convt_fn(gy, w, tuple(x.shape), ctx.cfg) if ctx.needs_input_grad[0] else None
-        gw = _wgrad_fn(x, gy, tuple(w.shape), ctx.cfg) if ctx.needs_input_grad[1] else None
+        gx = _convt_fn(gy, w, tuple(x.shape), ctx.cfg) if want_grad(ctx, 0) else None
+        gw = _wgrad_fn(x, gy, tuple(w.shape), ctx.cfg) if want_grad(ctx, 1) else None
         return gx, gw, None
 
 
@@ -590,6 +596,7 @@ class _ConvTG(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, u, w, xshape, cfg):
+        mark_inputs(ctx, u, w, xshape, cfg)
         if ctx is not None:
             ctx.save_for_backward(u, w)
             ctx.cfg = cfg
@@ -599,8 +606,8 @@ class _ConvTG(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gz):
         u, w = ctx.saved_tensors
-        gu = _conv_fn(gz, w, ctx.cfg) if ctx.needs_input_grad[0] else None
-        gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg) if ctx.needs_input_grad[1] else None
+        gu = _conv_fn(gz, w, ctx.cfg) if want_grad(ctx, 0) else None
+        gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg) if want_grad(ctx, 1) else None
         return gu, gw, None, None
 
 
@@ -609,6 +616,7 @@ class _WgradG(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gy, wshape, cfg):
+        mark_inputs(ctx, x, gy, wshape, cfg)
         if ctx is not None:
             ctx.save_for_backward(x, gy)
             ctx.cfg = cfg
@@ -618,8 +626,8 @@ class _WgradG(torch.autograd.Function):
     @staticmethod
     def backward(ctx, ggw):
         x, gy = ctx.saved_tensors
-        gx = _convt_fn(gy, ggw, tuple(x.shape), ctx.cfg) if ctx.needs_input_grad[0] else None
-        ggy = _conv_fn(x, ggw, ctx.cfg) if ctx.needs_input_grad[1] else None
+        gx = _convt_fn(gy, ggw, tuple(x.shape), ctx.cfg) if want_grad(ctx, 0) else None
+        ggy = _conv_fn(x, ggw, ctx.cfg) if want_grad(ctx, 1) else None
         return gx, ggy, None, None
 
 

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 from torch.autograd import Function
 
-from ._lib import check, lib, require_hip, stream_ptr
+from ._lib import check, lib, require_hip, stream_ptr, mark_inputs, want_grad
 
 ACT_NONE, ACT_SILU = 0, 1
 
@@ -25,6 +25,7 @@ def _ws(N, C, HW, G, device):
 class _GroupNormAct(Function):
     @staticmethod
     def forward(ctx, x, bias_nc, weight, bias, num_groups, eps, act):
+        mark_inputs(ctx, x, bias_nc, weight, bias)
         require_hip(x, what="group_norm_act")
         if x.dtype != torch.float32:
             raise RuntimeError(f"group_norm_act: float32 required, got {x.dtype}")
@@ -55,7 +56,7 @@ class _GroupNormAct(Function):
         HW = x.numel() // max(N * C, 1)
         G = ctx.num_groups
         dx = torch.empty_like(x)
-        need_affine = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        need_affine = weight is not None and (want_grad(ctx, 2) or want_grad(ctx, 3))
         dg = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
         db = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
         ws = _ws(N, C, HW, G, x.device)
@@ -66,9 +67,9 @@ class _GroupNormAct(Function):
             dx.data_ptr(), dg.data_ptr() if dg is not None else None,
             db.data_ptr() if db is not None else None, ws.data_ptr() if ws is not None else None,
             N, C, HW, G, ctx.act, stream_ptr(x.device)), "group_norm_act_bwd")
-        d_bnc = dx.reshape(N, C, -1).sum(-1) if (ctx.has_bnc and ctx.needs_input_grad[1]) else None
-        dw = dg.sum(0) if dg is not None and ctx.needs_input_grad[2] else None
-        dbeta = db.sum(0) if db is not None and ctx.needs_input_grad[3] else None
+        d_bnc = dx.reshape(N, C, -1).sum(-1) if (ctx.has_bnc and want_grad(ctx, 1)) else None
+        dw = dg.sum(0) if dg is not None and want_grad(ctx, 2) else None
+        dbeta = db.sum(0) if db is not None and want_grad(ctx, 3) else None
         return dx, d_bnc, dw, dbeta, None, None, None
 
 
@@ -140,6 +141,7 @@ def group_norm_affine(x, gn: torch.nn.GroupNorm, bias_nc=None):
 class _Residual(Function):
     @staticmethod
     def forward(ctx, x, h, bias, div):
+        mark_inputs(ctx, x, h, bias, div)
         require_hip(x, h, what="residual_rescale")
         x, h = x.contiguous(), h.contiguous()
         if x.shape != h.shape:
@@ -158,7 +160,7 @@ class _Residual(Function):
     @staticmethod
     def backward(ctx, g):
         gd = g / ctx.div
-        gb = gd.sum(dim=[0] + list(range(2, g.ndim))) if ctx.has_bias and ctx.needs_input_grad[2] \
+        gb = gd.sum(dim=[0] + list(range(2, g.ndim))) if ctx.has_bias and want_grad(ctx, 2) \
             else None
         return gd, gd, gb, None
 
