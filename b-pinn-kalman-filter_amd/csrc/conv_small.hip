@@ -10,7 +10,7 @@
 // byte time.)
 //
 //   * small_cout_kernel<COUT>: a workgroup owns a 16 x 64 output tile of one image; the
-//     18 x 66 input patch of 4 channels at a time is staged in LDS (GroupNorm affine + SiLU
+//     18 x 66 input patch of 8 channels at a time is staged in LDS (the next 8 prefetched into registers meanwhile) (GroupNorm affine + SiLU
 //     applied on the way in when `pre` is given; the zero padding stays zero), every thread
 //     accumulates a 1 x 4 pixel strip for all COUT outputs from a 3 x 6 register window;
 //     weights are workgroup-uniform (scalar loads).
@@ -28,7 +28,6 @@ namespace {
 constexpr int kTH = 16, kTW = 64;         // output tile
 constexpr int kPH = kTH + 2, kPW = kTW + 2;  // 18 x 66 input patch
 constexpr int kPWp = kPW + 1;             // padded LDS row
-constexpr int kCK = 4;                    // input channels per LDS chunk (small-Cout form)
 
 using f4 = __attribute__((ext_vector_type(4))) float;
 
@@ -62,13 +61,19 @@ __device__ inline void stage_patch(float* s, const float* __restrict__ xn,
   }
 }
 
+// small-Cout form: channels staged kCC at a time; each thread owns fixed patch positions
+// (their global / LDS offsets computed once), the next chunk's values are loaded into
+// registers while the current chunk is computed (one load latency per chunk hidden)
+constexpr int kCC = 8;                                 // channels per chunk
+constexpr int kPP = (kPH * kPW + 255) / 256;           // patch positions per thread (5)
+
 template <int COUT, bool PRE>
 __global__ __launch_bounds__(256) void small_cout_kernel(const float* __restrict__ x,
                                                          const float2* __restrict__ pre,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ y, SmallGeo g) {
-  __shared__ float s_patch[kCK * kPH * kPWp];  // 19.3 KB
+  __shared__ float s_patch[kCC * kPH * kPWp];  // 38.6 KB
   const int tile = blockIdx.x;
   const int tx = tile % g.tiles_x;
   const int ty = (tile / g.tiles_x) % g.tiles_y;
@@ -79,17 +84,55 @@ __global__ __launch_bounds__(256) void small_cout_kernel(const float* __restrict
   const float* xn = x + (int64_t)n * g.Cin * plane;
   const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
 
+  // this thread's patch positions: global offset within a plane (-1: padding / unused) and
+  // LDS offset within a channel slab
+  int goff[kPP], loff[kPP];
+#pragma unroll
+  for (int k = 0; k < kPP; ++k) {
+    const int p = threadIdx.x + 256 * k;
+    const int py = p / kPW, px = p - (p / kPW) * kPW;
+    const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+    const bool in = p < kPH * kPW && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+    goff[k] = in ? iy * g.W + ix : -1;
+    loff[k] = p < kPH * kPW ? py * kPWp + px : -1;
+  }
+  float pf[kCC][kPP];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int c = 0; c < kCC; ++c)
+#pragma unroll
+      for (int k = 0; k < kPP; ++k)
+        pf[c][k] = (goff[k] >= 0 && c0 + c < g.Cin) ? xn[(int64_t)(c0 + c) * plane + goff[k]]
+                                                    : 0.f;
+  };
+  auto store = [&](int c0) {
+#pragma unroll
+    for (int c = 0; c < kCC; ++c) {
+      float2 st = make_float2(1.f, 0.f);
+      if (PRE && c0 + c < g.Cin) st = pre_n[c0 + c];
+#pragma unroll
+      for (int k = 0; k < kPP; ++k) {
+        if (loff[k] < 0) continue;
+        float v = pf[c][k];
+        if (PRE && goff[k] >= 0) v = silu_f(v * st.x + st.y);  // padding stays zero
+        s_patch[c * kPH * kPWp + loff[k]] = v;
+      }
+    }
+  };
+
   float acc[COUT][4];
 #pragma unroll
   for (int co = 0; co < COUT; ++co)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[co][j] = 0.f;
 
-  for (int c0 = 0; c0 < g.Cin; c0 += kCK) {
-    const int nc = min(kCK, g.Cin - c0);
+  load(0);
+  for (int c0 = 0; c0 < g.Cin; c0 += kCC) {
+    const int nc = min(kCC, g.Cin - c0);
     __syncthreads();
-    stage_patch<PRE>(s_patch, xn, pre_n, c0, nc, oy0, ox0, g);
+    store(c0);
     __syncthreads();
+    if (c0 + kCC < g.Cin) load(c0 + kCC);
     for (int c = 0; c < nc; ++c) {
       float win[3][6];
 #pragma unroll
