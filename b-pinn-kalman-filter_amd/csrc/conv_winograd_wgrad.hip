@@ -465,43 +465,56 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
 }
 
 // dw[cout][cin] = G^T (sum_s part[s][cin][cout]) G,  G^T = [[1,.5,.5,0],[0,.5,-.5,0],[0,.5,.5,1]]
+// Block = 16 (cin, cout) pairs x 4 float4 columns of their 16 partial values x 4 groups of
+// splits (group g sums splits g, g + 4, ...; the groups combine in a fixed order in LDS):
+// deterministic, and 16x the parallelism of one thread per pair (the PINN shapes have few
+// pairs and hundreds of splits).
 __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __restrict__ part,
                                                                 float* __restrict__ dw,
                                                                 const float* __restrict__ part_b,
                                                                 float* __restrict__ db, int Cin,
                                                                 int Cout, int splits) {
+  __shared__ f4 red[4][64];
   const int64_t pairs = (int64_t)Cin * Cout;
-  if (db) {  // db[cout] = sum over splits, fixed order
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < Cout;
-         i += (int64_t)gridDim.x * blockDim.x) {
+  if (db && blockIdx.x == 0) {  // db[cout] = sum over splits, fixed order
+    for (int i = threadIdx.x; i < Cout; i += blockDim.x) {
       float acc = 0.f;
       for (int sp = 0; sp < splits; ++sp) acc += part_b[(int64_t)sp * Cout + i];
       db[i] = acc;
     }
   }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pairs;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    f4 u[4] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f},
-               f4{0.f, 0.f, 0.f, 0.f}};
-    for (int s = 0; s < splits; ++s) {
-      const f4* src = reinterpret_cast<const f4*>(part + ((int64_t)s * pairs + i) * 16);
+  const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 16 + (col >> 2);  // pair
+  const int q = col & 3;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  if (i < pairs)
+    for (int s = grp; s < splits; s += 4)
+      acc += *reinterpret_cast<const f4*>(part + ((int64_t)s * pairs + i) * 16 + 4 * q);
+  red[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0) red[0][col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int64_t pi = (int64_t)blockIdx.x * 16 + threadIdx.x;
+    if (pi < pairs) {
+      f4 u[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) u[q] += src[q];
-    }
-    float t[3][4];  // G^T dU (rows of dU = u[row])
+      for (int r = 0; r < 4; ++r) u[r] = red[0][4 * threadIdx.x + r];
+      float t[3][4];  // G^T dU (rows of dU = u[row])
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      t[0][j] = u[0][j] + 0.5f * (u[1][j] + u[2][j]);
-      t[1][j] = 0.5f * (u[1][j] - u[2][j]);
-      t[2][j] = 0.5f * (u[1][j] + u[2][j]) + u[3][j];
-    }
-    const int ci = (int)(i / Cout), co = (int)(i % Cout);
-    float* o = dw + ((int64_t)co * Cin + ci) * 9;
+      for (int j = 0; j < 4; ++j) {
+        t[0][j] = u[0][j] + 0.5f * (u[1][j] + u[2][j]);
+        t[1][j] = 0.5f * (u[1][j] - u[2][j]);
+        t[2][j] = 0.5f * (u[1][j] + u[2][j]) + u[3][j];
+      }
+      const int ci = (int)(pi / Cout), co = (int)(pi % Cout);
+      float* o = dw + ((int64_t)co * Cin + ci) * 9;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      o[3 * r + 0] = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
-      o[3 * r + 1] = 0.5f * (t[r][1] - t[r][2]);
-      o[3 * r + 2] = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
+      for (int r = 0; r < 3; ++r) {
+        o[3 * r + 0] = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
+        o[3 * r + 1] = 0.5f * (t[r][1] - t[r][2]);
+        o[3 * r + 2] = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
+      }
     }
   }
 }
@@ -570,8 +583,8 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
                        workspace, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
-  hipLaunchKernelGGL(wino_wgrad_reduce_kernel,
-                     dim3((unsigned)std::min<int64_t>(bpk::ceil_div(pairs, 256), 4096)),
+  BPK_REQUIRE(bpk::ceil_div(pairs, 16) < (1LL << 31), "conv3x3_wino_wgrad: too many pairs");
+  hipLaunchKernelGGL(wino_wgrad_reduce_kernel, dim3((unsigned)bpk::ceil_div(pairs, 16)),
                      dim3(256), 0, st, workspace, dw, part_b, db, Cin, Cout, g.splits);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad_reduce");
   return BPK_OK;
