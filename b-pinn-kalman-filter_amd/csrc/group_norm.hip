@@ -418,16 +418,28 @@ __global__ __launch_bounds__(256) void gn_bwd_partial2(
     const float be = beta ? beta[c] : 0.f;
     const int64_t base = ((int64_t)n * C + c) * HW;
     float pg = 0.f, pb = 0.f;
-    for (int e = blk.h0 + threadIdx.x * W; e < blk.h1; e += 256 * W) {
-      float xv[W], gv[W];
-      Vec<W>::load(x + base + e, xv);
-      Vec<W>::load(dy + base + e, gv);
+    // two strides per iteration, loads first; same accumulation order as one stride at a
+    // time (bit-identical partials)
+    for (int e = blk.h0 + threadIdx.x * W; e < blk.h1; e += 2 * 256 * W) {
+      const int e2 = e + 256 * W;
+      const bool two = e2 < blk.h1;
+      float xv[2][W], gv[2][W];
+      Vec<W>::load(x + base + e, xv[0]);
+      Vec<W>::load(dy + base + e, gv[0]);
+      if (two) {
+        Vec<W>::load(x + base + e2, xv[1]);
+        Vec<W>::load(dy + base + e2, gv[1]);
+      }
 #pragma unroll
-      for (int q = 0; q < W; ++q) {
-        const float xhat = (xv[q] + b - mean) * rstd;
-        const float dz = gv[q] * act_bwd(xhat * ga + be, act);
-        pg += dz * xhat;
-        pb += dz;
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+          const float xhat = (xv[u][q] + b - mean) * rstd;
+          const float dz = gv[u][q] * act_bwd(xhat * ga + be, act);
+          pg += dz * xhat;
+          pb += dz;
+        }
       }
     }
     la += pb * ga;
@@ -475,17 +487,29 @@ __global__ __launch_bounds__(256) void gn_bwd_apply2(
     const float ga = gamma ? gamma[c] : 1.f;
     const float be = beta ? beta[c] : 0.f;
     const int64_t base = ((int64_t)n * C + c) * HW;
-    for (int e = blk.h0 + threadIdx.x * W; e < blk.h1; e += 256 * W) {
-      float xv[W], gv[W], o[W];
-      Vec<W>::load(x + base + e, xv);
-      Vec<W>::load(dy + base + e, gv);
-#pragma unroll
-      for (int q = 0; q < W; ++q) {
-        const float xhat = (xv[q] + b - mean) * rstd;
-        const float dxhat = gv[q] * act_bwd(xhat * ga + be, act) * ga;
-        o[q] = rstd * (dxhat - A - xhat * B);
+    // two strides per iteration, all four loads issued before any use (more bytes in
+    // flight per thread: the pass is HBM-bound)
+    for (int e = blk.h0 + threadIdx.x * W; e < blk.h1; e += 2 * 256 * W) {
+      const int e2 = e + 256 * W;
+      const bool two = e2 < blk.h1;
+      float xv[2][W], gv[2][W], o[W];
+      Vec<W>::load(x + base + e, xv[0]);
+      Vec<W>::load(dy + base + e, gv[0]);
+      if (two) {
+        Vec<W>::load(x + base + e2, xv[1]);
+        Vec<W>::load(dy + base + e2, gv[1]);
       }
-      Vec<W>::store(dx + base + e, o);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+          const float xhat = (xv[u][q] + b - mean) * rstd;
+          const float dxhat = gv[u][q] * act_bwd(xhat * ga + be, act) * ga;
+          o[q] = rstd * (dxhat - A - xhat * B);
+        }
+        Vec<W>::store(dx + base + (u ? e2 : e), o);
+      }
     }
     if (blk.s == 0 && threadIdx.x == 0 && (dgamma_nc || dbeta_nc)) {
       float pg = 0.f, pb = 0.f;
