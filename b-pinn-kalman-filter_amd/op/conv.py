@@ -145,12 +145,14 @@ _WGRAD_PIPE = os.environ.get("BPK_WGRAD_PIPE", "1") != "0"  # the kernel with th
 
 
 def wgrad_supported(x, weight):
+    """weight: the weight tensor or just its shape"""
     if not _WGRAD:
         return False
     if x.dtype != torch.float32 or x.dim() != 4 or not x.is_cuda:
         return False
     N, C, H, W = x.shape
-    return bool(lib.bpk_conv3x3_wino_wgrad_supported(N, C, weight.shape[0], H, W))
+    cout = weight[0] if isinstance(weight, (tuple, list, torch.Size)) else weight.shape[0]
+    return bool(lib.bpk_conv3x3_wino_wgrad_supported(N, C, cout, H, W))
 
 
 def conv3x3_wgrad_raw(x, gy, wshape, bias_grad=False):
@@ -218,7 +220,7 @@ def _fwd_impl(x, w, bias=None, skip=None, div=1.0):
 def _wgrad_impl(x, gy, wshape, want_b):
     """(dw, db or None) without autograd: the Winograd weight gradient (+ bias) when the
     shape qualifies, MIOpen backward-weights otherwise."""
-    if wgrad_supported(x, gy.new_empty(wshape)):
+    if wgrad_supported(x, tuple(wshape)):
         if _WGRAD_PIPE:
             dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
             return dw, (db if want_b else None)
