@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--cifar-steps", type=int, default=6,
                     help="configs[1] train steps (NCSN++ CIFAR-10 32x32x3, batch 128/GPU); 0: skip")
-    ap.add_argument("--pinn-steps", type=int, default=5)
+    ap.add_argument("--pinn-steps", type=int, default=10)
     ap.add_argument("--pinn-warmup", type=int, default=2)
     ap.add_argument("--pinn-graph", action="store_true",
                     help="replay the PINN forward/backward from a hipGraph (measured slower than "
