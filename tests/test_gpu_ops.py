@@ -780,3 +780,32 @@ def test_conv3x3_backward_data_flip_in_filter_transform(hip, co, ci):
         got = _fwd_ft_impl(dy, w)
         ref = F.conv2d(dy, _flip_t(w).contiguous(), padding=1)
     assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+
+
+def test_grad_pruning_input_derivatives_then_parameter_gradients(hip):
+    """The PINN pattern: d out / d x with create_graph (the engine runs no parameter edge, so
+    the custom Functions skip weight / bias gradients), then a loss of that derivative
+    backpropagated to the parameters.  Input derivative and parameter gradients vs the same
+    network on F.conv2d (2e-5 relative)."""
+    from op.conv import conv3x3, conv1x1_ad
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.randn(2, 16, 16, 32, generator=g)
+    w1 = torch.randn(32, 16, 3, 3, generator=g) * 0.1
+    b1 = torch.randn(32, generator=g) * 0.1
+    w2 = torch.randn(128, 32, 1, 1, generator=g) * 0.1
+    w3 = torch.randn(16, 128, 3, 3, generator=g) * 0.05
+
+    def run(c3, c1):
+        ps = [t.to(hip).requires_grad_() for t in (w1, b1, w2, w3)]
+        x = x0.to(hip).requires_grad_()
+        h = torch.tanh(c3(x, ps[0], ps[1]))
+        h = torch.tanh(c1(h, ps[2]))
+        y = c3(h, ps[3], None)
+        (dx,) = torch.autograd.grad(y.sum(), x, create_graph=True)
+        (dx * dx).sum().backward()
+        return [dx.detach()] + [p.grad for p in ps]
+
+    got = run(lambda t, w, b: conv3x3(t, w, b), lambda t, w: conv1x1_ad(t, w))
+    ref = run(lambda t, w, b: F.conv2d(t, w, b, padding=1), lambda t, w: F.conv2d(t, w))
+    for a, r in zip(got, ref):
+        assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
