@@ -220,15 +220,15 @@ int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w
 // HBM-bound stencil needs on MI355X.  All tap bookkeeping is compile-time: input row t of
 // the strip feeds output row r through vertical tap i = t*UP - r*DOWN, and output column oc
 // of a lane reads relative input column q = (oc*DOWN + j - P0) / UP.
-template <int UP, int DOWN, int P0, int R, int SEGW>
+template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD = 1>
 __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict__ x,
                                                          const float* __restrict__ kern,
                                                          float* __restrict__ out, int in_h,
                                                          int in_w, int kh, int kw, int out_h,
                                                          int out_w, int strips_x, int strips_y,
                                                          int64_t n_strips) {
-  constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;  // output columns per lane
-  constexpr int LV = NOC * DOWN / UP;                   // input columns loaded per lane
+  constexpr int NOC = (UP == 1 && DOWN == 2) ? NOCD : 2;  // output columns per lane
+  constexpr int LV = NOC * DOWN / UP;                      // input columns loaded per lane
   constexpr int NIR = ((R - 1) * DOWN + 3) / UP + 1;    // input rows feeding R output rows
   constexpr int SEGS = 64 / SEGW;
   const int lane = threadIdx.x & 63;
@@ -265,7 +265,18 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
     const bool row_ok = active && iy >= 0 && iy < in_h;
     const float* row = xp + (int64_t)iy * in_w;
     float own[LV], left[LV], right[LV];
-    if constexpr (LV == 2) {
+    if constexpr (LV == 4) {  // 16-byte row loads (in_w % 4 == 0, 16-byte aligned x)
+      if (row_ok && mycol + 3 < in_w) {
+        const float4 v = *reinterpret_cast<const float4*>(row + mycol);
+        own[0] = v.x;
+        own[1] = v.y;
+        own[2] = v.z;
+        own[3] = v.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) own[c] = (row_ok && mycol + c < in_w) ? row[mycol + c] : 0.f;
+      }
+    } else if constexpr (LV == 2) {
       if (row_ok && mycol + 1 < in_w) {
         const float2 v = *reinterpret_cast<const float2*>(row + mycol);
         own[0] = v.x;
@@ -338,35 +349,35 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
   }
 }
 
-template <int UP, int DOWN, int P0, int R, int SEGW>
+template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD>
 int launch_stream_seg(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                       int kh, int kw, int out_h, int out_w, hipStream_t st) {
-  constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;
+  constexpr int NOC = (UP == 1 && DOWN == 2) ? NOCD : 2;
   const int strips_x = (int)bpk::ceil_div(out_w, SEGW * NOC);
   const int strips_y = (int)bpk::ceil_div(out_h, R);
   const int64_t n = (int64_t)major * strips_x * strips_y;
   if (n <= 0) return BPK_OK;
   const int64_t blocks = bpk::ceil_div(n, 4 * (64 / SEGW));
   BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
-  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R, SEGW>), dim3((unsigned)blocks), dim3(256),
+  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R, SEGW, NOCD>), dim3((unsigned)blocks), dim3(256),
                      0, st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, strips_x, strips_y, n);
   BPK_LAUNCH_CHECK("upfirdn2d_stream");
   return BPK_OK;
 }
 
 // segment width = lanes needed for one output row of the plane (power of two, 8..64)
-template <int UP, int DOWN, int P0, int R>
+template <int UP, int DOWN, int P0, int R, int NOCD = 1>
 int launch_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                   int kh, int kw, int out_h, int out_w, hipStream_t st) {
-  constexpr int NOC = (UP == 1 && DOWN == 2) ? 1 : 2;
+  constexpr int NOC = (UP == 1 && DOWN == 2) ? NOCD : 2;
   const int lanes = (int)bpk::ceil_div(out_w, NOC);
   if (lanes <= 8)
-    return launch_stream_seg<UP, DOWN, P0, R, 8>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+    return launch_stream_seg<UP, DOWN, P0, R, 8, NOCD>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
   if (lanes <= 16)
-    return launch_stream_seg<UP, DOWN, P0, R, 16>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+    return launch_stream_seg<UP, DOWN, P0, R, 16, NOCD>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
   if (lanes <= 32)
-    return launch_stream_seg<UP, DOWN, P0, R, 32>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
-  return launch_stream_seg<UP, DOWN, P0, R, 64>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+    return launch_stream_seg<UP, DOWN, P0, R, 32, NOCD>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
+  return launch_stream_seg<UP, DOWN, P0, R, 64, NOCD>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
 }
 
 // returns true (and sets *rc) when a streaming specialisation applies
@@ -383,6 +394,13 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
   // strip heights measured on MI355X (tools/ab_upfirdn.sh): R = 4 (down2), 16 (up2), 8 (1x1)
   if (in_w % 2 != 0) return false;  // 8-byte row loads need an even row pitch
   if (up == 1 && down == 2) {
+    // two output columns per lane (16-byte input loads) where rows allow it; BPK_UPFIRDN_NOC1=1
+    // keeps one column per lane (8-byte loads) everywhere
+    static const bool noc1 = getenv("BPK_UPFIRDN_NOC1") != nullptr;
+    if (!noc1 && in_w % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+      if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
+      if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
+    }
     if (p0 == 1) return BPK_STREAM(1, 2, 1, 4);
     if (p0 == 2) return BPK_STREAM(1, 2, 2, 4);
   }
