@@ -126,3 +126,38 @@ def test_dist_context_gloo_world2():
     assert res[0][1:3] == (0, 4) and res[1][1:3] == (4, 4)
     assert res[0][3] == [3.0, 30.0] == res[1][3]
     assert res[0][4] == [0.0] * 4 + [1.0] * 4
+
+
+def test_want_grad_prunes_parameter_edges_of_input_derivatives():
+    """op._lib.want_grad: inside a custom Function's backward, a parameter's gradient is
+    wanted for loss.backward() but not for torch.autograd.grad(out, inputs=x); tensor
+    positions are mapped past None / non-tensor arguments (mark_inputs)."""
+    import torch
+    from op._lib import mark_inputs, want_grad
+    seen = []
+
+    class Fn(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, bias, w, scale):
+            mark_inputs(ctx, x, bias, w, scale)
+            ctx.save_for_backward(x, w)
+            ctx.scale = scale
+            return x * w * scale
+
+        @staticmethod
+        def backward(ctx, g):
+            x, w = ctx.saved_tensors
+            seen.append((want_grad(ctx, 0), want_grad(ctx, 1), want_grad(ctx, 2)))
+            gx = g * w * ctx.scale if want_grad(ctx, 0) else None
+            gw = (g * x).sum(0) * ctx.scale if want_grad(ctx, 2) else None
+            return gx, None, gw, None
+
+    x = torch.randn(4, 3, requires_grad=True)
+    w = torch.randn(3, requires_grad=True)
+    y = Fn.apply(x * 1.0, None, w, 2.0).sum()
+    (gx,) = torch.autograd.grad(y, x, create_graph=True)
+    assert seen[-1] == (True, False, False)
+    assert torch.allclose(gx, 2.0 * w.expand(4, 3))
+    Fn.apply(x * 1.0, None, w, 2.0).sum().backward()
+    assert seen[-1] == (True, False, True)
+    assert torch.allclose(w.grad, 2.0 * x.detach().sum(0))
