@@ -397,7 +397,15 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
     // two output columns per lane (16-byte input loads) where rows allow it; BPK_UPFIRDN_NOC1=1
     // keeps one column per lane (8-byte loads) everywhere
     static const bool noc1 = getenv("BPK_UPFIRDN_NOC1") != nullptr;
+    static const int r2 = [] {
+      const char* e = getenv("BPK_UPFIRDN_R2");
+      return e ? atoi(e) : 4;
+    }();
     if (!noc1 && in_w % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+      if (r2 == 8) {
+        if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 8, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
+        if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 8, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
+      }
       if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
       if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
     }
