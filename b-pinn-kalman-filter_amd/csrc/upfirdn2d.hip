@@ -220,14 +220,15 @@ int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w
 // HBM-bound stencil needs on MI355X.  All tap bookkeeping is compile-time: input row t of
 // the strip feeds output row r through vertical tap i = t*UP - r*DOWN, and output column oc
 // of a lane reads relative input column q = (oc*DOWN + j - P0) / UP.
-template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD = 1>
+template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD = 0>
 __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict__ x,
                                                          const float* __restrict__ kern,
                                                          float* __restrict__ out, int in_h,
                                                          int in_w, int kh, int kw, int out_h,
                                                          int out_w, int strips_x, int strips_y,
                                                          int64_t n_strips) {
-  constexpr int NOC = (UP == 1 && DOWN == 2) ? NOCD : 2;  // output columns per lane
+  // output columns per lane: NOCD, or the default 1 (down2) / 2
+  constexpr int NOC = NOCD > 0 ? NOCD : ((UP == 1 && DOWN == 2) ? 1 : 2);
   constexpr int LV = NOC * DOWN / UP;                      // input columns loaded per lane
   constexpr int NIR = ((R - 1) * DOWN + 3) / UP + 1;    // input rows feeding R output rows
   constexpr int SEGS = 64 / SEGW;
@@ -334,7 +335,16 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
     const int oy = oyb + r;
     float* orow = op + (int64_t)oy * out_w;
     if (oy < out_h) {
-      if constexpr (NOC == 2) {
+      if constexpr (NOC == 4) {  // out_w % 4 == 0 (host check): 16-byte aligned quads
+        if (oxl + 3 < out_w) {
+          *reinterpret_cast<float4*>(orow + oxl) =
+              make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        } else {
+#pragma unroll
+          for (int oc = 0; oc < 4; ++oc)
+            if (oxl + oc < out_w) orow[oxl + oc] = acc[r][oc];
+        }
+      } else if constexpr (NOC == 2) {
         // 8-byte store when the pair is aligned (odd out_w makes every other row odd)
         if (oxl + 1 < out_w && (((int64_t)oy * out_w + oxl) & 1) == 0 && (out_h * out_w) % 2 == 0) {
           *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[r][0], acc[r][1]);
@@ -352,7 +362,7 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
 template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD>
 int launch_stream_seg(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                       int kh, int kw, int out_h, int out_w, hipStream_t st) {
-  constexpr int NOC = (UP == 1 && DOWN == 2) ? NOCD : 2;
+  constexpr int NOC = NOCD > 0 ? NOCD : ((UP == 1 && DOWN == 2) ? 1 : 2);
   const int strips_x = (int)bpk::ceil_div(out_w, SEGW * NOC);
   const int strips_y = (int)bpk::ceil_div(out_h, R);
   const int64_t n = (int64_t)major * strips_x * strips_y;
@@ -366,10 +376,10 @@ int launch_stream_seg(const float* x, const float* k, float* out, int major, int
 }
 
 // segment width = lanes needed for one output row of the plane (power of two, 8..64)
-template <int UP, int DOWN, int P0, int R, int NOCD = 1>
+template <int UP, int DOWN, int P0, int R, int NOCD = 0>
 int launch_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                   int kh, int kw, int out_h, int out_w, hipStream_t st) {
-  constexpr int NOC = (UP == 1 && DOWN == 2) ? NOCD : 2;
+  constexpr int NOC = NOCD > 0 ? NOCD : ((UP == 1 && DOWN == 2) ? 1 : 2);
   const int lanes = (int)bpk::ceil_div(out_w, NOC);
   if (lanes <= 8)
     return launch_stream_seg<UP, DOWN, P0, R, 8, NOCD>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
@@ -416,7 +426,14 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
     if (p0 == 1) return BPK_STREAM(1, 1, 1, 8);
     if (p0 == 2) return BPK_STREAM(1, 1, 2, 8);
   }
-  if (up == 2 && down == 1 && p0 == 2) return BPK_STREAM(2, 1, 2, 16);
+  if (up == 2 && down == 1 && p0 == 2) {
+    // four output columns per lane (8-byte input loads, 16-byte stores) when rows allow it;
+    // BPK_UPFIRDN_UP2=1 keeps two
+    static const bool up2 = getenv("BPK_UPFIRDN_UP2") != nullptr;
+    if (!up2 && out_w % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0)
+      return (*rc = launch_stream<2, 1, 2, 16, 4>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
+    return BPK_STREAM(2, 1, 2, 16);
+  }
 #undef BPK_STREAM
   return false;
 }
