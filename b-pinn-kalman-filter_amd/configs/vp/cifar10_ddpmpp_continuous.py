@@ -9,7 +9,7 @@ def get_config():
     c.sampling.update(method="pc", predictor="euler_maruyama", corrector="none")
     c.data.centered = True
     c.model.update(name="ddpm", scale_by_sigma=False, ema_rate=0.9999, normalization="GroupNorm",
-                   nonlinearity="swish", nf=128, ch_mult=(1, 2, 2, 2), num_res_blocks=2,
+                   nonlinearity="swish", nf=128, ch_mult=(1, 2, 2, 2), num_res_blocks=4,
                    attn_resolutions=(16,), resamp_with_conv=True, conditional=True, fir=False,
                    fir_kernel=[1, 3, 3, 1], skip_rescale=True, resblock_type="biggan",
                    progressive="none", progressive_input="none", progressive_combine="sum",

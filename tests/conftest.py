@@ -65,3 +65,116 @@ def hip():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+# ---------------------------------------------------------------------------------------
+# Shared by the fixture generators (tests/golden/make_golden_*.py) and the tests: seeded
+# weights and inputs that both sides rebuild, so fixtures store outputs, not 60M weights.
+
+def seeded_fill_(model, seed):
+    """Overwrite every parameter of `model` with a numpy-seeded normal draw (independent of
+    construction order and of torch's RNG): a per-tensor PCG64 stream keyed by (seed,
+    crc32(name)); >= 2-D tensors scaled 1/sqrt(prod(shape[1:])), 1-D `*weight` (norm
+    scales) 1 + 0.1 n, other 1-D tensors (biases, Fourier features) 0.05 n."""
+    import zlib
+
+    import torch
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            rng = np.random.default_rng([seed, zlib.crc32(name.encode())])
+            v = rng.standard_normal(tuple(p.shape))
+            if p.dim() >= 2:
+                v = v / np.sqrt(float(np.prod(p.shape[1:])))
+            elif name.endswith("weight"):
+                v = 1.0 + 0.1 * v
+            else:
+                v = 0.05 * v
+            p.copy_(torch.from_numpy(v.astype(np.float32)))
+    return model
+
+
+def sample_idx(n, k=256):
+    """Deterministic subset of flat indices stored for large step-fixture tensors."""
+    return np.unique(np.linspace(0, n - 1, min(n, k)).astype(np.int64))
+
+
+def sub(v, k=256):
+    v = np.asarray(v).reshape(-1)
+    return v[sample_idx(v.size, k)]
+
+
+def small_config(get_config):
+    """PINN fixture config of pinn_fwd / pinn_step / prelim_step: image 16, feature_nums
+    [4, 8, 8], B = 2."""
+    import torch
+    c = get_config()
+    c.data.image_size = 16
+    c.model.feature_nums = [4, 8, 8]
+    c.training.batch_size = 2
+    c.device = torch.device("cpu")
+    return c
+
+
+def full_pinn_config(get_config, batch=2):
+    """configs/pinn/pinn_pde.py as shipped (64 x 64, feature_nums [16, 32, 64, 96, 128]) at a
+    reduced batch."""
+    import torch
+    c = get_config()
+    c.training.batch_size = batch
+    c.device = torch.device("cpu")
+    return c
+
+
+def make_pinn_inputs(c, seed):
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    B, n = c.training.batch_size, c.data.image_size
+    f1 = torch.rand(B, 1, n, n, generator=g)
+    f2 = torch.rand(B, 1, n, n, generator=g)
+    # coordinate meshes with a small jitter: with an exact mesh the pixel holding both
+    # x.max() and y.max() puts sqrt(0) into get_spatial_embedding and every x/y
+    # sensitivity becomes NaN (in the reference as well)
+    lin = torch.linspace(0.05, 1, n)
+    x = (lin.view(1, 1, 1, n) + 0.01 * torch.rand(B, 1, n, n, generator=g)).contiguous()
+    y = (lin.view(1, 1, n, 1) + 0.01 * torch.rand(B, 1, n, n, generator=g)).contiguous()
+    t = torch.randint(300, 900, (B,), generator=g).float()
+    target = torch.randn(B, 3, n, n, generator=g) * 0.5
+    return f1, f2, x, y, t, target
+
+
+def build_pinn_weights(pinn_cls, c):
+    """Seeded PINN construction + a small perturbation (so the 1e-10-scaled convs carry
+    signal).  The build's PINN reproduces these weights bit for bit (same module order and
+    init as the reference)."""
+    import torch
+    torch.manual_seed(0)
+    model = pinn_cls(c)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    return model
+
+
+_PARITY = []
+
+
+def record_err(what, err, tol):
+    """Log a measured parity error (written to gpurun_out/parity_errors.json at session end
+    when gpurun_out/ exists, so the margins behind each tolerance are on record)."""
+    _PARITY.append({"what": what, "err": float(err), "tol": float(tol)})
+
+
+def pytest_sessionfinish(session, exitstatus):
+    out = os.path.join(REPO, "gpurun_out")
+    if _PARITY and os.path.isdir(out):
+        with open(os.path.join(out, "parity_errors.json"), "w") as f:
+            json.dump(_PARITY, f, indent=1)
+
+
+def regen_draws(seed, n, shape):
+    """The reference PC sampler's noise: n consecutive torch.randn_like draws of `shape` from
+    torch's CPU generator after manual_seed(seed) (no other consumer of the generator runs
+    in between: eval-mode nets draw nothing)."""
+    import torch
+    g = torch.Generator().manual_seed(int(seed))
+    return torch.stack([torch.randn(tuple(shape), generator=g) for _ in range(int(n))])

@@ -35,6 +35,11 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 
 def _install_stubs():
     import torch
+
+    # the build package (put on sys.path by tests/conftest.py) must not shadow the
+    # reference's modules -- its `inverse` is a namespace package, which loses to any
+    # regular package of the same name further down the path
+    sys.path[:] = [p for p in sys.path if os.path.basename(p.rstrip("/")) != "b-pinn-kalman-filter_amd"]
     import torch.utils.cpp_extension as ce
 
     ce.load = lambda *a, **k: types.SimpleNamespace()

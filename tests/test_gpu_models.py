@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, net_fixture, product_config
+from conftest import load_golden, net_fixture, product_config, record_err
 from oracle import nets_ref, score_sde_ref
 
 pytestmark = pytest.mark.gpu
@@ -12,6 +12,9 @@ pytestmark = pytest.mark.gpu
 # fp32 tolerance for whole networks: MIOpen / hipBLASLt accumulate in a different order
 # than the CPU reference (same dtype, different summation order)
 NET_RTOL = 1e-4
+# PC trajectories (N = 25, recorded noise) after the whole run, relative to max(1, max|ref|):
+# measured 2e-7 .. 2e-6 on MI355X (gpurun_out/parity_errors.json, profiles/r02_parity_errors.json)
+PC_RTOL = 2e-4
 
 
 def _model(name, hip):
@@ -24,9 +27,11 @@ def _model(name, hip):
     return cfg, model, x, labels, y
 
 
-def _close(a, b, rtol):
+def _close(a, b, rtol, what=None):
     scale = max(1.0, float(np.abs(b).max()))
     err = float(np.abs(a - b).max())
+    if what:
+        record_err(what, err / scale, rtol)
     assert err <= rtol * scale, f"max err {err:.3e} > {rtol:.1e} * {scale:.3e}"
 
 
@@ -35,7 +40,7 @@ def test_networks_match_reference_fixture(hip, name):
     cfg, model, x, labels, y = _model(name, hip)
     with torch.no_grad():
         out = model(torch.tensor(x, device=hip), torch.tensor(labels, device=hip))
-    _close(out.cpu().numpy(), y, NET_RTOL)
+    _close(out.cpu().numpy(), y, NET_RTOL, f"net {name}")
 
 
 def test_ncsnpp_128_full_size_matches_cpu_oracle(hip):
@@ -56,7 +61,7 @@ def test_ncsnpp_128_full_size_matches_cpu_oracle(hip):
         out = model(x.to(hip), t.to(hip)).cpu().numpy()
     params = nets_ref.init_params(model.state_dict())
     ref = nets_ref.forward(params, c, x, t).numpy()
-    _close(out, ref, NET_RTOL)
+    _close(out, ref, NET_RTOL, "ncsnpp 128 vs oracle")
 
 
 @pytest.mark.parametrize("name", ["em_langevin", "rd_ald", "anc_none", "em_none"])
@@ -84,7 +89,7 @@ def test_pc_sampler_matches_reference_with_injected_noise(hip, name):
                             noise_fn=lambda i, draw: table[(i, draw)])
     out, nfe = eng(model, x_init=torch.tensor(d["prior"]))
     assert nfe == int(d["nfe"])
-    _close(out.cpu().numpy(), d["out"], 2e-3)
+    _close(out.cpu().numpy(), d["out"], PC_RTOL, f"pc {name}")
 
 
 def test_pc_engine_graph_replay_equals_eager_and_is_shard_invariant(hip):

@@ -7,17 +7,14 @@ absolute on O(1) data; network outputs 1e-4 relative to max|ref|; equation_mse v
 their input / parameter sensitivities 2e-3 relative (they are products and sums of
 first and second derivatives through ~30 layers); post-step parameters 1e-5 absolute
 (Adam moves each parameter by <= lr)."""
-import os
-import sys
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, load_golden
+from conftest import build_pinn_weights, load_golden, sample_idx, small_config
 from oracle import correlation_ref as cr
 
-sys.path.insert(0, GOLDEN)
 pytestmark = pytest.mark.gpu
 
 
@@ -51,10 +48,9 @@ def test_correlation_rejects_cpu_tensors():
 
 def _model(dev):
     from configs.pinn import pinn_pde
-    from make_golden_pinn import build_weights, small_config
     from pinn_kalman.pinn import PINN
     c = small_config(pinn_pde.get_config)
-    m = build_weights(PINN, c).to(dev)
+    m = build_pinn_weights(PINN, c).to(dev)
     c.device = dev
     return c, m
 
@@ -69,7 +65,6 @@ def _close(a, ref, rel, what, floor=1e-30):
 
 
 def test_pinn_forward_and_residual_match_reference(hip):
-    from make_golden_pinn import sample_idx
     d = load_golden("pinn_fwd.npz")
     c, m = _model(hip)
     m.train()
@@ -104,7 +99,6 @@ def test_pinn_forward_and_residual_match_reference(hip):
 def test_pinn_train_steps_match_reference(hip, fixture, factory):
     import losses
     from inverse.operators import InpaintOperator
-    from make_golden_pinn import sample_idx
     from models.ema import ExponentialMovingAverage
     d = load_golden(fixture)
     c, m = _model(hip)

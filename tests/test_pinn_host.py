@@ -71,13 +71,11 @@ def test_pinn_parameter_counts_match_reference():
 def test_pinn_seeded_weights_reproduce_reference_fixture():
     """The seeded construction recipe of the fixture generator yields the reference's
     weights bit for bit (same module order and init) -- the GPU tests rely on it."""
-    import sys
-    sys.path.insert(0, __import__("os").path.join(__import__("conftest").GOLDEN))
-    from make_golden_pinn import build_weights, sample_idx, small_config
+    from conftest import build_pinn_weights, sample_idx, small_config
     from configs.pinn import pinn_pde
     from pinn_kalman.pinn import PINN
     d = load_golden("pinn_fwd.npz")
-    m = build_weights(PINN, small_config(pinn_pde.get_config))
+    m = build_pinn_weights(PINN, small_config(pinn_pde.get_config))
     sd = m.state_dict()
     keys = [k[6:] for k in d.files if k.startswith("sdsub:")]
     assert sorted(keys) == sorted(sd.keys())
