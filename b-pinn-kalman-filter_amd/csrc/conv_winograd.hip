@@ -37,7 +37,11 @@ constexpr int kTR = 4, kTC = 8;          // tiles per region (rows, cols)
 constexpr int kM = kTR * kTC;            // 32 tiles
 constexpr int kPR = 2 * kTR + 2;         // 10 patch rows
 constexpr int kPC = 2 * kTC + 2;         // 18 patch cols
-constexpr int kPCp = kPC + 1;            // padded LDS row
+// LDS row pitch of the input patch: 24 floats.  The V transform reads each 4 x 4 input tile
+// as 8 ds_read_b64 at dword offsets 24 (2 ty + i) + 2 tx: per 32-lane group (one cin, 32
+// tiles) the four tile rows land on dword banks {0-15, 48-63, 32-47, 16-31} (48 ty mod 64)
+// -- all 64 banks once, conflict-free (a pitch of 19 with 16 ds_read_b32 was 2-way)
+constexpr int kPCp = 24;
 constexpr int kCK = 8;                   // cin per chunk
 constexpr int kOutRows = 2 * kTR, kOutCols = 2 * kTC;  // 8 x 16 pixels
 
@@ -105,6 +109,27 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 // (zero padding stays zero), so the normalized tensor is never written to HBM.
 // fast exp / reciprocal: a few ulp, far inside the network tolerance (1e-4)
 __device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+
+// q = a / d, r = a % d for a block index: a shift when d is a power of two (every NCSN++ /
+// DDPM++ shape), else a 32-bit unsigned division -- the 64-bit forms were ~600 scalar
+// instructions of the workgroup prologue
+__device__ inline unsigned udivmod(unsigned a, unsigned d, unsigned& r) {
+  if ((d & (d - 1)) == 0) {
+    r = a & (d - 1);
+    return a >> __builtin_ctz(d);
+  }
+  const unsigned q = a / d;
+  r = a - q * d;
+  return q;
+}
+
+// a / b correctly rounded (== IEEE division, bit for bit) from r = 1 / b (correctly rounded,
+// computed once): q = a r, then one Markstein correction with the exact residual a - b q.
+// 3 VALU instead of the ~10 of a full-range division (the residual tail divides by sqrt 2).
+__device__ inline float div_rn(float a, float b, float r) {
+  const float q = a * r;
+  return fmaf(fmaf(-q, b, a), r, q);
+}
 
 // Coalesced stores of one wave's staged output (kWN couts x 8 rows x 16 cols, LDS s_w[co]
 // at stride kOS), with the residual-block tail, and -- stats != nullptr -- the GroupNorm
@@ -415,36 +440,27 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
     float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2) {
   constexpr int kWN = 16 * NB;  // couts per wave
   constexpr int kPatch = kCK * kPR * kPCp;
-  __shared__ float s_patch_raw[2][kPatch];                                  // 2 x 5.9 KB
-  // V double buffer; after the K loop the same LDS stages the output (NB x 33.8 KB)
+  __shared__ __attribute__((aligned(16))) float s_patch_raw[2][kPatch];     // 2 x 7.5 KB
   constexpr int kVBuf = kCK * kM * kVS;                                      // 20.5 KB
-  constexpr int kOutLds = 4 * kWN * kOS;
-  __shared__ __attribute__((aligned(16))) float s_vo[2 * kVBuf > kOutLds ? 2 * kVBuf : kOutLds];
-  float(*s_v)[kVBuf] = reinterpret_cast<float(*)[kVBuf]>(s_vo);
-  float* s_out = s_vo;
+  __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];              // V double buffer
   __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];  // PRE: (s, t) of every input channel
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  int64_t nblk = (int64_t)gridDim.x;
-  int64_t b = blockIdx.x;
-  if (xcd_remap) b = (b % 8) * (nblk / 8) + b / 8;
-  const int cb = (int)(b % g.cout_blocks);
-  int64_t r = b / g.cout_blocks;
-  const int rx = (int)(r % g.regions_x);
-  r /= g.regions_x;
-  const int ry = (int)(r % g.regions_y);
-  const int n = (int)(r / g.regions_y);
-  const int oy0 = ry * kOutRows, ox0 = rx * kOutCols;
-  const int cout_w = cb * (4 * kWN) + wave * kWN;
+  // grid < 2^31 blocks (host check): 32-bit block arithmetic
+  const unsigned nblk = gridDim.x;
+  unsigned b = blockIdx.x;
+  if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
+  unsigned cb, rx, ry;
+  unsigned r = udivmod(b, (unsigned)g.cout_blocks, cb);
+  r = udivmod(r, (unsigned)g.regions_x, rx);
+  const int n = (int)udivmod(r, (unsigned)g.regions_y, ry);
+  const int oy0 = (int)ry * kOutRows, ox0 = (int)rx * kOutCols;
+  const int cout_w = (int)cb * (4 * kWN) + wave * kWN;
 
+  // accumulators: the first chunk's k-step 0 MFMAs take an inline-constant zero C operand
+  // (no 128 register clears in the prologue)
   f4 acc[16][2][NB];
-#pragma unroll
-  for (int p = 0; p < 16; ++p)
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int64_t plane = (int64_t)g.H * g.W;
   const int C2 = g.Cin - g.C1;
@@ -527,7 +543,12 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[i][j] = sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j];
+      for (int j = 0; j < 4; j += 2) {
+        const float2 v2 =
+            *reinterpret_cast<const float2*>(&sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j]);
+        d[i][j] = v2.x;
+        d[i][j + 1] = v2.y;
+      }
   };
   auto write_v = [&](float* sv) {
     float t[4][4];
@@ -582,8 +603,9 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) a[q] = src[q];
   }
-  auto step = [&](int k, auto sb_c) {
+  auto step = [&](int k, auto sb_c, auto first_c) {
     constexpr int SB = decltype(sb_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
     const float* sv = s_v[SB];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
@@ -602,7 +624,8 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[4 * q + pp][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                a[q][pp], uo[ks][nb][q][pp], acc[4 * q + pp][mb][nb], 0, 0, 0);
+                a[q][pp], uo[ks][nb][q][pp],
+                (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb][nb], 0, 0, 0);
         // refill: A of the next group (the next chunk's group 0 comes after the barrier)
         if (grp < 3) a[q] = a_src(sv, grp + 1)[q];
         if (mb == 1) {
@@ -624,39 +647,82 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       for (int q = 0; q < 4; ++q) a[q] = src[q];
     }
   };
-  int k = 0;
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using F = std::false_type;
+  step(0, C0{}, std::true_type{});
+  int k = 1;
   for (; k + 1 < nch; k += 2) {
-    step(k, std::integral_constant<int, 0>{});
-    step(k + 1, std::integral_constant<int, 1>{});
+    step(k, C1{}, F{});
+    step(k + 1, C0{}, F{});
   }
-  if (k < nch) step(k, std::integral_constant<int, 0>{});
+  if (k < nch) step(k, C1{}, F{});
 
-  // output transform (lane-local) -> per-wave LDS staging [cout][8 x 16 pixels]
+  // output transform straight from registers to global memory (no LDS staging, no
+  // barrier).  Per M-block a lane holds tiles m = 16 mb + 4 kq + rg, rg = 0..3: tile row
+  // 2 mb + kq / 2, tile cols 4 (kq & 1) + rg -- 2 output rows x 8 pixels of channel
+  // cout_w + 16 nb + jj, stored as two 16-B strips per row (lanes kq, kq ^ 1 cover a whole
+  // 64-B row).  GroupNorm partial statistics: a running Chan merge over the lane's 32
+  // values, then the 4 lanes jj + 16 kq (equal counts, symmetric butterfly: same bits).
+  const float rdiv = 1.f / g.div;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    float* so = &s_out[(wave * kWN + 16 * nb + jj) * kOS];
-    const float bv = (bias && cout_w + 16 * nb + jj < g.CoutS) ? bias[cout_w + 16 * nb + jj] : 0.f;
+    if (cout_w + 16 * nb >= g.CoutS) continue;  // padded couts (wave-uniform: CoutS % 16 == 0)
+    const int co = cout_w + 16 * nb + jj;
+    const float bv = bias ? bias[co] : 0.f;
+    const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
+    float lm = 0.f, lm2 = 0.f;
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
+      const int oy = oy0 + 2 * (2 * mb + (kq >> 1));
+      const int ox = ox0 + 8 * (kq & 1);
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int m = mb * 16 + 4 * kq + rg;
-        const int ty = m / kTC, tx = m - ty * kTC;
-        float t0[4], t1[4];
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          t0[j] = acc[j][mb][nb][rg] + acc[4 + j][mb][nb][rg] + acc[8 + j][mb][nb][rg];
-          t1[j] = acc[4 + j][mb][nb][rg] - acc[8 + j][mb][nb][rg] - acc[12 + j][mb][nb][rg];
+        for (int e = 0; e < 2; ++e) {
+          f4 v;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int rg = 2 * e + u;
+            float t[4];  // row h of A^T M, A^T = [[1,1,1,0],[0,1,-1,-1]]
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              t[j] = h == 0 ? acc[j][mb][nb][rg] + acc[4 + j][mb][nb][rg] + acc[8 + j][mb][nb][rg]
+                            : acc[4 + j][mb][nb][rg] - acc[8 + j][mb][nb][rg] - acc[12 + j][mb][nb][rg];
+            v[2 * u] = t[0] + t[1] + t[2] + bv;
+            v[2 * u + 1] = t[1] - t[2] - t[3] + bv;
+          }
+          const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
+          if (skip) {  // residual block tail, bit-identical to bpk_residual_rescale_f32
+            const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = div_rn(sk[c] + v[c], g.div, rdiv);
+          }
+          *reinterpret_cast<f4*>(&y[o]) = v;
+          if (stats) {  // strip s = 4 mb + 2 h + e joins the s strips (4 s values) before it
+            const float sm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+            float sm2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sm2 = fmaf(v[c] - sm, v[c] - sm, sm2);
+            constexpr float kW[8] = {1.f, 1.f / 2, 1.f / 3, 1.f / 4, 1.f / 5, 1.f / 6, 1.f / 7, 1.f / 8};
+            const int st = 4 * mb + 2 * h + e;
+            const float d = sm - lm;
+            lm = lm + d * kW[st];
+            lm2 = (lm2 + sm2) + d * d * (4.f * st * kW[st]);
+          }
         }
-        so[(2 * ty) * kOutCols + 2 * tx] = t0[0] + t0[1] + t0[2] + bv;
-        so[(2 * ty) * kOutCols + 2 * tx + 1] = t0[1] - t0[2] - t0[3] + bv;
-        so[(2 * ty + 1) * kOutCols + 2 * tx] = t1[0] + t1[1] + t1[2] + bv;
-        so[(2 * ty + 1) * kOutCols + 2 * tx + 1] = t1[1] - t1[2] - t1[3] + bv;
+      }
+    }
+    if (stats) {
+      merge_stats(lm, lm2, __shfl_xor(lm, 16, 64), __shfl_xor(lm2, 16, 64), 32.f);
+      merge_stats(lm, lm2, __shfl_xor(lm, 32, 64), __shfl_xor(lm2, 32, 64), 64.f);
+      if (kq == 0) {
+        const int R = g.regions_x * g.regions_y;
+        const int region = (oy0 / kOutRows) * g.regions_x + ox0 / kOutCols;
+        stats[((int64_t)n * g.CoutS + co) * R + region] = make_float2(lm, lm2);
       }
     }
   }
-  __syncthreads();
-  store_tile<kWN>(&s_out[wave * kWN * kOS], skip, y, stats, g, n, cout_w, oy0, ox0, lane);
 }
 
 // Persistent form of the pipelined kernel (NB = 1: 4 waves x 16 couts = 64 couts, 32
