@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-pinn", action="store_true")
     ap.add_argument("--dps-steps", type=int, default=2, help="accepted RK45 steps timed")
     ap.add_argument("--no-dps", action="store_true")
+    ap.add_argument("--ns-steps", type=int, default=20, help="ns_step full steps timed; 0: skip")
+    ap.add_argument("--ncddpmpp-steps", type=int, default=10,
+                    help="nc_ddpmpp (ddpm, ancestral) 128^2 PC steps timed; 0: skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=8,
@@ -84,16 +87,6 @@ def build_model(dev, seed=0):
     return c, model
 
 
-def _pmc_traffic(kernel_key):
-    """HBM bytes per launch of a roofline kernel, from the committed PMC passes
-    (profiles/r01_pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, same kernel and shape)."""
-    try:
-        with open(os.path.join(REPO, "profiles", "r01_pmc_traffic.json")) as f:
-            return json.load(f)[kernel_key]["traffic_bytes"]
-    except (OSError, KeyError, ValueError):
-        return None
-
-
 def time_kernel(fn, stream, reps=10):
     """Average duration (s) of fn() measured with HIP events on `stream`."""
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -108,68 +101,160 @@ def time_kernel(fn, stream, reps=10):
     return s.elapsed_time(e) / 1e3 / reps
 
 
-def conv_roofline(dev, batch):
-    """Dominant kernel of the score net (~75 % of a PC step): the fused, software-pipelined
-    Winograd F(2x2,3x3) MFMA conv3x3 (csrc/conv_winograd.hip wino_f23_pipe_kernel), measured
-    on its most frequent shape, 128 -> 128 channels @ 128x128 (13 per forward, SURVEY 8(a)
-    a11).  MFMA-bound.
+# The sampler's dominant kernel: the Winograd conv with the GroupNorm+SiLU prologue
+# (csrc/conv_winograd.hip wino_f23_pipe_kernel<1, true>), ~75 % of a PC step.  Its roofline
+# is taken over the NCSN++ 128x128 shape mix it runs in the sampler: per (cin, cout, hw) the
+# PRE form with bias + GroupNorm partial statistics (Conv_0 of a BigGAN block) and with the
+# residual tail (Conv_1), weighted by their counts per forward.
+WINO_MIX = [  # (cin, cout, hw, PRE+stats convs per forward, PRE+residual convs per forward)
+    (128, 128, 128, 7, 6), (256, 128, 128, 4, 0), (256, 256, 128, 1, 1),
+    (256, 256, 64, 7, 7), (512, 256, 64, 4, 0), (128, 256, 64, 1, 0),
+    (256, 256, 32, 9, 8)]
 
-    achieved = the kernel's algorithmic MFMA FLOPs per launch -- Winograd F(2,3) multiplies
-    16 transformed values per 2x2 output tile per (cin, cout), i.e. 4/9 of the direct
-    convolution's 2*B*Cin*Cout*9*H*W -- over the HIP-event launch time on the launch
-    stream.  `direct_equivalent_tflops` restates the same time against the direct-conv FLOP
-    count (what MIOpen's implicit GEMM executes), `miopen_*` times F.conv2d on the same data."""
-    import torch.nn.functional as F
+
+def _pmc(key):
+    """HBM bytes of a roofline kernel from the committed PMC passes (FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction; profiles/r02_pmc_traffic.json)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "r02_pmc_traffic.json")) as f:
+            return json.load(f)[key]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def wino_mix_times(dev, batch, reps=10):
+    """Per-shape HIP-event launch times (s) of the PRE+stats and PRE+residual forms."""
     from op.conv import conv3x3, filter_transform
-    x = torch.randn(batch, 128, 128, 128, device=dev)
-    w = torch.randn(128, 128, 3, 3, device=dev) * 0.02
     st = torch.cuda.Stream(dev)
-    with torch.cuda.stream(st):
-        filter_transform(w)
-        t = time_kernel(lambda: conv3x3(x, w), st)
-        tm = time_kernel(lambda: F.conv2d(x, w, padding=1), st)
-    direct = 2.0 * batch * 128 * 128 * 9 * 128 * 128
-    wino = direct * 4.0 / 9.0
-    ach = wino / t / 1e12
+    g = torch.Generator(device=dev).manual_seed(0)
+    out = []
+    for cin, cout, hw, n_pre, n_res in WINO_MIX:
+        x = torch.randn(batch, cin, hw, hw, device=dev, generator=g)
+        w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
+        b = torch.randn(cout, device=dev, generator=g)
+        pre = torch.stack([torch.rand(batch, cin, device=dev, generator=g) + 0.5,
+                           torch.randn(batch, cin, device=dev, generator=g) * 0.1], -1).contiguous()
+        skip = torch.randn(batch, cout, hw, hw, device=dev, generator=g)
+        with torch.cuda.stream(st):
+            filter_transform(w)
+            t_pre = time_kernel(lambda: conv3x3(x, w, b, pre=pre, stats=True), st, reps)
+            t_res = time_kernel(lambda: conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre), st, reps)
+        fl = 2.0 * batch * cin * cout * 16 * (hw // 2) ** 2  # executed MFMA FLOPs (Winograd)
+        out.append(dict(cin=cin, cout=cout, hw=hw, n_pre=n_pre, n_res=n_res, t_pre=t_pre,
+                        t_res=t_res, flop=fl))
+        del x, skip
+    return out
+
+
+def conv_roofline(dev, batch):
+    """achieved = executed MFMA FLOPs of one forward's PRE-conv mix / its HIP-event time.
+    Winograd F(2,3) multiplies 16 transformed values per 2x2 output tile per (cin, cout):
+    2 * B * Cin * Cout * 16 * (H/2)(W/2) FLOPs per launch = 4/9 of the direct convolution
+    (`direct_equivalent_tflops` restates the time on the direct count)."""
+    rows = wino_mix_times(dev, batch)
+    t = sum(r["n_pre"] * r["t_pre"] + r["n_res"] * r["t_res"] for r in rows)
+    fl = sum((r["n_pre"] + r["n_res"]) * r["flop"] for r in rows)
+    n_launch = sum(r["n_pre"] + r["n_res"] for r in rows)
+    ach = fl / t / 1e12
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": _pmc_traffic("wino_f23_pipe_kernel conv3x3 128->128 @128x128 B=64")
-            if batch == 64 else None,
-            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-            "kernel": "wino_f23_pipe_kernel conv3x3 128->128 @128x128 fp32 (hand-written, f32 MFMA)",
-            "ms_per_launch": round(t * 1e3, 4), "flop_per_launch": wino,
-            "direct_equivalent_tflops": round(direct / t / 1e12, 2),
-            "miopen_ms_per_launch": round(tm * 1e3, 4),
-            "miopen_tflops": round(direct / tm / 1e12, 2)}
+            "traffic": _pmc("wino_pre_mix") if batch == 64 else None,
+            "traffic_unit": "HBM bytes per forward mix (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+            "algorithmic_bytes": sum((r["n_pre"] + r["n_res"]) * 4.0 * batch * (r["cin"] + r["cout"]) * r["hw"] ** 2
+                                     + r["n_res"] * 4.0 * batch * r["cout"] * r["hw"] ** 2 for r in rows),
+            "kernel": "wino_f23_pipe_kernel<1,true> (GroupNorm+SiLU prologue; bias + GN partial "
+                      "statistics or residual tail): the NCSN++ 128x128 forward's PRE-conv mix, "
+                      f"{n_launch} launches, B={batch}",
+            "flop_basis": "executed (Winograd, 4/9 of direct)",
+            "ms_per_mix": round(t * 1e3, 3), "flop_per_mix": fl,
+            "direct_equivalent_tflops": round(fl * 9 / 4 / t / 1e12, 2),
+            "per_shape": [dict(shape=f"{r['cin']}->{r['cout']}@{r['hw']}",
+                               pre_ms=round(r["t_pre"] * 1e3, 4), res_ms=round(r["t_res"] * 1e3, 4),
+                               pre_tflops=round(r["flop"] / r["t_pre"] / 1e12, 1))
+                          for r in rows]}
 
 
-def upfirdn_roofline(dev, batch):
-    """HBM roofline of upfirdn2d on the NCSN++ down2 shape [B,128,128,128] -> [B,128,64,64]."""
+# SURVEY.md 8(d) upfirdn2d shapes (B = 64), k = outer([1,3,3,1])/64 (x4 for up)
+UPFIRDN_SHAPES = [("down2 [64,128,128,128] pad(1,1)", (128, 128), dict(down=2, pad=(1, 1)), 1.0),
+                  ("up2 [64,256,64,64] pad(2,1)", (256, 64), dict(up=2, pad=(2, 1)), 4.0),
+                  ("down2 [64,256,64,64] pad(1,1)", (256, 64), dict(down=2, pad=(1, 1)), 1.0),
+                  ("fir [64,128,64,64] pad(2,2)", (128, 64), dict(pad=(2, 2)), 1.0)]
+
+
+def _upfirdn_out(hw, kw):
+    up, down = kw.get("up", 1), kw.get("down", 1)
+    p0, p1 = kw["pad"]
+    return (hw * up + p0 + p1 - 4) // down + 1
+
+
+def upfirdn_rooflines(dev, batch):
+    """HBM roofline of upfirdn2d on the four 8(d) shapes: bytes = 4 (in + out) per launch."""
     from op import upfirdn2d
     k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32, device=dev)
-    x = torch.randn(batch, 128, 128, 128, device=dev)
     st = torch.cuda.Stream(dev)
-    with torch.cuda.stream(st):
-        t = time_kernel(lambda: upfirdn2d(x, k, down=2, pad=(1, 1)), st)
-    nbytes = 4.0 * (x.numel() + x.numel() // 4)
-    ach = nbytes / t / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": _pmc_traffic("upfirdn2d down2 k4 [64,128,128,128]") if batch == 64 else None,
-            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-            "kernel": "upfirdn2d down2 k4 [B,128,128,128]", "ms_per_launch": round(t * 1e3, 4),
-            "bytes_per_launch": nbytes}
+    res = []
+    for name, (c, hw), kw, gain in UPFIRDN_SHAPES:
+        x = torch.randn(batch, c, hw, hw, device=dev)
+        with torch.cuda.stream(st):
+            t = time_kernel(lambda: upfirdn2d(x, k * gain, **kw), st)
+        ho = _upfirdn_out(hw, kw)
+        nbytes = 4.0 * (x.numel() + batch * c * ho * ho)
+        ach = nbytes / t / 1e9
+        res.append({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": _pmc("upfirdn2d " + name) if batch == 64 else None,
+                    "kernel": "upfirdn2d " + name, "ms_per_launch": round(t * 1e3, 4),
+                    "bytes_per_launch": nbytes})
+        del x
+    return res
+
+
+def cpu_upfirdn_baseline():
+    """The oracle's torch-CPU upfirdn2d (the reference's upfirdn2d_native algorithm: zero
+    insertion, pad, conv2d with the flipped kernel, stride) on bounded samples of the four
+    8(d) shapes (batch 4 instead of 64), best of 5, algorithmic GB/s."""
+    from oracle.upfirdn2d_ref import upfirdn2d_torch
+    k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32)
+    res = {}
+    for name, (c, hw), kw, gain in UPFIRDN_SHAPES:
+        x = torch.randn(4, c, hw, hw)
+        best = 1e9
+        for _ in range(5):
+            t0 = time.perf_counter()
+            y = upfirdn2d_torch(x, k * gain, kw.get("up", 1), kw.get("down", 1), kw["pad"])
+            best = min(best, time.perf_counter() - t0)
+        res[name] = round(4.0 * (x.numel() + y.numel()) / best / 1e9, 3)
+    return {"value": res, "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": "oracle.upfirdn2d_ref.upfirdn2d_torch on the 8(d) shapes at batch 4, best of 5"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _cpu_threads():
+    cores = len(os.sched_getaffinity(0))
+    return min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
 
 
 def cpu_baseline(n_samples):
-    """The oracle (torch-CPU restatement of the reference path) on the host cores: one warm-up
-    PC step on 1 sample, then 1 PC step (EM + Langevin = 2 evals/sample) on n_samples."""
+    """The oracle (torch-CPU restatement of the reference path, same aten op sequence) on the
+    host cores: one warm-up PC step on 1 sample, then 1 PC step (EM + Langevin = 2 evals per
+    sample) on n_samples.  Deviation from BASELINE.md's plan (B = 64 x 3 steps = 384 evals,
+    ~5 min at ~1.4 evals/s): a bounded 2 x n_samples-eval sample keeps the default bench
+    within minutes; evals/s does not depend on the number of steps."""
     from configs.vp import nc_ncsnpp_128
     from oracle import nets_ref, score_sde_ref
     import models  # noqa: F401
     from models import utils as mutils
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    cores = _cpu_threads()
     torch.set_num_threads(cores)
     c = nc_ncsnpp_128.get_config()
     c.device = "cpu"
@@ -184,9 +269,169 @@ def cpu_baseline(n_samples):
                             "langevin", 0.075, 1, True, n_iters=1)
     dt = time.perf_counter() - t0
     return {"value": round(2 * n_samples / dt, 4), "unit": "score-net evals/s", "cores": cores,
-            "kind": "port",
+            "kind": "port", "cpu": _cpu_model(),
             "sample": f"oracle/nets_ref + score_sde_ref: 1 PC step (EM+Langevin) on {n_samples} "
-                      f"samples of 128x128x1, {dt:.1f}s, cpu={platform.processor() or 'x86_64'}"}
+                      f"samples of 128x128x1 = {2 * n_samples} evals in {dt:.1f}s (plan: B=64 x 3 "
+                      "steps; bounded sample, same per-eval work)"}
+
+
+def cpu_train_baselines():
+    """The oracle's DSM train step on the host cores: nets_ref forward (same aten op sequence
+    as the reference) + autograd backward + torch Adam + EMA, continuous VP-SDE loss
+    (score_sde_ref.dsm_loss).  Bounded samples: NCSN++ 128x128x1 at B=1 (1 warm-up + 1 timed
+    step), CIFAR-10 NCSN++ 32x32x3 at B=4 (1 + 2).  Unit: samples/s (and steps/s at that
+    batch)."""
+    from configs.vp import cifar10_ncsnpp_continuous, nc_ncsnpp_128
+    from oracle import nets_ref, score_sde_ref
+    import models  # noqa: F401
+    from models import utils as mutils
+    cores = _cpu_threads()
+    torch.set_num_threads(cores)
+    out = {}
+    for key, mod, B, C, n, steps in (("ncsnpp128", nc_ncsnpp_128, 1, 1, 128, 1),
+                                     ("cifar", cifar10_ncsnpp_continuous, 4, 3, 32, 2)):
+        c = mod.get_config()
+        c.device = "cpu"
+        c.model.dropout = 0.0
+        torch.manual_seed(0)
+        params = nets_ref.init_params(mutils.create_model(c, wrap=False).state_dict())
+        leaves = [v for v in params.values() if isinstance(v, torch.Tensor) and v.is_floating_point()]
+        for v in leaves:
+            v.requires_grad_(True)
+        opt = torch.optim.Adam(leaves, lr=2e-4)
+        ema = [v.detach().clone() for v in leaves]
+        sde = score_sde_ref.SDESpec("vp", N=1000)
+        mf = lambda x, t: nets_ref.forward(params, c, x, t)
+        x = torch.rand(B, C, n, n)
+
+        def step():
+            opt.zero_grad()
+            t = torch.rand(B) * (1 - 1e-5) + 1e-5
+            loss = score_sde_ref.dsm_loss(mf, sde, x, t, torch.randn_like(x))
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(leaves, 1.0)
+            opt.step()
+            with torch.no_grad():
+                for e, v in zip(ema, leaves):
+                    e.mul_(0.999).add_(v.detach(), alpha=0.001)
+        step()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dt = (time.perf_counter() - t0) / steps
+        out[key] = {"value": round(B / dt, 4), "unit": "train samples/s",
+                    "steps_per_s": round(1 / dt, 4), "batch": B, "cores": cores, "kind": "port",
+                    "sample": f"oracle nets_ref DSM step ({key}) at B={B}: 1 warm-up + {steps} "
+                              f"timed, {dt:.1f}s/step"}
+    return out
+
+
+def cpu_ns_baseline():
+    """The C restatement of the reference ns_step (oracle/ns_step_ref.c, single thread) on a
+    bounded sample: B = 16 replicas of 192x192, 3 full steps (velocity, pressure, density)."""
+    from oracle import ns_step_ref
+    f, v, p = _ns_fields(np.random.default_rng(0), 16, 192)
+    ns_step_ref.full_step(f, v, p, 0.0025, 0.005)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        f, v, p = ns_step_ref.full_step(f, v, p, 0.0025, 0.005)
+    dt = time.perf_counter() - t0
+    return {"value": round(3 * 16 * 192 * 192 / dt / 1e9, 4), "unit": "Gsite/s", "cores": 1,
+            "kind": "port", "sample": "oracle/ns_step_ref.c (gcc -O2, 1 thread): 3 full steps of "
+                                      f"16 x 192^2, {dt:.2f}s"}
+
+
+def _ns_fields(rng, B, n):
+    """SURVEY.md 8(d) cfg #4 fields: f ~ U(0.1, 1), p ~ N(0, 0.01), u, v ~ U(0.05, 0.5) with a
+    random sign (|value| >= 0.05: no exact zero, which is NaN in the reference CIP)."""
+    f = rng.uniform(0.1, 1.0, (B, 1, n, n)).astype(np.float32)
+    p = rng.normal(0, 0.01, (B, 1, n, n)).astype(np.float32)
+    v = (rng.uniform(0.05, 0.5, (B, 2, n, n)) * rng.choice([-1.0, 1.0], (B, 2, n, n))).astype(np.float32)
+    return f, v, p
+
+
+def bench_ns_step(args, ctx, dev):
+    """configs[3]'s simulator workload (SURVEY.md 8(d) cfg #4): ns_step full step (velocity,
+    pressure, density; two fused launches) on B = 256 replicas of 192x192 per GPU,
+    dt = 0.0025, dx = 0.005.  Unit: site-updates/s.  HBM roofline at the algorithmic
+    32 B/site (read f, u, v, p; write f, u, v, p); the kernels are VALU-bound by the
+    reference-exact arithmetic (fp64 CIP terms, correctly rounded divisions)."""
+    from op import ns_step
+    B, n = 256, 192
+    f, v, p = (torch.tensor(a, device=dev) for a in _ns_fields(np.random.default_rng(ctx.rank), B, n))
+    bufs = [(torch.empty_like(f), torch.empty_like(v), torch.empty_like(p)) for _ in range(2)]
+    st = torch.cuda.Stream(dev)
+    steps = args.ns_steps
+
+    def run(k):
+        cur = (f, v, p)
+        for i in range(k):
+            cur = ns_step.full_step(*cur, 0.0025, 0.005, out=bufs[i % 2])
+        return cur
+
+    with torch.cuda.stream(st):
+        run(3)
+    st.synchronize()
+    ctx.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):
+        e0.record(st)
+        run(steps)
+        e1.record(st)
+    st.synchronize()
+    ctx.barrier()
+    dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
+    t_step = e0.elapsed_time(e1) / 1e3 / steps
+    sites = B * n * n
+    gbs = 32.0 * sites / t_step / 1e9
+    return {"ns_gsites_per_s": round(sites * steps * ctx.world_size / dt / 1e9, 3),
+            "ns_ms_per_step": round(t_step * 1e3, 4),
+            "ns_config": "configs[3] simulator: ns_step full step, 256 x 192x192 per GPU",
+            "roofline_ns_step": {"bound": "valu (reference-exact fp64/division arithmetic)",
+                                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                 "traffic": _pmc("ns_step full step B256 192^2"),
+                                 "kernel": "ns_step fused velocity + pressure/density launches",
+                                 "bytes_per_step": 32.0 * sites}}
+
+
+def bench_ncddpmpp(args, ctx, dev):
+    """The literal configs[2] variant: configs/vp/nc_ddpmpp.py at 128x128x1
+    (model `ddpm`, discrete VP, ancestral_sampling predictor, no corrector), B = 64 per GPU,
+    graph-replayed PC steps; 1 score evaluation per sample per step."""
+    import models  # noqa: F401
+    import sampling
+    import sde_lib
+    from configs.vp import nc_ddpmpp
+    from models import utils as mutils
+    c = nc_ddpmpp.get_config()
+    c.data.image_size = 128
+    c.device = dev
+    torch.manual_seed(0)
+    model = mutils.create_model(c, wrap=False).eval()
+    with torch.no_grad():
+        for prm in model.parameters():
+            prm.add_(torch.randn_like(prm) * 0.01)
+    B = args.batch
+    sde = sde_lib.VPSDE(c.model.beta_min, c.model.beta_max, c.model.num_scales)
+    eng = sampling.PCEngine(sde, (B, 1, 128, 128), sampling.AncestralSamplingPredictor,
+                            sampling.NoneCorrector, c.sampling.snr, 1, continuous=False,
+                            device=dev, seed=4321, dist_ctx=ctx if ctx.world_size > 1 else None)
+    eng.reset(model)
+    eng.advance(2)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    eng.advance(args.ncddpmpp_steps)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
+    return {"ncddpmpp_evals_per_s": round(B * ctx.world_size * args.ncddpmpp_steps / dt, 2),
+            "ncddpmpp_ms_per_step": round(dt / args.ncddpmpp_steps * 1e3, 2),
+            "ncddpmpp_tflops": round(B * ctx.world_size * args.ncddpmpp_steps * 300.53e9 / dt / 1e12, 2),
+            "ncddpmpp_config": "configs[2] literal: nc_ddpmpp (ddpm, 300.53 GFLOP/eval) 128x128x1, "
+                               "ancestral + none, discrete, B=64/GPU"}
 
 
 def pinn_batch(c, B, dev, seed=0):
@@ -407,6 +652,11 @@ def main():
     evals_per_s = evals / dt
     ms_per_step = dt / args.steps * 1e3
 
+    roof = None
+    if ctx.rank == 0:
+        log("dominant-kernel roofline (right after the sampler: same clock regime)")
+        roof = conv_roofline(dev, B)
+
     # ---------------------------------------------------------------- DSM train step
     train = None
     if not args.no_train:
@@ -458,11 +708,20 @@ def main():
         log("DPS function evaluations")
         dps = bench_dps(args, ctx, dev)
 
+    ns = None
+    if args.ns_steps > 0:
+        log("ns_step simulator steps")
+        ns = bench_ns_step(args, ctx, dev)
+
+    ncd = None
+    if args.ncddpmpp_steps > 0:
+        log("nc_ddpmpp 128^2 ancestral sampler")
+        ncd = bench_ncddpmpp(args, ctx, dev)
+
     result = None
     if ctx.rank == 0:
-        log("rooflines")
-        roof = conv_roofline(dev, B)
-        up_roof = upfirdn_roofline(dev, B)
+        log("upfirdn2d rooflines")
+        up_roof = upfirdn_rooflines(dev, B)
         model_tflops = evals_per_s * NCSNPP_GFLOP_PER_EVAL / 1e3
         result = {
             "metric": "PC-sampler score-net evals/s (NCSN++ 128x128x1, EM + Langevin)",
@@ -476,23 +735,23 @@ def main():
                        "seq_len": None, "parallelism": f"dp{world} (batch-sharded, RCCL)",
                        "hip_graph": eng.graph is not None},
             "score_net_tflops": round(model_tflops, 2),
-            "score_net_mfma_frac": round(model_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+            "score_net_mfma_frac_direct_equivalent": round(model_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
             "samples_finite": finite,
             "roofline": roof,
             "roofline_upfirdn2d": up_roof,
         }
-        if train:
-            result.update(train)
-        if cifar:
-            result.update(cifar)
-        if pinn:
-            result.update(pinn)
-        if dps:
-            result.update(dps)
+        for part in (train, cifar, pinn, dps, ns, ncd):
+            if part:
+                result.update(part)
     if world == 1 and not args.no_cpu_baseline and ctx.rank == 0:
         log("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(args.cpu_samples)
         result["speedup_vs_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+        log("cpu baselines of the other rows")
+        extra = {"upfirdn2d": cpu_upfirdn_baseline(), "ns_step": cpu_ns_baseline()}
+        if not args.no_train:
+            extra.update(cpu_train_baselines())
+        result["cpu_baselines_other"] = extra
     if ctx.rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

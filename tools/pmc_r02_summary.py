@@ -1,0 +1,83 @@
+"""Summarise the round-2 PMC passes (tools/gpu_pmc_r02.sh -> gpurun_out/pmc2) into
+profiles/r02_pmc_traffic.json (bench.py reads `traffic_bytes`) and profiles/r02_pmc_sq.json.
+FETCH_SIZE / WRITE_SIZE are in KB; FETCH_SIZE is doubled (MI355X_MICROARCH.md: on gfx950 it
+reports half of a wide streaming read)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO]
+SRC = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc2")
+
+
+def load(pattern, keep):
+    f = glob.glob(os.path.join(SRC, pattern, "pmc_counter_collection.csv"))[0]
+    agg = collections.defaultdict(dict)
+    for r in csv.DictReader(open(f)):
+        if keep(r["Kernel_Name"]):
+            agg[int(r["Dispatch_Id"])][r["Counter_Name"]] = \
+                agg[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            agg[int(r["Dispatch_Id"])]["_grid"] = int(r["Grid_Size"])
+    return [agg[d] for d in sorted(agg)]
+
+
+def main():
+    import bench
+    wino = lambda k: "wino_f23" in k
+    fetch = load("*_mix", wino) if False else None  # placeholder for readability
+    mix_f = [d["FETCH_SIZE"] for d in load("p3_mix", wino)]
+    mix_w = [d["WRITE_SIZE"] for d in load("p4_mix", wino)]
+    n = sum(r[3] + r[4] for r in bench.WINO_MIX)
+    assert len(mix_f) == len(mix_w) == n, (len(mix_f), len(mix_w), n)
+    out = {"wino_pre_mix": {
+        "traffic_bytes": 1024.0 * (2 * sum(mix_f) + sum(mix_w)),
+        "fetch_bytes_x2": 2048.0 * sum(mix_f), "write_bytes": 1024.0 * sum(mix_w),
+        "launches": n, "note": "one NCSN++ 128^2 forward's PRE-conv mix at B=64 (bench.WINO_MIX)"}}
+    up = lambda k: "upfirdn" in k
+    uf = load("p8_upfirdn", up)
+    uw = load("p9_upfirdn", up)
+    for i, (name, *_rest) in enumerate(bench.UPFIRDN_SHAPES):
+        f = sum(d["FETCH_SIZE"] for d in uf[3 * i:3 * i + 3]) / 3
+        w = sum(d["WRITE_SIZE"] for d in uw[3 * i:3 * i + 3]) / 3
+        out["upfirdn2d " + name] = {"traffic_bytes": 1024.0 * (2 * f + w),
+                                    "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w}
+    ns = lambda k: "k_fused" in k
+    nf = load("p5_ns", ns)
+    nw = load("p6_ns", ns)
+    f = sum(d["FETCH_SIZE"] for d in nf) / 3
+    w = sum(d["WRITE_SIZE"] for d in nw) / 3
+    out["ns_step full step B256 192^2"] = {"traffic_bytes": 1024.0 * (2 * f + w),
+                                            "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w,
+                                            "note": "both fused launches of one full step"}
+    out["_note"] = ("rocprofv3 --pmc passes (tools/gpu_pmc_r02.sh over tools/prof_r02.py); "
+                    "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB -> bytes")
+    json.dump(out, open(os.path.join(REPO, "profiles", "r02_pmc_traffic.json"), "w"), indent=1)
+    sq = {}
+    one = [d for d in load("p1_wino_one", wino)]
+    one2 = [d for d in load("p2_wino_one", wino)]
+    last = dict(one[-1]); last.update(one2[-1])
+    waves = last["_grid"] / 64
+    last["derived"] = {
+        "mfma_busy_frac_of_simd_cycles": last["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * last["GRBM_GUI_ACTIVE"] / 8),
+        "lds_bank_conflict_frac": last["SQ_LDS_BANK_CONFLICT"] / max(1.0, last["SQ_LDS_IDX_ACTIVE"]),
+        "wait_inst_any_frac": last["SQ_WAIT_INST_ANY"] / last["SQ_WAVE_CYCLES"],
+        "wait_any_frac": last["SQ_WAIT_ANY"] / last["SQ_WAVE_CYCLES"],
+        "valu_per_mfma": last["SQ_INSTS_VALU"] / last["SQ_INSTS_MFMA"],
+        "waves": waves}
+    sq["wino_pre_stats 128->128@128 B=16 (one dispatch)"] = last
+    nsq = load("p7_ns", ns)
+    sq["ns_step launches (3 full steps)"] = nsq
+    sq["_note"] = ("SQ_* wave counters in quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES (cycles, = 32 per "
+                   "v_mfma_f32_16x16x4_f32); GRBM_GUI_ACTIVE summed over the 8 XCDs; MFMA busy "
+                   "fraction = MFMA busy cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)")
+    json.dump(sq, open(os.path.join(REPO, "profiles", "r02_pmc_sq.json"), "w"), indent=1)
+    print(json.dumps({k: v.get("traffic_bytes") for k, v in out.items() if isinstance(v, dict)}, indent=1))
+    print(json.dumps(last["derived"], indent=1))
+
+
+if __name__ == "__main__":
+    main()
