@@ -220,7 +220,11 @@ int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w
 // HBM-bound stencil needs on MI355X.  All tap bookkeeping is compile-time: input row t of
 // the strip feeds output row r through vertical tap i = t*UP - r*DOWN, and output column oc
 // of a lane reads relative input column q = (oc*DOWN + j - P0) / UP.
-template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD = 0>
+// TAIL: the plane is one strip wide plus one column (odd widths 2^k + 1: the FIR pad(2, 2)
+// of conv_downsample_2d, 64 -> 65): the segment's last lane also produces the plane's last
+// column from the values it already holds, so a 65-wide row takes a 32-lane segment
+// instead of a half-idle 64-lane one.
+template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD = 0, bool TAIL = false>
 __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict__ x,
                                                          const float* __restrict__ kern,
                                                          float* __restrict__ out, int in_h,
@@ -253,11 +257,12 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
     for (int j = 0; j < 4; ++j)
       w[i][j] = (i < kh && j < kw) ? kern[(kh - 1 - i) * kw + (kw - 1 - j)] : 0.f;
 
-  float acc[R][NOC];
+  constexpr int NOCT = NOC + (TAIL ? 1 : 0);  // columns computed (the tail one on the last lane)
+  float acc[R][NOCT];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int oc = 0; oc < NOC; ++oc) acc[r][oc] = 0.f;
+    for (int oc = 0; oc < NOCT; ++oc) acc[r][oc] = 0.f;
 
   const float* xp = x + plane * in_h * in_w;
 #pragma unroll
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
       const int i = t * UP - r * DOWN;
       if (i < 0 || i >= 4) continue;
 #pragma unroll
-      for (int oc = 0; oc < NOC; ++oc) {
+      for (int oc = 0; oc < NOCT; ++oc) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int u = oc * DOWN + j - P0;
@@ -335,7 +340,19 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
     const int oy = oyb + r;
     float* orow = op + (int64_t)oy * out_w;
     if (oy < out_h) {
-      if constexpr (NOC == 4) {  // out_w % 4 == 0 (host check): 16-byte aligned quads
+      if constexpr (NOC == 4 && TAIL) {  // odd row pitch: the widest store the address allows
+        const int64_t e0 = (plane * out_h + oy) * (int64_t)out_w + oxl;  // element index
+        if ((e0 & 3) == 0) {
+          *reinterpret_cast<float4*>(orow + oxl) =
+              make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        } else if ((e0 & 1) == 0) {
+          *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[r][0], acc[r][1]);
+          *reinterpret_cast<float2*>(orow + oxl + 2) = make_float2(acc[r][2], acc[r][3]);
+        } else {
+#pragma unroll
+          for (int oc = 0; oc < 4; ++oc) orow[oxl + oc] = acc[r][oc];
+        }
+      } else if constexpr (NOC == 4) {  // out_w % 4 == 0 (host check): 16-byte aligned quads
         if (oxl + 3 < out_w) {
           *reinterpret_cast<float4*>(orow + oxl) =
               make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
@@ -355,21 +372,24 @@ __global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict_
       } else {
         if (oxl < out_w) orow[oxl] = acc[r][0];
       }
+      if constexpr (TAIL) {
+        if (sl == SEGW - 1) orow[out_w - 1] = acc[r][NOC];
+      }
     }
   }
 }
 
-template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD>
+template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD, bool TAIL = false>
 int launch_stream_seg(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                       int kh, int kw, int out_h, int out_w, hipStream_t st) {
   constexpr int NOC = NOCD > 0 ? NOCD : ((UP == 1 && DOWN == 2) ? 1 : 2);
-  const int strips_x = (int)bpk::ceil_div(out_w, SEGW * NOC);
+  const int strips_x = TAIL ? 1 : (int)bpk::ceil_div(out_w, SEGW * NOC);
   const int strips_y = (int)bpk::ceil_div(out_h, R);
   const int64_t n = (int64_t)major * strips_x * strips_y;
   if (n <= 0) return BPK_OK;
   const int64_t blocks = bpk::ceil_div(n, 4 * (64 / SEGW));
   BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
-  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R, SEGW, NOCD>), dim3((unsigned)blocks), dim3(256),
+  hipLaunchKernelGGL((upfirdn2d_stream<UP, DOWN, P0, R, SEGW, NOCD, TAIL>), dim3((unsigned)blocks), dim3(256),
                      0, st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, strips_x, strips_y, n);
   BPK_LAUNCH_CHECK("upfirdn2d_stream");
   return BPK_OK;
@@ -423,6 +443,45 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
     if (p0 == 2) return BPK_STREAM(1, 2, 2, 4);
   }
   if (up == 1 && down == 1) {
+    if (p0 == 2 && (out_w & 1) && kw == 4) {
+      // odd width 2^k + 1 (the FIR pad(2, 2) of conv_downsample_2d): a segment of
+      // (out_w - 1) / 2 lanes with the tail column on its last lane
+      const int lanes = (out_w - 1) / 2;
+      static const int rt = [] {
+        const char* e = getenv("BPK_UPFIRDN_RT");
+        return e ? atoi(e) : 4;
+      }();
+      // BPK_UPFIRDN_RT: 4 (default) / 8 = strip height with 4 columns per lane (16-byte row
+      // loads); 2 = 8 rows with 2 columns per lane.  [64,128,64,64] -> 65^2 on MI355X:
+      // 0.086 / 0.088 / 0.105 ms (39.8 / 38.8 / 32.6 % of HBM peak); before the tail path a
+      // half-idle 64-lane segment took 0.135 ms (25 %)
+#define BPK_TAIL2(SW) \
+  return (*rc = launch_stream_seg<1, 1, 2, 8, SW, 0, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true)
+#define BPK_TAIL4(SW, RR) \
+  return (*rc = launch_stream_seg<1, 1, 2, RR, SW, 4, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true)
+      const int lanes4 = (out_w - 1) / 4;
+      if (rt == 2) {
+        if (lanes == 64) BPK_TAIL2(64);
+        if (lanes == 32) BPK_TAIL2(32);
+        if (lanes == 16) BPK_TAIL2(16);
+        if (lanes == 8) BPK_TAIL2(8);
+      } else if ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && in_w % 4 == 0) {
+        if (rt == 4) {
+          if (lanes4 == 64) BPK_TAIL4(64, 4);
+          if (lanes4 == 32) BPK_TAIL4(32, 4);
+          if (lanes4 == 16) BPK_TAIL4(16, 4);
+          if (lanes4 == 8) BPK_TAIL4(8, 4);
+        }
+        if (lanes4 == 64) BPK_TAIL4(64, 8);
+        if (lanes4 == 32) BPK_TAIL4(32, 8);
+        if (lanes4 == 16) BPK_TAIL4(16, 8);
+        if (lanes4 == 8) BPK_TAIL4(8, 8);
+      }
+      if (lanes == 16) BPK_TAIL2(16);  // 33-wide
+      if (lanes == 8) BPK_TAIL2(8);    // 17-wide
+#undef BPK_TAIL2
+#undef BPK_TAIL4
+    }
     if (p0 == 1) return BPK_STREAM(1, 1, 1, 8);
     if (p0 == 2) return BPK_STREAM(1, 1, 2, 8);
   }

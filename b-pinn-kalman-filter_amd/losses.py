@@ -195,6 +195,65 @@ def _sync_grads(params, ctx):
         g.copy_(s)
 
 
+class GradBucketer:
+    """Gradient averaging overlapped with backward, for models whose backward DDP cannot
+    hook (the PINN step differentiates the networks twice, then calls backward()).
+
+    Parameters are grouped, in reverse registration order (roughly the order backward
+    produces their gradients), into buckets of ~bucket_mb; a post-accumulate-grad hook
+    counts the bucket's arrivals and, when the last one lands, flattens the bucket and
+    starts an asynchronous all-reduce (RCCL on its own stream over xGMI) while backward
+    keeps running.  finish() waits for the in-flight buckets, syncs the ones that never
+    completed (parameters without a gradient this step) with one coalesced call, and
+    divides by the world size -- the same values as _sync_grads.  A NaN on any rank
+    reaches every rank's averaged gradient, so the NaN-skip of the step functions
+    (reference losses.py:361-366) is taken by all ranks together."""
+
+    def __init__(self, params, ctx, bucket_mb=16.0):
+        self.ctx = ctx
+        self.params = [p for p in params if p.requires_grad]
+        self.buckets, cur, size = [], [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= bucket_mb * 2 ** 20:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.where = {id(p): i for i, b in enumerate(self.buckets) for p in b}
+        self.handles = [p.register_post_accumulate_grad_hook(self._arrived) for p in self.params]
+        self.reset()
+
+    def reset(self):
+        self.count = [0] * len(self.buckets)
+        self.works = {}
+
+    def _arrived(self, p):
+        i = self.where[id(p)]
+        self.count[i] += 1
+        if self.count[i] == len(self.buckets[i]):
+            grads = [q.grad for q in self.buckets[i]]
+            flat = torch._utils._flatten_dense_tensors(grads)
+            work = torch.distributed.all_reduce(flat, group=self.ctx.group, async_op=True)
+            self.works[i] = (work, flat, grads)
+
+    def finish(self):
+        n = self.ctx.world_size
+        for i, (work, flat, grads) in sorted(self.works.items()):
+            work.wait()
+            flat.div_(n)
+            for g, s in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                g.copy_(s)
+        rest = [p for i, b in enumerate(self.buckets) if i not in self.works for p in b]
+        _sync_grads(rest, self.ctx)
+        self.reset()
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+
+
 def _observe(config, operator, f):
     """inpainting measurement + Gaussian noise of variance config.inverse.variance."""
     return operator(f, keep_shape=True) + torch.randn_like(f) * config.inverse.variance ** 0.5
@@ -334,12 +393,16 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
         gstate["graph"].replay()
         return gstate["out"]
 
+    bucketer = [None]  # eager + sharded: gradient buckets all-reduced during backward
+
     def step_fn(state, operator, batch):
         model = state["model"]
         operator.next()
         if train:
             opt_flow, opt_pres = state["optimizer"]
             model.train()
+            if not graph and ctx is not None and ctx.enabled and bucketer[0] is None:
+                bucketer[0] = GradBucketer(model.parameters(), ctx)
             if graph:
                 loss, pinn_loss, data_loss = graph_forward_backward(model, operator, batch,
                                                                     opt_flow, opt_pres)
@@ -350,8 +413,10 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                 opt_pres.zero_grad()
                 loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
                 loss.backward()
-            params = list(model.parameters())
-            _sync_grads(params, ctx)
+            if bucketer[0] is not None:
+                bucketer[0].finish()  # buckets all-reduced while backward ran
+            else:
+                _sync_grads(list(model.parameters()), ctx)
             w = model.pressurenet.end[-1].weight
             if w.grad is not None and torch.isnan(w.grad).any():
                 print(">>> Nan Grad Detected <<<")

@@ -43,18 +43,32 @@ def simulate(model, begin, t_range=(0, 100), stride=1):
     return result, vel
 
 
-def step(model, begin, t_range=(0, 100), stride=1, replicas=256, device=None):
+def step(model, begin, t_range=(0, 100), stride=1, replicas=256, device=None, ctx=None,
+         compat=True):
     """ns_step rollout of `replicas` copies of snapshot t_range[0]; velocity channels are
-    swapped into (v, u) order as the reference does (simulator.py:52-53)."""
+    swapped into (v, u) order as the reference does (simulator.py:52-53).
+
+    ctx (dist.DistContext): batch-sharded over the ranks, no collective -- rank r advances
+    replicas [r * R, (r + 1) * R) with R = replicas / world and returns those.
+    compat=False: replicas are independent and the shards equal the single-process rollout
+    bit for bit.  compat=True (the reference's behaviour): update_velocity's unbind quirk
+    (op/ns_step.cpp:70) makes sample b advect velocity planes b and b + 1, i.e. samples
+    b / 2 and (b + 1) / 2, so the replicas diverge after the first step and a shard equals
+    the reference's own rollout of R replicas -- reproducing the single-process batch would
+    need every rank's velocities each step."""
     dev = device if device is not None else model.mask_u.device
     t0, _ = t_range
+    if ctx is not None and ctx.enabled:
+        if replicas % ctx.world_size:
+            raise ValueError(f"replicas {replicas} do not split over {ctx.world_size} ranks")
+        replicas //= ctx.world_size
     f = _prep(begin[0 + t0, 2:3], dev).repeat(replicas, 1, 1, 1)
     v = _prep(begin[0 + t0, 3:5], dev)
     v = torch.cat([v[:, 1:2], v[:, 0:1]], 1).repeat(replicas, 1, 1, 1)
     p = _prep(begin[0 + t0, 5:6], dev).repeat(replicas, 1, 1, 1)
     result, vel, pres = [], [], []
     for _ in torch.arange(*t_range, stride):
-        f, v, p = ns_step.full_step(f, v, p, dt, dx)
+        f, v, p = ns_step.full_step(f, v, p, dt, dx, compat=compat)
         result.append(f)
         vel.append(v)
         pres.append(p)

@@ -135,3 +135,119 @@ def test_ddp_train_step_matches_single_rank():
     diff = np.abs(two[0][1] - one)
     assert diff.max() <= 2 * 4e-5 + 1e-6
     assert (diff > 1e-5).mean() < 1e-4
+
+
+def _sim_worker(rank, world, port, compat, q):
+    try:
+        ctx = _setup(rank, world, port)
+        from pinn_kalman import simulator
+        rng = np.random.default_rng(0)
+        begin = np.zeros((2, 6, 200, 200), np.float32)
+        begin[:, 2] = rng.uniform(0.1, 1.0, (2, 200, 200))
+        begin[:, 3:5] = rng.uniform(0.05, 0.5, (2, 2, 200, 200)) * rng.choice([-1, 1], (2, 2, 200, 200))
+        begin[:, 5] = rng.normal(0, 0.01, (2, 200, 200))
+        res, vel, pres = simulator.step(None, begin, t_range=(0, 3), replicas=8,
+                                        device=torch.device("cuda:0"), ctx=ctx, compat=compat)
+        q.put((rank, [np.stack([r.cpu().numpy() for r in a]) for a in (res, vel, pres)], None))
+        if world > 1:
+            torch.distributed.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_sharded_simulator_equals_single_process_bit_for_bit():
+    """pinn_kalman.simulator.step(ctx=...): rank r rolls replicas [4r, 4r + 4) of 8, no
+    collective.  compat=False (independent replicas): the shards equal the single-process
+    rollout exactly.  compat=True: the reference's unbind quirk couples sample b to velocity
+    planes b, b + 1 (samples b / 2 ...), so a shard reproduces the reference run of its own
+    R replicas -- the single-process rollout at replicas = R -- bit for bit."""
+    one = _run(_sim_worker, 1, False)[0][1]
+    two = _run(_sim_worker, 2, False)
+    for k in range(3):
+        both = np.concatenate([two[0][1][k], two[1][1][k]], 1)  # [steps, replicas, ...]
+        np.testing.assert_array_equal(both, one[k])
+    two_c = _run(_sim_worker, 2, True)
+    eight = _run(_sim_worker, 1, True)[0][1]  # replicas=8 in one process
+    for k in range(3):
+        # sample b < 4 only ever reads planes of samples <= (b + 1) / 2 < 4: the first shard
+        # equals the first four replicas of the 8-replica rollout, and both shards (same
+        # initial replicas) are identical
+        np.testing.assert_array_equal(two_c[0][1][k], eight[k][:, :4])
+        np.testing.assert_array_equal(two_c[1][1][k], two_c[0][1][k])
+
+
+def _pinn_worker(rank, world, port, nan_rank, q):
+    try:
+        ctx = _setup(rank, world, port)
+        import losses
+        from configs.pinn import pinn_pde
+        from conftest import build_pinn_weights, load_golden, small_config
+        from inverse.operators import InpaintOperator
+        from models.ema import ExponentialMovingAverage
+        from pinn_kalman.pinn import PINN
+        dev = torch.device("cuda:0")
+        c = small_config(pinn_pde.get_config)
+        m = build_pinn_weights(PINN, c).to(dev)
+        c.device = dev
+        c.inverse.variance = 0.0  # the measurement noise draws then do not matter
+        d = load_golden("pinn_step.npz")
+        B = 2 // world
+        sl = slice(rank * B, (rank + 1) * B)
+        T = lambda k: torch.tensor(d[k][sl].copy(), device=dev)
+        batch = [T("f1"), T("f2"), T("x").requires_grad_(), T("y").requires_grad_(),
+                 T("t").requires_grad_(), T("target")]
+        if rank == nan_rank:  # the pressure target: reaches PressureNet's last conv
+            batch[5][0, 2, 3, 3] = float("nan")
+        op = InpaintOperator(mask=[torch.tensor(d["mask"][sl].copy(), device=dev)])
+        em = ExponentialMovingAverage(m.parameters(), decay=c.model.ema_rate)
+        opt_f = losses.get_optimizer(c, m.flownet.parameters())
+        opt_p = losses.get_optimizer(c, m.pressurenet.parameters(), 0.001)
+        state = dict(optimizer=(opt_f, opt_p), model=m, ema=em, step=50)
+        grads = {}
+        for opt, pref in ((opt_f, "flownet."), (opt_p, "pressurenet.")):
+            net = getattr(m, pref[:-1])
+
+            def capture(*a, _real=opt.step, _net=net, _pref=pref, **k):
+                for kk, p in _net.named_parameters():
+                    if p.grad is not None:
+                        grads[_pref + kk] = p.grad.detach().reshape(-1).cpu().numpy()
+                return _real(*a, **k)
+
+            opt.step = capture
+        p0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+        step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
+                                          ctx=ctx if world > 1 else None)
+        losses_out = step_fn(state, op, tuple(batch))
+        p1 = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+        g = np.concatenate([grads[k] for k in sorted(grads)]) if grads else None
+        q.put((rank, (state["step"], g, p1, p0, [float(v) for v in losses_out]), None))
+        if world > 1:
+            torch.distributed.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_sharded_pinn_step_matches_single_rank():
+    """get_pinn_step_fn(ctx=...) on 2 ranks x 1 sample == 1 rank x 2 samples: the
+    bucketed, backward-overlapped gradient average equals the full-batch gradient (each
+    rank's loss is the mean over its shard; fp32 reduction order differs)."""
+    (_, (s1, g1, p1, _, l1), _), = _run(_pinn_worker, 1, -1)
+    two = _run(_pinn_worker, 2, -1)
+    (s_a, g_a, pa, _, la), (s_b, g_b, pb, _, lb) = two[0][1], two[1][1]
+    assert s1 == s_a == s_b == 51
+    np.testing.assert_array_equal(g_a, g_b)
+    np.testing.assert_array_equal(pa, pb)  # replicas stay identical
+    assert np.abs(g_a - g1).max() <= 2e-3 * np.abs(g1).max()
+    np.testing.assert_allclose(0.5 * (la[0] + lb[0]), l1[0], rtol=2e-4)
+
+
+def test_nan_on_one_rank_makes_every_rank_skip():
+    """A NaN in rank 1's pressure target: its gradient reaches every rank through the all-reduce,
+    so both ranks take the reference's NaN skip (losses.py:361-366) -- no optimizer step,
+    no EMA update, step counter unchanged, parameters unchanged on both."""
+    two = _run(_pinn_worker, 2, 1)
+    for _, (step, g, p1, p0, _), _ in two:
+        assert step == 50
+        np.testing.assert_array_equal(p1, p0)

@@ -809,3 +809,19 @@ def test_grad_pruning_input_derivatives_then_parameter_gradients(hip):
     ref = run(lambda t, w, b: F.conv2d(t, w, b, padding=1), lambda t, w: F.conv2d(t, w))
     for a, r in zip(got, ref):
         assert (a - r).abs().max().item() <= 2e-5 * max(1e-6, r.abs().max().item())
+
+
+@pytest.mark.parametrize("hw", [(16, 16), (32, 32), (64, 64), (128, 128), (20, 64), (64, 16)])
+def test_upfirdn2d_fir_pad2_odd_width_tail_path(hip, hw):
+    """FIR-only pad(2, 2) (conv_downsample_2d's FIR, op/upfirdn2d.py:145) on 2^k-wide planes:
+    the 2^k + 1 output width takes the streaming kernel's tail-column path; vs the oracle."""
+    from op import upfirdn2d
+    from oracle.upfirdn2d_ref import upfirdn2d_np
+    H, W = hw
+    g = torch.Generator().manual_seed(H * 1000 + W)
+    x = torch.randn(3, 5, H, W, generator=g)
+    k = np.outer([1, 3, 3, 1], [1, 3, 3, 1]).astype(np.float32) / 64
+    y = upfirdn2d(x.to(hip), torch.tensor(k, device=hip), pad=(2, 2)).cpu().numpy()
+    ref = upfirdn2d_np(x.numpy(), k, (1, 1), (1, 1), (2, 2, 2, 2))
+    assert y.shape == ref.shape == (3, 5, H + 1, W + 1)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-6)
