@@ -121,7 +121,107 @@ def grid_sample_2d(input, grid, padding_mode="zeros", align_corners=True):
     return _GridSample2dForward.apply(input, grid, padding_mode, align_corners)
 
 
+def _fns3(dtype):
+    if dtype == torch.float32:
+        return (lib.bpk_grid_sample3d_fwd_f32, lib.bpk_grid_sample3d_bwd_f32,
+                lib.bpk_grid_sample3d_grad2_f32)
+    if dtype == torch.float64:
+        return (lib.bpk_grid_sample3d_fwd_f64, lib.bpk_grid_sample3d_bwd_f64,
+                lib.bpk_grid_sample3d_grad2_f64)
+    raise RuntimeError(f"grid_sample_3d: unsupported dtype {dtype}")
+
+
+def _geom3(input, grid):
+    N, C, D, H, W = input.shape
+    return N, C, D, H, W, grid.shape[1], grid.shape[2], grid.shape[3]
+
+
+def grid_sample3d_fwd_raw(input, grid, padding_mode: int, align_corners: bool):
+    require_hip(input, grid, what="grid_sample_3d")
+    input, grid = input.contiguous(), grid.contiguous()
+    N, C, D, H, W, Do, Ho, Wo = _geom3(input, grid)
+    out = torch.empty((N, C, Do, Ho, Wo), device=input.device, dtype=input.dtype)
+    check(_fns3(input.dtype)[0](input.data_ptr(), grid.data_ptr(), out.data_ptr(), N, C, D, H, W,
+                                Do, Ho, Wo, padding_mode, int(align_corners),
+                                stream_ptr(input.device)), "grid_sample3d_fwd")
+    return out
+
+
+def grid_sample3d_bwd_raw(grad_out, input, grid, padding_mode, align_corners):
+    grad_out, input, grid = grad_out.contiguous(), input.contiguous(), grid.contiguous()
+    N, C, D, H, W, Do, Ho, Wo = _geom3(input, grid)
+    gi = torch.zeros_like(input)
+    gg = torch.empty_like(grid)
+    check(_fns3(input.dtype)[1](grad_out.data_ptr(), input.data_ptr(), grid.data_ptr(),
+                                gi.data_ptr(), gg.data_ptr(), N, C, D, H, W, Do, Ho, Wo,
+                                padding_mode, int(align_corners), stream_ptr(input.device)),
+          "grid_sample3d_bwd")
+    return gi, gg
+
+
+def grid_sample3d_grad2_raw(g2_input, g2_grid, grad_out, input, grid, padding_mode,
+                            align_corners):
+    g2_input, g2_grid, grad_out, input, grid = (
+        t.contiguous() for t in (g2_input, g2_grid, grad_out, input, grid))
+    N, C, D, H, W, Do, Ho, Wo = _geom3(input, grid)
+    ggo = torch.empty_like(grad_out)
+    gi = torch.zeros_like(input)
+    gg = torch.empty_like(grid)
+    check(_fns3(input.dtype)[2](g2_input.data_ptr(), g2_grid.data_ptr(), grad_out.data_ptr(),
+                                input.data_ptr(), grid.data_ptr(), ggo.data_ptr(), gi.data_ptr(),
+                                gg.data_ptr(), N, C, D, H, W, Do, Ho, Wo, padding_mode,
+                                int(align_corners), stream_ptr(input.device)),
+          "grid_sample3d_grad2")
+    return ggo, gi, gg
+
+
+class _GridSample3dForward(torch.autograd.Function):
+    """reference op/grid_sample.py:79-99"""
+
+    @staticmethod
+    def forward(ctx, input, grid, padding_mode="zeros", align_corners=True):
+        assert input.ndim == 5 and grid.ndim == 5
+        assert input.shape[0] == grid.shape[0] and grid.shape[4] == 3
+        pm = _PADDING[padding_mode]
+        out = grid_sample3d_fwd_raw(input, grid, pm, align_corners)
+        ctx.save_for_backward(input, grid)
+        ctx.padding_mode, ctx.align_corners = pm, align_corners
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, grid = ctx.saved_tensors
+        gi, gg = _GridSample3dBackward.apply(grad_output, input, grid, ctx.padding_mode,
+                                             ctx.align_corners)
+        return gi, gg, None, None
+
+
+class _GridSample3dBackward(torch.autograd.Function):
+    """reference op/grid_sample.py:102-131: first backward (aten::grid_sampler_3d_backward
+    there), whose own backward is the double-backward kernel (grad2_3d)"""
+
+    @staticmethod
+    def forward(ctx, grad_output, input, grid, padding_mode=0, align_corners=True):
+        gi, gg = grid_sample3d_bwd_raw(grad_output, input, grid, padding_mode, align_corners)
+        ctx.save_for_backward(grad_output, input, grid)
+        ctx.padding_mode, ctx.align_corners = padding_mode, align_corners
+        return gi, gg
+
+    @staticmethod
+    def backward(ctx, g2_input, g2_grid):
+        grad_output, input, grid = ctx.saved_tensors
+        if g2_input is None:
+            g2_input = torch.zeros_like(input)
+        if g2_grid is None:
+            g2_grid = torch.zeros_like(grid)
+        ggo, gi, gg = grid_sample3d_grad2_raw(g2_input, g2_grid, grad_output, input, grid,
+                                              ctx.padding_mode, ctx.align_corners)
+        return ggo, gi, gg, None, None
+
+
 def grid_sample_3d(input, grid, padding_mode="zeros", align_corners=True):
-    """The reference ships a 3-D variant (op/grid_sample.py:19-22) with no caller on the
-    hot path; not built in this round."""
-    raise NotImplementedError("grid_sample_3d is not part of the MI355X hot path yet")
+    """Trilinear grid sampling of [N, C, D, H, W] at grid [N, Do, Ho, Wo, 3] (x, y, z),
+    twice differentiable (reference op/grid_sample.py:19-22; no caller on the hot path)."""
+    assert padding_mode in ["zeros", "border"]
+    require_hip(input, grid, what="grid_sample_3d")
+    return _GridSample3dForward.apply(input, grid, padding_mode, align_corners)

@@ -19,6 +19,27 @@ import torch.nn as nn
 from models.flownet import FlowNet, PressureNet, project
 
 
+def fd_residual_mse(u, v, p, u_t, v_t, h, Re):
+    """MSEs of the x/y momentum and mass residuals with spatial derivatives on the ns_step
+    stencil (reference diff_x / diff_y, op/ns_step_kernel.cu:50-75): u, v, p [B, 1, H, W],
+    u_t, v_t [B], grid spacing h.  Second derivatives are the stencil applied twice."""
+    from op.ns_step import stencil_gradient
+    u_x, u_y = stencil_gradient(u, h)
+    v_x, v_y = stencil_gradient(v, h)
+    p_x, p_y = stencil_gradient(p, h)
+    u_xx = stencil_gradient(u_x, h)[0]
+    u_yy = stencil_gradient(u_y, h)[1]
+    v_xx = stencil_gradient(v_x, h)[0]
+    v_yy = stencil_gradient(v_y, h)[1]
+    u_t = u_t[:, None, None, None]
+    v_t = v_t[:, None, None, None]
+    nu = 1.0 / Re
+    res_x = u_t + (u * u_x + v * u_y) + p_x - nu * (u_xx + u_yy)
+    res_y = v_t + (u * v_x + v * v_y) + p_y - nu * (v_xx + v_yy)
+    res_mass = u_x + v_y
+    return (res_x ** 2).mean() + (res_y ** 2).mean() + (res_mass ** 2).mean()
+
+
 def get_model(config):
     arch = config.model.arch
     if arch == "flownet":
@@ -86,7 +107,6 @@ class PINN(nn.Module):
         autograd derivatives w.r.t. t as in `equation_mse`.  `h` is the grid spacing
         (default: the mean spacing of the x coordinate channel along the width).
         Differentiable to any order (the stencil's backward is its adjoint kernel)."""
-        from op.ns_step import stencil_gradient
         u = (self.mask_u * flow).sum(dim=1).unsqueeze(1)
         v = (self.mask_v * flow).sum(dim=1).unsqueeze(1)
         p = pres
@@ -94,22 +114,7 @@ class PINN(nn.Module):
             h = float((x[:, :, :, -1] - x[:, :, :, 0]).mean()) / (x.shape[-1] - 1)
         u_t = torch.autograd.grad(u.sum(), t, create_graph=True, retain_graph=True)[0]
         v_t = torch.autograd.grad(v.sum(), t, create_graph=True, retain_graph=True)[0]
-        u_x, u_y = stencil_gradient(u, h)
-        v_x, v_y = stencil_gradient(v, h)
-        p_x, p_y = stencil_gradient(p, h)
-        u_xx = stencil_gradient(u_x, h)[0]
-        u_yy = stencil_gradient(u_y, h)[1]
-        v_xx = stencil_gradient(v_x, h)[0]
-        v_yy = stencil_gradient(v_y, h)[1]
-        u_t = u_t[:, None, None, None]
-        v_t = v_t[:, None, None, None]
-        nu = 1.0 / Re
-        res_x = u_t + (u * u_x + v * u_y) + p_x - nu * (u_xx + u_yy)
-        res_y = v_t + (u * v_x + v * v_y) + p_y - nu * (v_xx + v_yy)
-        res_mass = u_x + v_y
-        mse = torch.nn.MSELoss()
-        zeros = torch.zeros_like(x)
-        return mse(res_x, zeros) + mse(res_y, zeros) + mse(res_mass, zeros)
+        return fd_residual_mse(u, v, p, u_t, v_t, h, Re)
 
     def step(self, ft, u):
         """Advance a field by the predicted flow (reference pinn.py:113-114)."""

@@ -115,6 +115,38 @@ int bpk_grid_sample2d_grad2_f64(const double* g2_input, const double* g2_grid,
                                 int align_corners, void* stream);
 
 /* ------------------------------------------------------------------------- *
+ * grid_sample_3d (trilinear) -- replaces F.grid_sample on 5-D tensors and
+ * aten::grid_sampler_3d_backward as op/grid_sample.py:79-113 calls them, and
+ * gridsample_grad2.grad2_3d (op/grid_sample.cpp:42-57, op/grid_sample_kernel.cu:212-533,
+ * host 601-666).  input [N, C, D, H, W], grid [N, Do, Ho, Wo, 3] (x, y, z), contiguous;
+ * same output conventions as the 2-D entries (grad_input zero-filled by the caller).
+ * ------------------------------------------------------------------------- */
+int bpk_grid_sample3d_fwd_f32(const float* input, const float* grid, float* out, int N, int C,
+                              int D, int H, int W, int Do, int Ho, int Wo, int padding_mode,
+                              int align_corners, void* stream);
+int bpk_grid_sample3d_bwd_f32(const float* grad_out, const float* input, const float* grid,
+                              float* grad_input, float* grad_grid, int N, int C, int D, int H,
+                              int W, int Do, int Ho, int Wo, int padding_mode, int align_corners,
+                              void* stream);
+int bpk_grid_sample3d_grad2_f32(const float* g2_input, const float* g2_grid, const float* grad_out,
+                                const float* input, const float* grid, float* grad_grad_out,
+                                float* grad_input, float* grad_grid, int N, int C, int D, int H,
+                                int W, int Do, int Ho, int Wo, int padding_mode, int align_corners,
+                                void* stream);
+int bpk_grid_sample3d_fwd_f64(const double* input, const double* grid, double* out, int N, int C,
+                              int D, int H, int W, int Do, int Ho, int Wo, int padding_mode,
+                              int align_corners, void* stream);
+int bpk_grid_sample3d_bwd_f64(const double* grad_out, const double* input, const double* grid,
+                              double* grad_input, double* grad_grid, int N, int C, int D, int H,
+                              int W, int Do, int Ho, int Wo, int padding_mode, int align_corners,
+                              void* stream);
+int bpk_grid_sample3d_grad2_f64(const double* g2_input, const double* g2_grid,
+                                const double* grad_out, const double* input, const double* grid,
+                                double* grad_grad_out, double* grad_input, double* grad_grid,
+                                int N, int C, int D, int H, int W, int Do, int Ho, int Wo,
+                                int padding_mode, int align_corners, void* stream);
+
+/* ------------------------------------------------------------------------- *
  * ns_step: explicit 2-D incompressible-flow step on B planes.
  * Memory convention follows the reference exactly (op/ns_step_kernel.cu:30-37):
  * a plane is addressed as field[y * nx + x] with nx = tensor.size(2) (the

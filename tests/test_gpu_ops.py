@@ -825,3 +825,50 @@ def test_upfirdn2d_fir_pad2_odd_width_tail_path(hip, hw):
     ref = upfirdn2d_np(x.numpy(), k, (1, 1), (1, 1), (2, 2, 2, 2))
     assert y.shape == ref.shape == (3, 5, H + 1, W + 1)
     np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------ grid_sample 3-D
+@pytest.mark.parametrize("pm", ["zeros", "border"])
+@pytest.mark.parametrize("ac", [True, False])
+def test_grid_sample_3d_fwd_bwd_vs_aten_cpu(hip, pm, ac):
+    from op.grid_sample import grid_sample_3d
+    torch.manual_seed(11)
+    inp = torch.randn(2, 3, 5, 6, 7)
+    grid = torch.rand(2, 4, 3, 5, 3) * 2.4 - 1.2
+    gout = torch.randn(2, 3, 4, 3, 5)
+    ri, rg = inp.clone().requires_grad_(True), grid.clone().requires_grad_(True)
+    ref = F.grid_sample(ri, rg, mode="bilinear", padding_mode=pm, align_corners=ac)
+    ref.backward(gout)
+    gi, gg = inp.to(hip).requires_grad_(True), grid.to(hip).requires_grad_(True)
+    out = grid_sample_3d(gi, gg, pm, ac)
+    out.backward(gout.to(hip))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), atol=1e-5)
+    np.testing.assert_allclose(gi.grad.cpu().numpy(), ri.grad.numpy(), atol=1e-5)
+    np.testing.assert_allclose(gg.grad.cpu().numpy(), rg.grad.numpy(), atol=1e-4)
+
+
+@pytest.mark.parametrize("pm", [0, 1])
+def test_grid_sample_3d_grad2_vs_oracle(hip, pm):
+    """vs oracle/grid_sample_ref.grad3 (restatement of op/grid_sample_kernel.cu:212-533,
+    pinned by finite differences of ATen's first backward, tests/test_grid_sample3d_host.py)"""
+    from op.grid_sample import grid_sample3d_grad2_raw
+    torch.manual_seed(12)
+    d = torch.float64
+    inp = torch.randn(2, 3, 4, 5, 6, dtype=d)
+    grid = torch.rand(2, 3, 2, 4, 3, dtype=d) * 2.4 - 1.2
+    gout = torch.randn(2, 3, 3, 2, 4, dtype=d)
+    g2i, g2g = torch.randn_like(inp), torch.randn_like(grid)
+    ref = grid_sample_ref.grad3(g2i, g2g, gout, inp, grid, pm, True)
+    got = grid_sample3d_grad2_raw(*(t.to(hip) for t in (g2i, g2g, gout, inp, grid)), pm, True)
+    for a, r in zip(got, ref):
+        np.testing.assert_allclose(a.cpu().numpy(), r.numpy(), rtol=1e-10, atol=1e-10)
+
+
+def test_grid_sample_3d_double_backward_gradgradcheck(hip):
+    from op.grid_sample import grid_sample_3d
+    torch.manual_seed(13)
+    inp = torch.randn(1, 2, 3, 4, 4, dtype=torch.float64, device=hip, requires_grad=True)
+    grid = (torch.rand(1, 2, 3, 2, 3, dtype=torch.float64, device=hip) * 1.6 - 0.8).requires_grad_(True)
+    f = lambda a, g: grid_sample_3d(a, g, "border", True)
+    assert torch.autograd.gradcheck(f, (inp, grid))
+    assert torch.autograd.gradgradcheck(f, (inp, grid))

@@ -193,7 +193,7 @@ def test_stencil_gradient_forward_exact_and_adjoint(hip):
     gx = torch.randn_like(fx)
     gy = torch.randn_like(fy)
     (gf,) = torch.autograd.grad((fx * gx).sum() + (fy * gy).sum(), ft, create_graph=True)
-    lhs = float((fx.double() * gx.double()).sum() + (fy.double() * gy.double()).sum())
+    lhs = float((fx.detach().double() * gx.double()).sum() + (fy.detach().double() * gy.double()).sum())
     rhs = float((gf.double() * ft.double()).sum())
     assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
     # d/df of sum(Dx(Dx f) * w) through the stencil twice == Dx^T Dx^T w
@@ -258,3 +258,52 @@ def test_pinn_step_graph_replay_matches_eager(hip):
     # turns last-bit differences of near-zero gradients (MIOpen's backward kernels are not
     # bitwise reproducible) into +-lr steps
     assert ((g1 - g2).norm() / g1.norm()).item() <= 1e-3
+
+
+def test_ns_dynamics_bit_exact_vs_oracle(hip):
+    """UKF NSDynamics.forward (reference ukf_utils.py:95-119) on the fused ns_step == the
+    oracle's unpatch -> three C ns_step ops (compat quirk on) -> patch, bit for bit; the
+    process covariance is the reference's 1e-8 I per state row."""
+    from configs.pinn import pinn_pde
+    from oracle import pinn_fd_ref
+    from pinn_kalman.ukf_utils import NSDynamics, patch
+    c = pinn_pde.get_config()
+    assert c.kf.patch_size == 8 and c.data.image_size == 64
+    rng = np.random.default_rng(4)
+    B, n = 2, 64
+    fields = np.concatenate([
+        rng.uniform(0.1, 1.0, (B, 1, n, n)),
+        rng.uniform(0.05, 0.5, (B, 2, n, n)) * rng.choice([-1, 1], (B, 2, n, n)),
+        rng.normal(0, 0.01, (B, 1, n, n))], 1).astype(np.float32)
+    states = patch(torch.from_numpy(fields), 8).numpy()
+    dyn = NSDynamics(c)
+    st, cov = dyn(torch.from_numpy(states).to(hip), None)
+    ref_st, ref_cov = pinn_fd_ref.ns_dynamics(states, 8, 64)
+    np.testing.assert_array_equal(st.cpu().numpy(), ref_st)
+    np.testing.assert_array_equal(cov.cpu().numpy(), ref_cov)
+
+
+def test_stencil_residual_matches_cpu_oracle(hip):
+    """PINN.equation_mse_fd (the residual on the ns_step stencil kernel) == the float64
+    oracle residual of the same fields and time derivatives (oracle/pinn_fd_ref.py);
+    float32 vs float64: 1e-5 relative.  The fields and u_t / v_t come from the build's
+    forward (checked against the reference elsewhere); the oracle recomputes every
+    spatial derivative and the residual."""
+    from oracle import pinn_fd_ref
+    d = load_golden("pinn_fwd.npz")
+    c, m = _model(hip)
+    m.train()
+    T = lambda k: torch.tensor(d[k], device=hip)
+    x, y, t = (T(k).requires_grad_() for k in ("x", "y", "t"))
+    flows, pres = m(T("f1"), T("f2"), x, y, t)
+    h = float((x[:, :, :, -1] - x[:, :, :, 0]).mean()) / (x.shape[-1] - 1)
+    for Re in (50.0, 1e7):
+        val = m.equation_mse_fd(x, y, t, flows[-1], pres, Re, h=h)
+        u = (m.mask_u * flows[-1]).sum(1, keepdim=True)
+        v = (m.mask_v * flows[-1]).sum(1, keepdim=True)
+        u_t = torch.autograd.grad(u.sum(), t, retain_graph=True)[0]
+        v_t = torch.autograd.grad(v.sum(), t, retain_graph=True)[0]
+        ref = pinn_fd_ref.fd_residual_mse(u.detach().cpu().numpy(), v.detach().cpu().numpy(),
+                                          pres.detach().cpu().numpy(), u_t.cpu().numpy(),
+                                          v_t.cpu().numpy(), h, Re)
+        assert abs(float(val) - ref) <= 1e-5 * abs(ref), (Re, float(val), ref)
