@@ -64,3 +64,21 @@ def test_product_ops_refuse_cpu_tensors():
         ns_step.update_pressure(x, torch.zeros(1, 2, 8, 8), 0.1, 0.1)
     with pytest.raises(RuntimeError, match="HIP"):
         group_norm_act(torch.zeros(1, 4, 4, 4), torch.nn.GroupNorm(2, 4))
+
+
+def test_reference_extension_names_are_dispatcher_ops():
+    """torch.ops.<extension>.<name> exist for every reference pybind entry point
+    (op/upfirdn2d.cpp:12-22, op/fused_bias_act.cpp:11-20, op/grid_sample.cpp:26-57,
+    op/ns_step.cpp:45-107), with no CPU kernel: a CPU tensor fails loudly."""
+    import pytest
+    import torch
+    import op  # noqa: F401
+    names = [("upfirdn2d_op", "upfirdn2d"), ("fused", "fused_bias_act"),
+             ("gridsample_grad2", "grad2_2d"), ("gridsample_grad2", "grad2_3d"),
+             ("ns_step_forward", "update_density"), ("ns_step_forward", "update_velocity"),
+             ("ns_step_forward", "update_pressure"), ("correlation", "forward")]
+    for ns, name in names:
+        assert hasattr(getattr(torch.ops, ns), name), (ns, name)
+    with pytest.raises((NotImplementedError, RuntimeError)):
+        torch.ops.upfirdn2d_op.upfirdn2d(torch.zeros(1, 4, 4, 1), torch.ones(2, 2), 1, 1, 1, 1,
+                                         0, 0, 0, 0)

@@ -872,3 +872,31 @@ def test_grid_sample_3d_double_backward_gradgradcheck(hip):
     f = lambda a, g: grid_sample_3d(a, g, "border", True)
     assert torch.autograd.gradcheck(f, (inp, grid))
     assert torch.autograd.gradgradcheck(f, (inp, grid))
+
+
+def test_dispatcher_ops_equal_the_op_wrappers(hip):
+    """torch.ops.<reference extension>.* (op/torch_ops.py) run the same kernels as op/*."""
+    import op
+    from op import ns_step
+    from op.grid_sample import grid_sample2d_grad2_raw
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(2, 3, 16, 16, generator=g).to(hip)
+    k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32, device=hip)
+    a = torch.ops.upfirdn2d_op.upfirdn2d(x.reshape(6, 16, 16, 1), k, 1, 1, 2, 2, 1, 1, 1, 1)
+    assert torch.equal(a.reshape(2, 3, 8, 8), op.upfirdn2d(x, k, down=2, pad=(1, 1)))
+    b = torch.randn(3, generator=g).to(hip)
+    e = torch.empty(0, device=hip)
+    assert torch.equal(torch.ops.fused.fused_bias_act(x, b, e, 3, 0, 0.2, 2 ** 0.5),
+                       op.fused_leaky_relu(x, b))
+    f = torch.rand(2, 1, 16, 16, generator=g).to(hip) + 0.1
+    v = (torch.rand(2, 2, 16, 16, generator=g).to(hip) + 0.05)
+    p = torch.randn(2, 1, 16, 16, generator=g).to(hip) * 0.01
+    assert torch.equal(torch.ops.ns_step_forward.update_velocity(v, p, 0.0025, 0.005),
+                       ns_step.update_velocity(v, p, 0.0025, 0.005))
+    inp = torch.randn(2, 3, 5, 6, generator=g, dtype=torch.float64).to(hip)
+    grid = (torch.rand(2, 4, 3, 2, generator=g, dtype=torch.float64) * 2 - 1).to(hip)
+    go = torch.randn(2, 3, 4, 3, generator=g, dtype=torch.float64).to(hip)
+    g2i, g2g = torch.randn_like(inp), torch.randn_like(grid)
+    for u, w in zip(torch.ops.gridsample_grad2.grad2_2d(g2i, g2g, go, inp, grid, True, True),
+                    grid_sample2d_grad2_raw(g2i, g2g, go, inp, grid, 1, True)):
+        assert torch.allclose(u, w, rtol=0, atol=1e-12)
