@@ -376,6 +376,9 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                 l3 = loss_fn(model, operator, gstate["batch"])
                 l3[0].backward()
             cur.wait_stream(side)
+            # drop the warm-up graph: its AccumulateGrad nodes (created on the side stream)
+            # would otherwise be reused by the capture, on another stream
+            del l3
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for p in model.parameters():
@@ -384,7 +387,10 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                 out = loss_fn(model, operator, gstate["batch"])
                 out[0].backward()
             operator.mask = real_mask
-            gstate["graph"], gstate["out"] = g, out
+            # detached views of the static outputs: replays rewrite them in place, and no
+            # autograd graph outlives the capture
+            gstate["graph"], gstate["out"] = g, tuple(o.detach() for o in out)
+            del out
         with torch.no_grad():
             for s_, t in zip(gstate["batch"], batch):
                 if s_ is not t:
@@ -408,6 +414,9 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                                                                     opt_flow, opt_pres)
                 if gstate["eager"] <= 2 and "graph" not in gstate:
                     loss.backward()
+                # no graph kept alive by the caller's reference to the losses (AccumulateGrad
+                # nodes of an eager step must not survive into the capture)
+                loss, pinn_loss, data_loss = loss.detach(), pinn_loss.detach(), data_loss.detach()
             else:
                 opt_flow.zero_grad()
                 opt_pres.zero_grad()
