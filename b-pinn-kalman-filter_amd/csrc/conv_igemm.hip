@@ -1,0 +1,504 @@
+// General 2-D convolution (any kernel size, stride, zero padding; groups = 1, dilation = 1)
+// as implicit GEMM on the f32-input MFMA (v_mfma_f32_16x16x4_f32), NCHW fp32, gfx950.
+//
+// The Winograd kernel (conv_winograd.hip) covers the score networks' big 3x3 / stride-1
+// convs; everything else the networks run -- the PINN's convs at 2^2..8^2 and with Cin not a
+// multiple of 8 (FlowNet's 49- and 2f+2-channel inputs), every stride-2 conv, the CIFAR nets'
+// 8^2 / 4^2 levels, the ConvTranspose2d layers (PressureNet up path, FlowNet flow upsample) --
+// ran on MIOpen (plus its NHWC transposes and per-call host search).  One kernel family
+// covers all three products of a conv:
+//
+//   MODE 0  forward        C[co][p]      = sum_{ci,r,s} w[co][ci][r][s] x[n][ci][oy s_h - p_h + r][ox s_w - p_w + s]
+//                          (p = (n, oy, ox) over the whole batch: small images do not
+//                          starve the grid)
+//   MODE 1  backward-data  C[ci][p_in]   = sum_{co,r,s} w[co][ci][r][s] gy[n][co][oy][ox]
+//                          with oy = (iy + p_h - r) / s_h when that divides exactly (the
+//                          conv transpose; also ConvTranspose2d's forward)
+//   MODE 2  weight grad    C[co][(ci,r,s)] = sum_p gy[n][co][oy][ox] x[n][ci][iy][ix], plus
+//                          one extra column of ones: the bias gradient sum_p gy[co][p]
+//
+// Tile: 64 x 64 (or, when those alone fill the chip, 128 x 128) outputs per workgroup (4
+// waves, 2 x 2 of 32 x 32 / 64 x 64, each 2 x 2 / 4 x 4 MFMA blocks),
+// K in chunks of 16 staged through double-buffered LDS (operands gathered with the
+// convolution's index arithmetic and zero padding; the next chunk's global loads are in
+// flight while the current chunk's 16 MFMAs per wave run).  Split-K over grid.z when the
+// output tiles alone cannot fill the chip (tiny images, the weight gradient's long pixel
+// sum): partials go to a workspace and a second kernel adds them in a fixed order, so
+// results are deterministic (no atomics).
+#include "bpk_common.h"
+
+#include <algorithm>
+
+namespace {
+
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int BK = 16;
+
+// n / d for 0 <= n < 2^31 by multiply-high and shift (d > 0 fixed per launch): the runtime
+// divisors (pixels per image, row width, stride, generic tap counts) would otherwise cost a
+// ~40-instruction integer division per gathered element
+struct FDiv {
+  unsigned d, m, s;
+};
+FDiv make_fdiv(unsigned d) {
+  unsigned s = 0;
+  while ((1u << s) < d) ++s;
+  const uint64_t m = ((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1;
+  return FDiv{d, (unsigned)m, s};
+}
+__device__ inline int fdiv(int n, const FDiv& f) {
+  return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.s);
+}
+
+struct IgGeo {
+  int N, Cin, H, W, Cout, Ho, Wo, KH, KW, sh, sw, ph, pw;
+  int M, Ncol, K;  // GEMM shape
+  int KHW, HW, HoWo;
+  int nchunk, chunks_per_split, splits, tile;  // tile: 0 = 64x64, 1 = 128x128, 2 = 16x256
+  int wcols;  // MODE 2: Cin * KH * KW (the column Ncol - 1 == wcols is the bias column)
+  FDiv f_howo, f_wo, f_hw, f_w, f_khw, f_kw, f_sh, f_sw;
+};
+
+// k -> (c, r, s) of a filter tap index k = (c * KH + r) * KW + s; compile-time KH, KW turn
+// the divisions into multiplies
+template <int KH_, int KW_>
+__device__ inline void split_tap(int k, const IgGeo& g, int& c, int& r, int& s) {
+  const int khw = KH_ ? KH_ * KW_ : g.KHW;
+  const int kw = KW_ ? KW_ : g.KW;
+  c = KH_ ? k / khw : fdiv(k, g.f_khw);
+  const int rs = k - c * khw;
+  r = KW_ ? rs / kw : fdiv(rs, g.f_kw);
+  s = rs - r * kw;
+}
+
+// TM x TN outputs per workgroup of 4 waves (WMW along M x 4 / WMW along N; each wave
+// NBM x NBN MFMA blocks of 16 x 16), K chunks of 16 through double-buffered LDS
+template <int MODE, int KH_, int KW_, int TM, int TN, int WMW>
+__global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0,
+                                                    const float* __restrict__ B0,
+                                                    const float* __restrict__ bias,
+                                                    float* __restrict__ out,
+                                                    float* __restrict__ out2,
+                                                    float* __restrict__ ws, IgGeo g) {
+  constexpr int WNW = 4 / WMW;
+  constexpr int WTM = TM / WMW, WTN = TN / WNW;  // wave tile
+  constexpr int NBM = WTM / 16, NBN = WTN / 16;  // MFMA blocks per wave
+  constexpr int NLA = TM / 16, NLB = TN / 16;    // A / B elements each thread stages per chunk
+  constexpr int kAP = BK + 1;                    // LDS pitch of the A tile [m][k]
+  constexpr int kBP = TN + 16;  // LDS pitch of the B tile [k][n]: MFMA reads conflict-free
+  __shared__ float s_a[2][TM * kAP];
+  __shared__ float s_b[2][BK * kBP];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, jj = lane & 15;
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
+  const int kc0 = blockIdx.z * g.chunks_per_split;
+  const int kc1 = min(g.nchunk, kc0 + g.chunks_per_split);
+
+  // ---- A loads: thread -> (k = tid & 15, m = tid / 16 + 16 j)
+  const int ak = tid & 15, am = tid >> 4;
+  // ---- B loads: MODE 0/1 thread -> (n = tid % TN, k = tid / TN + (256 / TN) j)
+  //      (pixels coalesced); MODE 2 thread -> (k = tid & 15, n = tid / 16 + 16 j) (k = pixels)
+  constexpr int kBStep = TN >= 256 ? 1 : 256 / TN;
+  const int bn = MODE == 2 ? (tid >> 4) : (tid % TN);
+  const int bk = MODE == 2 ? (tid & 15) : (tid / TN);
+
+  // per-thread fixed part of the B gather
+  int64_t bbase = 0;  // MODE 0/1: image base of this thread's pixel column
+  int py = 0, px = 0;
+  bool pvalid = false;
+  int bc[NLB], br[NLB], bs[NLB];  // MODE 2: the (c, r, s) of this thread's columns
+  bool bcol_ok[NLB], bcol_one[NLB];
+  if (MODE != 2) {
+    const int p = n0 + bn;
+    pvalid = p < g.Ncol;
+    const int pp = pvalid ? p : 0;
+    if (MODE == 0) {
+      const int n = fdiv(pp, g.f_howo), pix = pp - n * g.HoWo;
+      const int oy = fdiv(pix, g.f_wo), ox = pix - oy * g.Wo;
+      py = oy * g.sh - g.ph;
+      px = ox * g.sw - g.pw;
+      bbase = (int64_t)n * g.Cin * g.HW;
+    } else {
+      const int n = fdiv(pp, g.f_hw), pix = pp - n * g.HW;
+      const int iy = fdiv(pix, g.f_w), ix = pix - iy * g.W;
+      py = iy + g.ph;
+      px = ix + g.pw;
+      bbase = (int64_t)n * g.Cout * g.HoWo;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NLB; ++j) {
+      const int col = n0 + bn + 16 * j;
+      bcol_ok[j] = col < g.Ncol;
+      bcol_one[j] = col == g.wcols;
+      int c, r, s;
+      split_tap<KH_, KW_>(bcol_ok[j] && !bcol_one[j] ? col : 0, g, c, r, s);
+      bc[j] = c;
+      br[j] = r;
+      bs[j] = s;
+    }
+  }
+
+  float ra[NLA], rb[NLB];
+  auto gload = [&](int kc) {
+    const int kb = kc * BK;
+    // A
+    {
+      const int k = kb + ak;
+      int a_co = 0, a_rs = 0, a_n = 0, a_pix = 0;
+      if (MODE == 1) {
+        const int khw = KH_ ? KH_ * KW_ : g.KHW;
+        a_co = KH_ ? k / khw : fdiv(k, g.f_khw);
+        a_rs = k - a_co * khw;
+      } else if (MODE == 2) {
+        a_n = fdiv(k < g.K ? k : 0, g.f_howo);
+        a_pix = k - a_n * g.HoWo;
+      }
+#pragma unroll
+      for (int j = 0; j < NLA; ++j) {
+        const int m = m0 + am + 16 * j;
+        float v = 0.f;
+        if (m < g.M && k < g.K) {
+          if (MODE == 0) {
+            v = A0[(int64_t)m * g.K + k];
+          } else if (MODE == 1) {  // m = ci, k = (co, r, s)
+            const int khw = KH_ ? KH_ * KW_ : g.KHW;
+            v = A0[((int64_t)a_co * g.Cin + m) * khw + a_rs];
+          } else {  // m = co, k = pixel
+            v = A0[((int64_t)a_n * g.Cout + m) * g.HoWo + a_pix];
+          }
+        }
+        ra[j] = v;
+      }
+    }
+    // B
+    if (MODE != 2) {
+#pragma unroll
+      for (int j = 0; j < NLB; ++j) {
+        const int k = kb + bk + kBStep * j;
+        float v = 0.f;
+        int c, r, s;
+        split_tap<KH_, KW_>(k < g.K ? k : 0, g, c, r, s);
+        if (MODE == 0) {
+          const int iy = py + r, ix = px + s;
+          if (pvalid && k < g.K && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+            v = B0[bbase + ((int64_t)c * g.H + iy) * g.W + ix];
+        } else {
+          const int ty = py - r, tx = px - s;
+          if (pvalid && k < g.K && ty >= 0 && tx >= 0) {
+            const int oy = fdiv(ty, g.f_sh), ox = fdiv(tx, g.f_sw);
+            if (oy * g.sh == ty && ox * g.sw == tx && oy < g.Ho && ox < g.Wo)
+              v = B0[bbase + ((int64_t)c * g.Ho + oy) * g.Wo + ox];
+          }
+        }
+        rb[j] = v;
+      }
+    } else {
+      const int k = kb + bk;  // pixel
+      const bool kv = k < g.K;
+      const int kk = kv ? k : 0;
+      const int n = fdiv(kk, g.f_howo), pix = kk - n * g.HoWo;
+      const int oy = fdiv(pix, g.f_wo), ox = pix - oy * g.Wo;
+      const int iy0 = oy * g.sh - g.ph, ix0 = ox * g.sw - g.pw;
+      const int64_t xb = (int64_t)n * g.Cin * g.HW;
+#pragma unroll
+      for (int j = 0; j < NLB; ++j) {
+        float v = 0.f;
+        if (kv && bcol_ok[j]) {
+          if (bcol_one[j]) {
+            v = 1.f;
+          } else {
+            const int iy = iy0 + br[j], ix = ix0 + bs[j];
+            if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+              v = B0[xb + ((int64_t)bc[j] * g.H + iy) * g.W + ix];
+          }
+        }
+        rb[j] = v;
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NLA; ++j) s_a[buf][(am + 16 * j) * kAP + ak] = ra[j];
+#pragma unroll
+    for (int j = 0; j < NLB; ++j) {
+      if (MODE == 2)
+        s_b[buf][bk * kBP + bn + 16 * j] = rb[j];
+      else
+        s_b[buf][(bk + kBStep * j) * kBP + bn] = rb[j];
+    }
+  };
+
+  const int wm = wave % WMW, wn = wave / WMW;
+  f4 acc[NBM][NBN];
+#pragma unroll
+  for (int i = 0; i < NBM; ++i)
+#pragma unroll
+    for (int j = 0; j < NBN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (kc0 < kc1) {
+    gload(kc0);
+    sstore(0);
+    __syncthreads();
+    for (int kc = kc0; kc < kc1; ++kc) {
+      const int buf = (kc - kc0) & 1;
+      const bool more = kc + 1 < kc1;
+      if (more) gload(kc + 1);
+      const float* sa = s_a[buf];
+      const float* sb = s_b[buf];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        float a[NBM], b[NBN];
+#pragma unroll
+        for (int mb = 0; mb < NBM; ++mb) a[mb] = sa[(wm * WTM + mb * 16 + jj) * kAP + 4 * ks + kq];
+#pragma unroll
+        for (int nb = 0; nb < NBN; ++nb) b[nb] = sb[(4 * ks + kq) * kBP + wn * WTN + nb * 16 + jj];
+#pragma unroll
+        for (int mb = 0; mb < NBM; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NBN; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mb], b[nb], acc[mb][nb], 0, 0, 0);
+      }
+      if (more) sstore(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: acc[mb][nb][i] = C[m0 + WTM wm + 16 mb + 4 kq + i][n0 + WTN wn + 16 nb + jj]
+#pragma unroll
+  for (int nb = 0; nb < NBN; ++nb) {
+    const int col = n0 + wn * WTN + nb * 16 + jj;
+    if (col >= g.Ncol) continue;
+    int64_t obase = 0;
+    int64_t ostride = 0;  // output offset step per row m
+    if (g.splits > 1) {
+      obase = (int64_t)blockIdx.z * g.M * g.Ncol + col;
+      ostride = g.Ncol;
+    } else if (MODE == 0) {
+      const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
+      obase = (int64_t)n * g.Cout * g.HoWo + pix;
+      ostride = g.HoWo;
+    } else if (MODE == 1) {
+      const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
+      obase = (int64_t)n * g.Cin * g.HW + pix;
+      ostride = g.HW;
+    } else {
+      obase = col;
+      ostride = g.wcols;
+    }
+#pragma unroll
+    for (int mb = 0; mb < NBM; ++mb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * WTM + mb * 16 + 4 * kq + i;
+        if (m >= g.M) continue;
+        float v = acc[mb][nb][i];
+        if (g.splits > 1) {
+          ws[obase + (int64_t)m * ostride] = v;
+        } else if (MODE == 2) {
+          if (col == g.wcols)
+            out2[m] = v;
+          else
+            out[obase + (int64_t)m * ostride] = v;
+        } else {
+          if (MODE == 0 && bias) v += bias[m];
+          out[obase + (int64_t)m * ostride] = v;
+        }
+      }
+  }
+}
+
+// sum of the split-K partials in split order, scattered to the output layout
+template <int MODE>
+__global__ __launch_bounds__(256) void igemm_reduce_kernel(const float* __restrict__ ws,
+                                                           const float* __restrict__ bias,
+                                                           float* __restrict__ out,
+                                                           float* __restrict__ out2, IgGeo g) {
+  const int64_t total = (int64_t)g.M * g.Ncol;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / g.Ncol), col = (int)(i - (int64_t)m * g.Ncol);
+    float v = ws[i];
+    for (int z = 1; z < g.splits; ++z) v += ws[(int64_t)z * total + i];
+    if (MODE == 0) {
+      const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
+      if (bias) v += bias[m];
+      out[((int64_t)n * g.Cout + m) * g.HoWo + pix] = v;
+    } else if (MODE == 1) {
+      const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
+      out[((int64_t)n * g.Cin + m) * g.HW + pix] = v;
+    } else {
+      if (col == g.wcols)
+        out2[m] = v;
+      else
+        out[(int64_t)m * g.wcols + col] = v;
+    }
+  }
+}
+
+int g_num_cus = 0;
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    g_num_cus = cus;
+  }
+  return g_num_cus;
+}
+
+constexpr int64_t kMaxWorkspace = 16ll << 20;  // split-K partials (bytes): their round trip stays small
+
+// geometry, tile and split-K choice; false when the shape is out of range
+bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, int sh, int sw,
+              int ph, int pw, int Ho, int Wo, int bias_col, IgGeo& g) {
+  if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0 || KH <= 0 || KW <= 0 || sh <= 0 ||
+      sw <= 0 || ph < 0 || pw < 0 || Ho <= 0 || Wo <= 0)
+    return false;
+  // element offsets are 64-bit per image; the flattened GEMM indices (n, pixel) are 32-bit
+  const int64_t xin = (int64_t)N * Cin * H * W, yout = (int64_t)N * Cout * Ho * Wo;
+  const int64_t wsz = (int64_t)Cout * Cin * KH * KW;
+  if (xin >= (1ll << 31) || yout >= (1ll << 31) || wsz >= (1ll << 31)) return false;
+  g = IgGeo{};
+  g.N = N; g.Cin = Cin; g.H = H; g.W = W; g.Cout = Cout; g.Ho = Ho; g.Wo = Wo;
+  g.KH = KH; g.KW = KW; g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
+  g.KHW = KH * KW; g.HW = H * W; g.HoWo = Ho * Wo;
+  g.wcols = Cin * KH * KW;
+  g.f_howo = make_fdiv(g.HoWo); g.f_wo = make_fdiv(Wo); g.f_hw = make_fdiv(g.HW);
+  g.f_w = make_fdiv(W); g.f_khw = make_fdiv(g.KHW); g.f_kw = make_fdiv(KW);
+  g.f_sh = make_fdiv(sh); g.f_sw = make_fdiv(sw);
+  if (mode == 0) {
+    g.M = Cout; g.Ncol = N * Ho * Wo; g.K = Cin * g.KHW;
+  } else if (mode == 1) {
+    g.M = Cin; g.Ncol = N * H * W; g.K = Cout * g.KHW;
+  } else {
+    g.M = Cout; g.Ncol = g.wcols + (bias_col ? 1 : 0); g.K = N * Ho * Wo;
+  }
+  g.nchunk = (g.K + BK - 1) / BK;
+  const int64_t cus = num_cus();
+  // 16 x 256 tiles for M <= 16 (a forward / backward-data conv into 1-16 channels: no
+  // 64-row tile mostly idle; the weight gradient's columns are gathers, kept at 64); 128 x 128 (4x the MFMA work per staged chunk) when M, N are large;
+  // else 64 x 64
+  int tm, tn;
+  if (g.M <= 16 && mode != 2) {
+    g.tile = 2; tm = 16; tn = 256;
+  } else if (g.M >= 128 && (int64_t)g.M * g.Ncol >= 128ll * 128 * cus / 2) {
+    g.tile = 1; tm = tn = 128;
+  } else {
+    g.tile = 0; tm = tn = 64;
+  }
+  const int64_t tiles = bpk::ceil_div(g.M, tm) * bpk::ceil_div(g.Ncol, tn);
+  // split K until ~4 (64 x 64: 8) workgroups per CU for latency hiding, >= 8 chunks (128
+  // of K) per split, partials within the workspace cap
+  const int64_t want = (g.tile == 0 ? 8 : 4) * cus;
+  int64_t splits = 1;
+  if (tiles < want) splits = std::min<int64_t>(bpk::ceil_div(want, tiles), g.nchunk / 8);
+  const int64_t cap = kMaxWorkspace / ((int64_t)g.M * g.Ncol * 4);
+  splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::min<int64_t>(cap, 4096)));
+  g.chunks_per_split = (int)bpk::ceil_div(g.nchunk, splits);
+  g.splits = (int)bpk::ceil_div(g.nchunk, g.chunks_per_split);
+  return true;
+}
+
+template <int MODE, int TM, int TN, int WMW>
+void launch_tile(const IgGeo& g, const float* A0, const float* B0, const float* bias,
+                 float* out, float* out2, float* wsp, hipStream_t st) {
+  const dim3 grid((unsigned)bpk::ceil_div(g.Ncol, TN), (unsigned)bpk::ceil_div(g.M, TM),
+                  (unsigned)g.splits);
+#define BPK_IG(KH_, KW_) \
+  igemm_kernel<MODE, KH_, KW_, TM, TN, WMW><<<grid, 256, 0, st>>>(A0, B0, bias, out, out2, wsp, g)
+  if (g.KH == 3 && g.KW == 3)
+    BPK_IG(3, 3);
+  else if (g.KH == 1 && g.KW == 1)
+    BPK_IG(1, 1);
+  else if (g.KH == 2 && g.KW == 2)
+    BPK_IG(2, 2);
+  else if (g.KH == 4 && g.KW == 4)
+    BPK_IG(4, 4);
+  else
+    BPK_IG(0, 0);
+#undef BPK_IG
+}
+
+template <int MODE>
+int launch(const IgGeo& g, const float* A0, const float* B0, const float* bias, float* out,
+           float* out2, float* ws, hipStream_t st) {
+  float* wsp = g.splits > 1 ? ws : nullptr;
+  if (g.tile == 1)
+    launch_tile<MODE, 128, 128, 2>(g, A0, B0, bias, out, out2, wsp, st);
+  else if (g.tile == 2)
+    launch_tile<MODE, 16, 256, 1>(g, A0, B0, bias, out, out2, wsp, st);
+  else
+    launch_tile<MODE, 64, 64, 2>(g, A0, B0, bias, out, out2, wsp, st);
+  BPK_LAUNCH_CHECK("conv2d_igemm");
+  if (g.splits > 1) {
+    const int64_t total = (int64_t)g.M * g.Ncol;
+    const unsigned blocks = (unsigned)std::min<int64_t>(bpk::ceil_div(total, 256), 4096);
+    igemm_reduce_kernel<MODE><<<blocks, 256, 0, st>>>(ws, bias, out, out2, g);
+    BPK_LAUNCH_CHECK("conv2d_igemm_reduce");
+  }
+  return BPK_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t bpk_conv2d_igemm_workspace_bytes(int mode, int N, int Cin, int H, int W,
+                                                    int Cout, int KH, int KW, int sh, int sw,
+                                                    int ph, int pw, int Ho, int Wo,
+                                                    int bias_grad) {
+  IgGeo g;
+  if (mode < 0 || mode > 2 ||
+      !make_geo(mode, N, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo, bias_grad, g))
+    return -1;
+  return g.splits > 1 ? (int64_t)g.splits * g.M * g.Ncol * 4 : 0;
+}
+
+extern "C" int bpk_conv2d_igemm_fwd_f32(const float* x, const float* w, const float* bias,
+                                        float* y, void* wsv, int N, int Cin, int H, int W,
+                                        int Cout, int KH, int KW, int sh, int sw, int ph, int pw,
+                                        int Ho, int Wo, void* stream) {
+  IgGeo g;
+  float* ws = static_cast<float*>(wsv);
+  BPK_REQUIRE(make_geo(0, N, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo, 0, g),
+              "conv2d_igemm_fwd: bad shape N=%d Cin=%d %dx%d Cout=%d k=%dx%d", N, Cin, H, W,
+              Cout, KH, KW);
+  BPK_REQUIRE(Ho == (H + 2 * ph - KH) / sh + 1 && Wo == (W + 2 * pw - KW) / sw + 1,
+              "conv2d_igemm_fwd: output %dx%d inconsistent", Ho, Wo);
+  BPK_REQUIRE(x && w && y && (g.splits == 1 || ws), "conv2d_igemm_fwd: null pointer");
+  return launch<0>(g, w, x, bias, y, nullptr, ws, bpk::as_stream(stream));
+}
+
+extern "C" int bpk_conv2d_igemm_dgrad_f32(const float* gy, const float* w, float* gx, void* wsv,
+                                          int N, int Cin, int H, int W, int Cout, int KH, int KW,
+                                          int sh, int sw, int ph, int pw, int Ho, int Wo,
+                                          void* stream) {
+  IgGeo g;
+  float* ws = static_cast<float*>(wsv);
+  BPK_REQUIRE(make_geo(1, N, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo, 0, g),
+              "conv2d_igemm_dgrad: bad shape N=%d Cin=%d %dx%d Cout=%d k=%dx%d", N, Cin, H, W,
+              Cout, KH, KW);
+  BPK_REQUIRE((H + 2 * ph - KH) / sh + 1 == Ho && (W + 2 * pw - KW) / sw + 1 == Wo,
+              "conv2d_igemm_dgrad: output %dx%d inconsistent with input %dx%d", Ho, Wo, H, W);
+  BPK_REQUIRE(gy && w && gx && (g.splits == 1 || ws), "conv2d_igemm_dgrad: null pointer");
+  return launch<1>(g, w, gy, nullptr, gx, nullptr, ws, bpk::as_stream(stream));
+}
+
+extern "C" int bpk_conv2d_igemm_wgrad_f32(const float* x, const float* gy, float* dw, float* db,
+                                          void* wsv, int N, int Cin, int H, int W, int Cout,
+                                          int KH, int KW, int sh, int sw, int ph, int pw, int Ho,
+                                          int Wo, void* stream) {
+  IgGeo g;
+  float* ws = static_cast<float*>(wsv);
+  BPK_REQUIRE(make_geo(2, N, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo, db != nullptr, g),
+              "conv2d_igemm_wgrad: bad shape N=%d Cin=%d %dx%d Cout=%d k=%dx%d", N, Cin, H, W,
+              Cout, KH, KW);
+  BPK_REQUIRE((H + 2 * ph - KH) / sh + 1 == Ho && (W + 2 * pw - KW) / sw + 1 == Wo,
+              "conv2d_igemm_wgrad: output %dx%d inconsistent with input %dx%d", Ho, Wo, H, W);
+  BPK_REQUIRE(x && gy && dw && (g.splits == 1 || ws), "conv2d_igemm_wgrad: null pointer");
+  return launch<2>(g, gy, x, nullptr, dw, db, ws, bpk::as_stream(stream));
+}

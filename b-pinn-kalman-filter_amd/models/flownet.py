@@ -130,8 +130,8 @@ class Matching(nn.Module):
     def __init__(self, config, level):
         super().__init__()
         self.dt = config.data.dt * 0.5 ** level
-        self.flow_upsample = nn.ConvTranspose2d(2, 2, kernel_size=4, stride=2, padding=1,
-                                                bias=False, groups=2)
+        self.flow_upsample = layers.ConvTranspose2d(2, 2, kernel_size=4, stride=2, padding=1,
+                                                    bias=False, groups=2)
         self.corr_conv = get_conv_field_layer(49, 2)
 
     def forward(self, feature1, feature2, flow=None):
@@ -228,7 +228,7 @@ def get_down_layer(in_channels, out_channels):
 
 
 def get_up_layer(in_channels, out_channels):
-    return nn.Sequential(nn.ConvTranspose2d(in_channels, out_channels, kernel_size=2, stride=2))
+    return nn.Sequential(layers.ConvTranspose2d(in_channels, out_channels, kernel_size=2, stride=2))
 
 
 class PressureNet(nn.Module):
@@ -252,8 +252,9 @@ class PressureNet(nn.Module):
         self.up = nn.ModuleList(ups)
         self.up_conv = nn.ModuleList(up_convs)
         half = ch[0] // 2
-        self.end = nn.Sequential(get_double_res(ch[0], half), nn.Conv2d(half, half, kernel_size=1),
-                                 get_double_res(half, 1), nn.Conv2d(1, 1, kernel_size=1))
+        self.end = nn.Sequential(get_double_res(ch[0], half),
+                                 layers.Conv2d(half, half, kernel_size=1),
+                                 get_double_res(half, 1), layers.Conv2d(1, 1, kernel_size=1))
 
     def get_norm_feature(self, flow):
         """features of [u, v, -(u^2 + v^2)] (reference flownet.py:280-283)."""

@@ -130,9 +130,10 @@ def conv2d(x, conv: nn.Conv2d, bias=True):
         return conv_op.conv3x3(x, conv.weight, b)
     if _is_1x1(x, conv) and conv_op.conv1x1_train_supported(x, conv.weight):
         return conv_op.conv1x1_ad(x, conv.weight, b)  # MFMA GEMMs, every derivative order
-    if (x.is_cuda and torch.is_grad_enabled() and _WINO_ENABLED and conv.padding_mode == "zeros"
+    if (x.is_cuda and _WINO_ENABLED and conv.padding_mode == "zeros"
             and isinstance(conv.padding, tuple)):
-        # under autograd: higher derivatives as plain convolutions (op.conv.conv2d_general)
+        # implicit-GEMM MFMA kernels; under autograd every derivative order stays a plain
+        # convolution (op.conv.conv2d_general)
         return conv_op.conv2d_general(x, conv.weight, b, conv.stride, conv.padding,
                                       conv.dilation, conv.groups)
     return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
@@ -187,6 +188,20 @@ class Conv2d(nn.Conv2d):
 
     def forward(self, x):
         return conv2d(x, self)
+
+
+class ConvTranspose2d(nn.ConvTranspose2d):
+    """nn.ConvTranspose2d (same parameters / state-dict keys) as the adjoint of a conv on the
+    implicit-GEMM MFMA kernels, every derivative order a plain convolution
+    (op.conv.conv_transpose2d_general)."""
+
+    def forward(self, x, output_size=None):
+        if (not x.is_cuda or not _WINO_ENABLED or output_size is not None
+                or self.padding_mode != "zeros" or isinstance(self.padding, str)):
+            return super().forward(x, output_size)
+        return conv_op.conv_transpose2d_general(x, self.weight, self.bias, self.stride,
+                                                self.padding, self.output_padding, self.groups,
+                                                self.dilation)
 
 
 def ddpm_conv3x3(in_planes, out_planes, stride=1, bias=True, dilation=1, init_scale=1., padding=1):

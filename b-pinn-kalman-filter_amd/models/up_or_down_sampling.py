@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from op import conv as conv_op
 from op import upfirdn2d
 
 _KERNEL_CACHE: dict = {}
@@ -67,7 +68,21 @@ class Conv2d(nn.Module):
             return x + b.reshape(1, -1, 1, 1) if b is not None else x
         if self.down:
             return conv_downsample_2d(x, self.weight, k=self.resample_kernel, bias=b)
-        return F.conv2d(x, self.weight, b, stride=1, padding=self.kernel // 2)
+        return _conv(x, self.weight, b, 1, self.kernel // 2)
+
+
+def _native(x):
+    return x.is_cuda and x.dtype == torch.float32
+
+
+def _conv(x, w, bias, stride, padding):
+    """F.conv2d on the native kernels (op.conv: Winograd / implicit-GEMM MFMA, every
+    derivative order a plain convolution) for fp32 HIP tensors."""
+    if _native(x):
+        if stride == 1 and padding == 1 and tuple(w.shape[2:]) == (3, 3):
+            return conv_op.conv3x3(x, w, bias)
+        return conv_op.conv2d_general(x, w, bias, stride, padding)
+    return F.conv2d(x, w, bias, stride=stride, padding=padding)
 
 
 def naive_upsample_2d(x, factor=2):
@@ -99,7 +114,10 @@ def upsample_conv_2d(x, w, k=None, factor=2, gain=1):
     wt = torch.reshape(w, (num_groups, -1, inC, convH, convW))
     wt = torch.flip(wt, [3, 4]).permute(0, 2, 1, 3, 4)
     wt = torch.reshape(wt, (num_groups * inC, -1, convH, convW))
-    x = F.conv_transpose2d(x, wt, stride=(factor, factor), output_padding=op, padding=0)
+    if _native(x):
+        x = conv_op.conv_transpose2d_general(x, wt, None, factor, 0, op)
+    else:
+        x = F.conv_transpose2d(x, wt, stride=(factor, factor), output_padding=op, padding=0)
     kt = fir_kernel(kk, gain * (factor ** 2), x.device, x.dtype)
     return upfirdn2d(x, kt, pad=((p + 1) // 2 + factor - 1, p // 2 + 1))
 
@@ -113,7 +131,7 @@ def conv_downsample_2d(x, w, k=None, factor=2, gain=1, bias=None):
     kt = fir_kernel(kk, gain, x.device, x.dtype)
     p = (kt.shape[0] - factor) + (convW - 1)
     x = upfirdn2d(x, kt, pad=((p + 1) // 2, p // 2))
-    return F.conv2d(x, w, bias, stride=[factor, factor], padding=0)
+    return _conv(x, w, bias, factor, 0)
 
 
 def upsample_2d(x, k=None, factor=2, gain=1):

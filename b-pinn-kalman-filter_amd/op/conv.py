@@ -194,6 +194,155 @@ def conv3x3_small_raw(x, weight, bias=None, pre=None):
     return y
 
 
+# ------------------------------------------------ general convolutions on the MFMA (igemm)
+_IGEMM = os.environ.get("BPK_IGEMM", "1") != "0"  # 0: MIOpen for the shapes below
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(int(e) for e in v)
+
+
+def igemm_supported(x, w, stride=1, padding=0, dilation=1, groups=1):
+    """The implicit-GEMM MFMA kernels (csrc/conv_igemm.hip) run conv2d(x, w) and all of its
+    derivatives: fp32 NCHW HIP tensors, groups = 1, dilation = 1, zero padding.  `w`: the
+    weight tensor or its shape."""
+    wshape = tuple(w) if isinstance(w, (tuple, list, torch.Size)) else tuple(w.shape)
+    if isinstance(w, torch.Tensor) and w.dtype != torch.float32:
+        return False
+    return (_IGEMM and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and len(wshape) == 4 and int(groups) == 1
+            and _pair(dilation) == (1, 1) and wshape[1] == x.shape[1]
+            and x.shape[2] + 2 * _pair(padding)[0] >= wshape[2]
+            and x.shape[3] + 2 * _pair(padding)[1] >= wshape[3])
+
+
+def _igemm_ws(mode, N, C, H, W, Co, KH, KW, s, p, Ho, Wo, bias_grad, device):
+    nbytes = lib.bpk_conv2d_igemm_workspace_bytes(mode, N, C, H, W, Co, KH, KW, s[0], s[1],
+                                                  p[0], p[1], Ho, Wo, int(bias_grad))
+    if nbytes < 0:
+        raise RuntimeError(f"conv2d_igemm: unsupported shape x [{N}, {C}, {H}, {W}], "
+                           f"w [{Co}, {C}, {KH}, {KW}]")
+    return torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=device)
+
+
+def conv2d_igemm_raw(x, w, bias=None, stride=1, padding=0):
+    """F.conv2d(x, w, bias, stride, padding) on the implicit-GEMM MFMA kernel (no autograd)."""
+    s, p = _pair(stride), _pair(padding)
+    x = x.detach().contiguous()
+    w = w.detach().contiguous()
+    N, C, H, W = x.shape
+    Co, _, KH, KW = w.shape
+    Ho, Wo = (H + 2 * p[0] - KH) // s[0] + 1, (W + 2 * p[1] - KW) // s[1] + 1
+    b = None if bias is None else bias.detach().contiguous()
+    y = torch.empty((N, Co, Ho, Wo), dtype=torch.float32, device=x.device)
+    ws = _igemm_ws(0, N, C, H, W, Co, KH, KW, s, p, Ho, Wo, False, x.device)
+    check(lib.bpk_conv2d_igemm_fwd_f32(x.data_ptr(), w.data_ptr(),
+                                       None if b is None else b.data_ptr(), y.data_ptr(),
+                                       ws.data_ptr(), N, C, H, W, Co, KH, KW, s[0], s[1], p[0],
+                                       p[1], Ho, Wo, stream_ptr(x.device)), "conv2d_igemm_fwd")
+    return y
+
+
+def conv2d_input_igemm_raw(xshape, w, gy, stride=1, padding=0):
+    """torch.nn.grad.conv2d_input(xshape, w, gy, stride, padding) -- the conv's adjoint, i.e.
+    F.conv_transpose2d(gy, w) cropped / extended to xshape -- on the MFMA kernel."""
+    s, p = _pair(stride), _pair(padding)
+    w = w.detach().contiguous()
+    gy = gy.detach().contiguous()
+    N, C, H, W = (int(v) for v in xshape)
+    Co, _, KH, KW = w.shape
+    Ho, Wo = gy.shape[2], gy.shape[3]
+    gx = torch.empty((N, C, H, W), dtype=torch.float32, device=gy.device)
+    ws = _igemm_ws(1, N, C, H, W, Co, KH, KW, s, p, Ho, Wo, False, gy.device)
+    check(lib.bpk_conv2d_igemm_dgrad_f32(gy.data_ptr(), w.data_ptr(), gx.data_ptr(),
+                                         ws.data_ptr(), N, C, H, W, Co, KH, KW, s[0], s[1],
+                                         p[0], p[1], Ho, Wo, stream_ptr(gy.device)),
+          "conv2d_igemm_dgrad")
+    return gx
+
+
+def conv2d_weight_igemm_raw(x, wshape, gy, stride=1, padding=0, bias_grad=False):
+    """(torch.nn.grad.conv2d_weight(x, wshape, gy, stride, padding), gy.sum((0, 2, 3)) or
+    None) from one MFMA kernel (the bias gradient is an extra GEMM column of ones)."""
+    s, p = _pair(stride), _pair(padding)
+    x = x.detach().contiguous()
+    gy = gy.detach().contiguous()
+    N, C, H, W = x.shape
+    Co, _, KH, KW = (int(v) for v in wshape)
+    Ho, Wo = gy.shape[2], gy.shape[3]
+    dw = torch.empty((Co, C, KH, KW), dtype=torch.float32, device=x.device)
+    db = torch.empty((Co,), dtype=torch.float32, device=x.device) if bias_grad else None
+    ws = _igemm_ws(2, N, C, H, W, Co, KH, KW, s, p, Ho, Wo, bias_grad, x.device)
+    check(lib.bpk_conv2d_igemm_wgrad_f32(x.data_ptr(), gy.data_ptr(), dw.data_ptr(),
+                                         None if db is None else db.data_ptr(), ws.data_ptr(),
+                                         N, C, H, W, Co, KH, KW, s[0], s[1], p[0], p[1], Ho, Wo,
+                                         stream_ptr(x.device)), "conv2d_igemm_wgrad")
+    return dw, db
+
+
+# Kernel selection per distinct call: the implicit-GEMM kernels win on the small images /
+# odd channel counts / 1x1 weight gradients the PINN and the CIFAR-10 net's lowest levels run
+# (no NHWC transposes, no per-call solver search on the host), MIOpen's Winograd solvers on
+# big 3x3 convs at 8x8+ (tools/bench_igemm.py, profiles/r02_igemm_shapes.jsonl).  The first
+# eager call of each (op, shapes) times both once and caches the faster; under graph
+# capture an unseen call takes the implicit-GEMM kernel.  BPK_IGEMM=2: always igemm.
+_IG_MODE = os.environ.get("BPK_IGEMM", "1")
+_CHOICE: dict = {}
+
+
+def _time_us(fn, reps=3):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def _pick(key, run_ig, run_mi):
+    """run_ig() or run_mi(), whichever the cached per-key timing says is faster."""
+    if _IG_MODE == "2":
+        return run_ig()
+    c = _CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return run_ig()
+        with torch.no_grad():
+            c = _time_us(run_ig) <= _time_us(run_mi)
+        _CHOICE[key] = c
+    return run_ig() if c else run_mi()
+
+
+def conv2d_select(x, w, bias, stride, padding):
+    """F.conv2d(x, w, bias, stride, padding) (no autograd) on the faster of igemm / MIOpen."""
+    s, p = _pair(stride), _pair(padding)
+    key = ("fwd", tuple(x.shape), tuple(w.shape), s, p, bias is not None)
+    b = None if bias is None else bias.detach()
+    return _pick(key, lambda: conv2d_igemm_raw(x, w, b, s, p),
+                 lambda: F.conv2d(x.detach(), w.detach(), b, s, p))
+
+
+def conv2d_input_select(xshape, w, gy, stride, padding):
+    s, p = _pair(stride), _pair(padding)
+    xshape = tuple(int(v) for v in xshape)
+    key = ("dgrad", xshape, tuple(w.shape), s, p)
+    return _pick(key, lambda: conv2d_input_igemm_raw(xshape, w, gy, s, p),
+                 lambda: torch.nn.grad.conv2d_input(xshape, w.detach(), gy.detach(), s, p))
+
+
+def conv2d_weight_select(x, wshape, gy, stride, padding, bias_grad):
+    s, p = _pair(stride), _pair(padding)
+    wshape = tuple(int(v) for v in wshape)
+    key = ("wgrad", tuple(x.shape), wshape, s, p, bool(bias_grad))
+
+    def mi():
+        dw = torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), s, p)
+        return dw, (gy.detach().sum((0, 2, 3)) if bias_grad else None)
+    return _pick(key, lambda: conv2d_weight_igemm_raw(x, wshape, gy, s, p, bias_grad), mi)
+
+
 def _flip_t(w):
     """[Cout, Cin, 3, 3] -> the flipped, transposed filter [Cin, Cout, 3, 3]: backward-data of
     a 3x3 / stride-1 / pad-1 conv is the forward conv of the output gradient with it."""
@@ -209,6 +358,8 @@ def _fwd_impl(x, w, bias=None, skip=None, div=1.0):
     with torch.no_grad():
         if small_supported(x, w):
             y = conv3x3_small_raw(x.detach(), w, bias)
+        elif igemm_supported(x, w, 1, 1):
+            y = conv2d_select(x, w, bias, 1, 1)
         else:
             y = F.conv2d(x.detach(), w, None if bias is None else bias.detach(), padding=1)
         if skip is not None:
@@ -225,6 +376,8 @@ def _wgrad_impl(x, gy, wshape, want_b):
             dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
             return dw, (db if want_b else None)
         dw = conv3x3_wgrad_raw(x, gy, wshape)
+    elif _IGEMM and x.is_cuda and x.dtype == torch.float32:
+        return conv2d_weight_select(x, tuple(wshape), gy, 1, 1, want_b)
     else:
         with torch.no_grad():
             dw = torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), padding=1)
@@ -239,6 +392,9 @@ def _fwd_ft_impl(x, w):
     if (C == w.shape[0] and x.is_cuda and x.dtype == torch.float32
             and bool(lib.bpk_conv3x3_wino_supported(N, C, w.shape[1], H, W))):
         return conv3x3_fwd_raw(x.detach(), w, ft=True)
+    if _IGEMM and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32:
+        # conv3x3(x, flip_t(w)) is the adjoint of conv3x3(., w): the dgrad kernel, no flip
+        return conv2d_input_select((N, w.shape[1], H, W), w, x, 1, 1)
     return _fwd_impl(x, _flip_t(w))
 
 
@@ -546,19 +702,27 @@ def conv1x1_ad(x, weight, bias=None):
 
 
 # ---------------------------------------------------------------- general convolutions
-# Every other Conv2d of the networks (stride-2 3x3, 1x1, ...) runs on MIOpen, but through
-# three autograd Functions -- conv, its adjoint (conv transpose) and the weight gradient --
-# whose backward passes are written in terms of each other.  Higher derivatives (the PINN
+# Every other Conv2d / ConvTranspose2d of the networks (stride-2 3x3, the PINN's tiny
+# levels and odd channel counts, 2x2 / 4x4 transposed convs, ...) runs through three
+# autograd Functions -- conv, its adjoint (conv transpose) and the weight gradient -- whose
+# backward passes are written in terms of each other.  Higher derivatives (the PINN
 # residual differentiates the networks twice) thus stay plain convolutions, instead of the
 # generic convolution double backward, which runs its weight terms as batch/channel-swapped
-# convolutions with H x W kernels (0.5-5 ms each on the PINN shapes).
+# convolutions with H x W kernels (0.5-5 ms each on the PINN shapes).  Underneath: the
+# implicit-GEMM MFMA kernels (igemm_supported), MIOpen for anything else (groups, dilation).
 
 def _cfg(ctx_like):
     return dict(stride=ctx_like[0], padding=ctx_like[1], dilation=ctx_like[2], groups=ctx_like[3])
 
 
-def _conv_fn(x, w, cfg):
-    return _ConvG.apply(x, w, cfg) if torch.is_grad_enabled() else _ConvG.forward(None, x, w, cfg)
+def _ig_ok(x, w, cfg):
+    return igemm_supported(x, w, cfg[0], cfg[1], cfg[2], cfg[3])
+
+
+def _conv_fn(x, w, cfg, b=None):
+    if torch.is_grad_enabled():
+        return _ConvG.apply(x, w, b, cfg)
+    return _ConvG.forward(None, x, w, b, cfg)
 
 
 def _convt_fn(u, w, xshape, cfg):
@@ -567,30 +731,39 @@ def _convt_fn(u, w, xshape, cfg):
     return _ConvTG.forward(None, u, w, xshape, cfg)
 
 
-def _wgrad_fn(x, gy, wshape, cfg):
+def _wgrad_fn(x, gy, wshape, cfg, bias_grad=False):
+    """(dw, db or None)"""
     if torch.is_grad_enabled():
-        return _WgradG.apply(x, gy, wshape, cfg)
-    return _WgradG.forward(None, x, gy, wshape, cfg)
+        return _WgradG.apply(x, gy, wshape, cfg, bias_grad)
+    return _WgradG.forward(None, x, gy, wshape, cfg, bias_grad)
 
 
 class _ConvG(torch.autograd.Function):
-    """y = conv2d(x, w) (no bias), MIOpen forward; grads: conv transpose and weight grad."""
+    """y = conv2d(x, w) + b; grads: conv transpose, weight (+ bias) gradient."""
 
     @staticmethod
-    def forward(ctx, x, w, cfg):
-        mark_inputs(ctx, x, w, cfg)
+    def forward(ctx, x, w, b, cfg):
+        mark_inputs(ctx, x, w, b, cfg)
         if ctx is not None:
             ctx.save_for_backward(x, w)
             ctx.cfg = cfg
+            ctx.has_b = b is not None
+        if _ig_ok(x, w, cfg):
+            return conv2d_select(x, w, b, cfg[0], cfg[1])
         with torch.no_grad():
-            return F.conv2d(x.detach(), w.detach(), None, **_cfg(cfg))
+            return F.conv2d(x.detach(), w.detach(), None if b is None else b.detach(), **_cfg(cfg))
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gx = _convt_fn(gy, w, tuple(x.shape), ctx.cfg) if want_grad(ctx, 0) else None
-        gw = _wgrad_fn(x, gy, tuple(w.shape), ctx.cfg) if want_grad(ctx, 1) else None
-        return gx, gw, None
+        gw = gb = None
+        want_b = ctx.has_b and want_grad(ctx, 2)
+        if want_grad(ctx, 1) or want_b:
+            gw, gb = _wgrad_fn(x, gy, tuple(w.shape), ctx.cfg, bool(want_b))
+            if not want_grad(ctx, 1):
+                gw = None
+        return gx, gw, gb, None
 
 
 class _ConvTG(torch.autograd.Function):
@@ -602,6 +775,9 @@ class _ConvTG(torch.autograd.Function):
         if ctx is not None:
             ctx.save_for_backward(u, w)
             ctx.cfg = cfg
+        if (_IGEMM and u.is_cuda and u.dtype == torch.float32 and w.dtype == torch.float32
+                and int(cfg[3]) == 1 and _pair(cfg[2]) == (1, 1)):
+            return conv2d_input_select(xshape, w, u, cfg[0], cfg[1])
         with torch.no_grad():
             return torch.nn.grad.conv2d_input(xshape, w.detach(), u.detach(), **_cfg(cfg))
 
@@ -609,34 +785,66 @@ class _ConvTG(torch.autograd.Function):
     def backward(ctx, gz):
         u, w = ctx.saved_tensors
         gu = _conv_fn(gz, w, ctx.cfg) if want_grad(ctx, 0) else None
-        gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg) if want_grad(ctx, 1) else None
+        gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg)[0] if want_grad(ctx, 1) else None
         return gu, gw, None, None
 
 
 class _WgradG(torch.autograd.Function):
-    """dw = d<conv2d(x, w), gy>/dw; linear in x and gy."""
+    """(dw, db) = d<conv2d(x, w) + b, gy>/d(w, b); bilinear in (x, gy)."""
 
     @staticmethod
-    def forward(ctx, x, gy, wshape, cfg):
-        mark_inputs(ctx, x, gy, wshape, cfg)
+    def forward(ctx, x, gy, wshape, cfg, bias_grad):
+        mark_inputs(ctx, x, gy, wshape, cfg, bias_grad)
         if ctx is not None:
             ctx.save_for_backward(x, gy)
             ctx.cfg = cfg
+        if _ig_ok(x, tuple(wshape), cfg):
+            return conv2d_weight_select(x, wshape, gy, cfg[0], cfg[1], bias_grad)
         with torch.no_grad():
-            return torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), **_cfg(cfg))
+            dw = torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), **_cfg(cfg))
+            return dw, (gy.detach().sum((0, 2, 3)) if bias_grad else None)
 
     @staticmethod
-    def backward(ctx, ggw):
+    def backward(ctx, ggw, ggb):
         x, gy = ctx.saved_tensors
-        gx = _convt_fn(gy, ggw, tuple(x.shape), ctx.cfg) if want_grad(ctx, 0) else None
-        ggy = _conv_fn(x, ggw, ctx.cfg) if want_grad(ctx, 1) else None
-        return gx, ggy, None, None
+        gx = ggy = None
+        if want_grad(ctx, 0) and ggw is not None:
+            gx = _convt_fn(gy, ggw, tuple(x.shape), ctx.cfg)
+        if want_grad(ctx, 1):
+            if ggw is not None:
+                ggy = _conv_fn(x, ggw, ctx.cfg, ggb)
+            elif ggb is not None:
+                ggy = ggb.view(1, -1, 1, 1).expand_as(gy)
+        return gx, ggy, None, None, None
 
 
 def conv2d_general(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
     """F.conv2d with every derivative order expressed as convolutions / conv transposes /
-    weight gradients (see above).  MIOpen kernels underneath."""
-    pair = lambda v: (v, v) if isinstance(v, int) else tuple(v)
-    cfg = (pair(stride), pair(padding), pair(dilation), int(groups))
-    y = _conv_fn(x, weight, cfg)
+    weight gradients (see above); bias fused into the forward and weight-gradient kernels."""
+    cfg = (_pair(stride), _pair(padding), _pair(dilation), int(groups))
+    return _conv_fn(x, weight, cfg, bias)
+
+
+def _dense_groups(w, groups):
+    """ConvTranspose2d weight [Cin, Cout / g, k, k] -> the block-diagonal dense weight
+    [Cin, Cout, k, k] (differentiable; the FlowNet flow upsample has g = 2 channels)."""
+    if groups == 1:
+        return w
+    ci, cog, kh, kw = w.shape
+    wv = w.reshape(groups, ci // groups, cog, kh, kw)
+    eye = torch.eye(groups, dtype=w.dtype, device=w.device)
+    return torch.einsum("aijkl,ab->aibjkl", wv, eye).reshape(ci, groups * cog, kh, kw)
+
+
+def conv_transpose2d_general(u, weight, bias=None, stride=1, padding=0, output_padding=0,
+                             groups=1, dilation=1):
+    """F.conv_transpose2d(u, weight, bias, stride, padding, output_padding, groups, dilation)
+    as the adjoint of conv2d(., weight) (the dgrad kernel), every derivative order on the
+    same three Functions; groups through a block-diagonal dense weight."""
+    s, p, op, d = _pair(stride), _pair(padding), _pair(output_padding), _pair(dilation)
+    w = _dense_groups(weight, int(groups))
+    N, _, Hu, Wu = u.shape
+    Ho = (Hu - 1) * s[0] - 2 * p[0] + d[0] * (w.shape[2] - 1) + op[0] + 1
+    Wo = (Wu - 1) * s[1] - 2 * p[1] + d[1] * (w.shape[3] - 1) + op[1] + 1
+    y = _convt_fn(u, w, (N, w.shape[1], Ho, Wo), (s, p, d, 1))
     return y if bias is None else y + bias.view(1, -1, 1, 1)

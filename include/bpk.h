@@ -432,6 +432,36 @@ int64_t bpk_gemm_nchw_wgrad_workspace_bytes(int N, int M, int K, int P);
 int bpk_gemm_nchw_wgrad_f32(const float* GY, const float* X, float* dW, float* db,
                             void* workspace, int N, int M, int K, int P, void* stream);
 
+/* General convolution (any KH x KW, stride, zero padding; groups = 1, dilation = 1) as
+ * implicit GEMM on the f32 MFMA: the forward, its adjoint (backward-data = conv transpose)
+ * and the weight (+ bias) gradient.  Replaces the cuDNN convolutions the reference runs
+ * for every conv the Winograd / small-channel / 1x1 kernels above do not take: the
+ * stride-2 convs of FIR downsampling (models/up_or_down_sampling.py:144-178, F.conv2d) and
+ * of the PINN feature pyramid (models/flownet.py:27-33), the PINN / CIFAR-10 3x3 convs at
+ * 2^2..8^2 and with Cin % 8 != 0 (flownet.py:42-58, 93-138), ConvTranspose2d
+ * (flownet.py:97, 229-231: forward == this dgrad), under loss.backward() and the PINN
+ * residual's create_graph derivatives (pinn_kalman/pinn.py:72-111).
+ *   x [N, Cin, H, W], w [Cout, Cin, KH, KW], y / gy [N, Cout, Ho, Wo] with
+ *   Ho = (H + 2 ph - KH) / sh + 1 (same for Wo); dw like w, db [Cout] or NULL.
+ * fwd: y = conv(x, w) + bias (bias NULL = none); dgrad: gx = conv^T(gy) (gx fully written);
+ * wgrad: dw (and db = sum over n, oy, ox of gy when db != NULL).  Split-K partials in a
+ * caller-provided workspace of workspace_bytes(mode 0 / 1 / 2, ..., bias_grad) bytes
+ * (0: none needed; -1: unsupported shape), summed in a fixed order (deterministic). */
+int64_t bpk_conv2d_igemm_workspace_bytes(int mode, int N, int Cin, int H, int W, int Cout,
+                                         int KH, int KW, int sh, int sw, int ph, int pw, int Ho,
+                                         int Wo, int bias_grad);
+int bpk_conv2d_igemm_fwd_f32(const float* x, const float* w, const float* bias, float* y,
+                             void* workspace, int N, int Cin, int H, int W, int Cout, int KH,
+                             int KW, int sh, int sw, int ph, int pw, int Ho, int Wo,
+                             void* stream);
+int bpk_conv2d_igemm_dgrad_f32(const float* gy, const float* w, float* gx, void* workspace,
+                               int N, int Cin, int H, int W, int Cout, int KH, int KW, int sh,
+                               int sw, int ph, int pw, int Ho, int Wo, void* stream);
+int bpk_conv2d_igemm_wgrad_f32(const float* x, const float* gy, float* dw, float* db,
+                               void* workspace, int N, int Cin, int H, int W, int Cout, int KH,
+                               int KW, int sh, int sw, int ph, int pw, int Ho, int Wo,
+                               void* stream);
+
 #ifdef __cplusplus
 }
 #endif

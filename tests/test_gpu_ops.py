@@ -900,3 +900,107 @@ def test_dispatcher_ops_equal_the_op_wrappers(hip):
     for u, w in zip(torch.ops.gridsample_grad2.grad2_2d(g2i, g2g, go, inp, grid, True, True),
                     grid_sample2d_grad2_raw(g2i, g2g, go, inp, grid, 1, True)):
         assert torch.allclose(u, w, rtol=0, atol=1e-12)
+
+
+# ------------------------------------------------ implicit-GEMM MFMA conv (conv_igemm.hip)
+_IG_CASES = [
+    # N, Cin, H, W, Cout, k, stride, pad
+    (3, 5, 7, 9, 6, 3, 1, 1),        # odd everything, generic edges
+    (2, 16, 16, 20, 32, 3, 2, 1),    # FlowNet pyramid stride-2 conv
+    (4, 8, 17, 17, 8, 3, 2, 0),      # FIR conv_downsample_2d (pad 0 after the FIR pad)
+    (2, 49, 8, 8, 128, 3, 1, 1),     # FlowNet corr_conv first conv (Cin 49)
+    (64, 258, 2, 2, 128, 3, 1, 1),   # refinement conv at 2^2 (split-K)
+    (16, 256, 8, 8, 256, 3, 1, 1),   # CIFAR 8^2 level
+    (8, 128, 4, 4, 256, 3, 1, 1),    # CIFAR 4^2 level
+    (2, 12, 6, 10, 20, 2, 2, 0),     # ConvTranspose2d(k2, s2) adjoint shape
+    (2, 6, 9, 9, 4, 4, 2, 1),        # flow_upsample k4 s2 p1
+    (3, 33, 5, 5, 17, 1, 1, 0),      # 1x1, non-multiple-of-16 channels
+    (2, 7, 11, 13, 5, 5, 1, 2),      # generic-kernel template (5x5)
+]
+
+
+@pytest.mark.parametrize("case", _IG_CASES)
+def test_conv2d_igemm_fwd_dgrad_wgrad_vs_fp64(hip, case):
+    """The implicit-GEMM kernels (forward + bias, backward-data, weight + bias gradient) vs
+    float64 F.conv2d on the CPU; fp32 MFMA (exact products, k-ordered fma chain): error
+    within 2e-5 of the output's magnitude (sums of up to ~2300 products; an indexing or
+    padding error shows up as O(1))."""
+    from op.conv import conv2d_igemm_raw, conv2d_input_igemm_raw, conv2d_weight_igemm_raw
+    N, C, H, W, Co, k, s, p = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5
+    b = torch.randn(Co, generator=g)
+    xd, wd, bd = (t.double().requires_grad_() for t in (x, w, b))
+    yref = F.conv2d(xd, wd, bd, s, p)
+    gy = torch.randn(yref.shape, generator=g)
+    gx_ref, gw_ref, gb_ref = torch.autograd.grad(yref, (xd, wd, bd), gy.double())
+
+    def close(got, ref, what):
+        ref = ref.detach()
+        tol = 2e-5 * max(1.0, float(ref.abs().max()))
+        err = float((got.double().cpu() - ref).abs().max())
+        assert err <= tol, f"{what}: {err} > {tol}"
+
+    y = conv2d_igemm_raw(x.to(hip), w.to(hip), b.to(hip), s, p)
+    close(y, yref, "forward")
+    gx = conv2d_input_igemm_raw(x.shape, w.to(hip), gy.to(hip), s, p)
+    close(gx, gx_ref, "dgrad")
+    dw, db = conv2d_weight_igemm_raw(x.to(hip), w.shape, gy.to(hip), s, p, bias_grad=True)
+    close(dw, gw_ref, "wgrad")
+    close(db, gb_ref, "bias grad")
+    dw2, none = conv2d_weight_igemm_raw(x.to(hip), w.shape, gy.to(hip), s, p, bias_grad=False)
+    assert none is None and torch.equal(dw2, dw)
+
+
+@pytest.mark.parametrize("k,stride,pad,cin,cout,hw", [(3, 2, 1, 3, 16, 12), (3, 1, 1, 49, 32, 4),
+                                                       (2, 2, 0, 8, 8, 6), (1, 1, 0, 5, 1, 7)])
+def test_conv2d_general_igemm_double_backward(hip, k, stride, pad, cin, cout, hw):
+    """conv2d_general on the implicit-GEMM kernels: forward, first derivatives with
+    create_graph and a second derivative w.r.t. (x, w, b) equal F.conv2d's (fp32 on the
+    device, both sides), as the PINN residual takes them."""
+    from op.conv import conv2d_general
+    g = torch.Generator().manual_seed(k * 7 + cin)
+    x0 = torch.randn(2, cin, hw, hw + 1, generator=g).to(hip)
+    w0 = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(hip)
+    b0 = torch.randn(cout, generator=g).to(hip)
+
+    def second(fn):
+        x, w, b = (t.clone().requires_grad_() for t in (x0, w0, b0))
+        y = fn(x, w, b)
+        (gx,) = torch.autograd.grad((y ** 2).sum(), x, create_graph=True)
+        loss = (gx * torch.sin(x)).sum() + y.mean()
+        return [y.detach()] + list(torch.autograd.grad(loss, (x, w, b)))
+
+    got = second(lambda x, w, b: conv2d_general(x, w, b, stride, pad))
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = second(lambda x, w, b: F.conv2d(x, w, b, stride, pad))
+    for a, r in zip(got, ref):
+        tol = 1e-4 * max(1.0, float(r.abs().max()))
+        assert float((a - r).abs().max()) <= tol
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p,op,groups", [(2, 2, 4, 2, 1, 0, 2), (32, 16, 2, 2, 0, 0, 1),
+                                                       (4, 6, 3, 2, 1, 1, 1)])
+def test_conv_transpose2d_general_vs_torch(hip, cin, cout, k, s, p, op, groups):
+    """layers.ConvTranspose2d (the dgrad kernel as the transposed conv, groups through a
+    block-diagonal dense weight): forward, input / weight / bias gradients and a second
+    derivative equal torch's ConvTranspose2d."""
+    import copy
+    import torch.nn as nn
+    from models import layers
+    torch.manual_seed(cin * 10 + k)
+    ref = nn.ConvTranspose2d(cin, cout, k, s, p, op, groups=groups).to(hip)
+    mod = layers.ConvTranspose2d(cin, cout, k, s, p, op, groups=groups).to(hip)
+    mod.load_state_dict(copy.deepcopy(ref.state_dict()))
+    x0 = torch.randn(3, cin, 5, 7, device=hip)
+    outs = []
+    for m in (mod, ref):
+        x = x0.clone().requires_grad_()
+        y = m(x)
+        (gx,) = torch.autograd.grad((y ** 2).sum(), x, create_graph=True)
+        loss = (gx * x).sum() + y.sum()
+        outs.append([y.detach()] + list(torch.autograd.grad(loss, [x] + list(m.parameters()))))
+    for a, r in zip(*outs):
+        assert a.shape == r.shape
+        assert float((a - r).abs().max()) <= 1e-4 * max(1.0, float(r.abs().max()))

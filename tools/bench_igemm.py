@@ -1,0 +1,100 @@
+"""Per-shape timing of the implicit-GEMM conv kernels (csrc/conv_igemm.hip) vs MIOpen on the
+shapes the PINN (configs[3]) and CIFAR-10 (configs[1]) train steps send them: one step of
+each is run with the igemm entry points wrapped to record (mode, shapes, stride, padding);
+then every distinct call is timed both ways (HIP events, 20 reps) and weighted by its count
+per step."""
+import collections
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
+import torch
+import torch.nn.functional as F
+
+import bench
+from dist import DistContext
+from op import conv as C
+
+dev = torch.device("cuda:0")
+rec = collections.Counter()
+orig = (C.conv2d_igemm_raw, C.conv2d_input_igemm_raw, C.conv2d_weight_igemm_raw)
+
+
+def r_fwd(x, w, bias=None, stride=1, padding=0):
+    rec[("fwd", tuple(x.shape), tuple(w.shape), C._pair(stride), C._pair(padding), bias is not None)] += 1
+    return orig[0](x, w, bias, stride, padding)
+
+
+def r_dgrad(xshape, w, gy, stride=1, padding=0):
+    rec[("dgrad", tuple(int(v) for v in xshape), tuple(w.shape), C._pair(stride), C._pair(padding), False)] += 1
+    return orig[1](xshape, w, gy, stride, padding)
+
+
+def r_wgrad(x, wshape, gy, stride=1, padding=0, bias_grad=False):
+    rec[("wgrad", tuple(x.shape), tuple(int(v) for v in wshape), C._pair(stride), C._pair(padding), bool(bias_grad))] += 1
+    return orig[2](x, wshape, gy, stride, padding, bias_grad)
+
+
+C.conv2d_igemm_raw, C.conv2d_input_igemm_raw, C.conv2d_weight_igemm_raw = r_fwd, r_dgrad, r_wgrad
+
+
+class A:
+    pass
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def measure(tag):
+    rows, tot_ig, tot_mi = [], 0.0, 0.0
+    for key, cnt in sorted(rec.items(), key=lambda kv: -kv[1]):
+        mode, xs, ws_, st, pd, hb = key
+        g = torch.Generator(device=dev).manual_seed(0)
+        w = torch.randn(ws_, device=dev, generator=g)
+        b = torch.randn(ws_[0], device=dev, generator=g) if hb else None
+        x = torch.randn(xs, device=dev, generator=g)
+        Ho = (xs[2] + 2 * pd[0] - ws_[2]) // st[0] + 1
+        Wo = (xs[3] + 2 * pd[1] - ws_[3]) // st[1] + 1
+        gy = torch.randn((xs[0], ws_[0], Ho, Wo), device=dev, generator=g)
+        if mode == "fwd":
+            fi = lambda: orig[0](x, w, b, st, pd)
+            fm = lambda: F.conv2d(x, w, b, st, pd)
+        elif mode == "dgrad":
+            fi = lambda: orig[1](xs, w, gy, st, pd)
+            fm = lambda: torch.nn.grad.conv2d_input(xs, w, gy, st, pd)
+        else:
+            fi = lambda: orig[2](x, ws_, gy, st, pd, hb)
+            fm = lambda: (torch.nn.grad.conv2d_weight(x, ws_, gy, st, pd), gy.sum((0, 2, 3)) if hb else None)
+        with torch.no_grad():
+            ti, tm = timeit(fi), timeit(fm)
+        flop = 2.0 * xs[0] * ws_[0] * ws_[1] * ws_[2] * ws_[3] * Ho * Wo
+        rows.append(dict(mode=mode, x=xs, w=ws_, stride=st, pad=pd, per_step=cnt, igemm_us=round(ti, 1),
+                         miopen_us=round(tm, 1), igemm_tflops=round(flop / ti / 1e6, 1)))
+        tot_ig += cnt * ti
+        tot_mi += cnt * tm
+    print(json.dumps(dict(workload=tag, igemm_ms_per_step=round(tot_ig / 1e3, 2),
+                          miopen_ms_per_step=round(tot_mi / 1e3, 2))), flush=True)
+    for r in rows:
+        print(json.dumps(r), flush=True)
+
+
+a = A()
+a.batch, a.pinn_warmup, a.pinn_steps, a.pinn_graph = 64, 0, 1, False
+bench.bench_pinn(a, DistContext(), dev)
+measure("pinn (configs[3], B=64, 64x64), one train step")
+rec.clear()
+a.cifar_steps = 1
+bench.bench_cifar_train(a, DistContext(), dev)
+measure("cifar10_ncsnpp (configs[1], B=128), one train step")

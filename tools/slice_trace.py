@@ -13,8 +13,10 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 if per_step == 0:  # infer: the marker's total count over warmup + steps
     per_step = len(idx) // (warmup + steps)
-assert len(idx) == per_step * (warmup + steps), (len(idx), per_step * (warmup + steps))
-lo = idx[per_step * warmup - 1] + 1
+# counted from the end: the last `steps` steps hold per_step * steps marker launches (extra
+# marker launches before the warm-up, e.g. an initialisation, do not shift the slice)
+assert len(idx) >= per_step * (warmup + steps), (len(idx), per_step * (warmup + steps))
+lo = idx[len(idx) - per_step * steps - 1] + 1
 sel = rows[lo:]
 agg = defaultdict(lambda: [0, 0])
 for r in sel:
