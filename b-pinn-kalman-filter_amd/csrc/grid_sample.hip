@@ -9,8 +9,9 @@
 // w.r.t. (grad_output, input, grid).  This is what makes the PINN residual's
 // second derivatives possible (pinn_kalman/pinn.py:89-92).
 //
-// One thread per output location (n, h, w) looping over channels, as the
-// reference does; grad_input accumulation uses hardware float atomics.
+// Forward: one thread per output location (n, h, w) looping over channels; backward and
+// double backward: each location's channels split over S threads (see gs_bwd); grad_input
+// accumulation uses hardware float atomics.
 #include "bpk_common.h"
 
 #include <algorithm>
@@ -116,28 +117,39 @@ __device__ inline void safe_add(T* base, int y, int x, int H, int W, T v) {
   if (inb(y, x, H, W)) atomicAdd(base + (int64_t)y * W + x, v);
 }
 
-template <typename T>
+// Backward: a block is P = 256 / S output locations x S channel slices (thread (p, s) runs
+// channels s, s + S, ...): S x the parallelism of one thread per location -- the PINN
+// warps [64, 16..128, 2..32, 2..32] feature maps, where a per-location channel loop of
+// atomics left the chip latency-bound (186 us per call).  grad_grid's channel sum is
+// combined over the slices in LDS in a fixed order.
+template <typename T, int S>
 __global__ __launch_bounds__(256) void gs_bwd(const T* __restrict__ gout,
                                               const T* __restrict__ inp,
                                               const T* __restrict__ grid, T* grad_inp,
                                               T* __restrict__ grad_grid, int N, int C, int H, int W,
                                               int Ho, int Wo, int padding, int align) {
+  constexpr int P = 256 / S;
+  __shared__ T red[2][S][P];
+  const int lp = threadIdx.x % P, sl = threadIdx.x / P;
   const int64_t total = (int64_t)N * Ho * Wo;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t idx = (int64_t)blockIdx.x * P + lp;
+  const bool valid = idx < total;
+  T gix = T(0), giy = T(0);
+  Corners<T> q{};
+  if (valid) {
     const int w = (int)(idx % Wo);
     const int h = (int)((idx / Wo) % Ho);
     const int64_t n = idx / ((int64_t)Ho * Wo);
     const T gx = grid[idx * 2], gy = grid[idx * 2 + 1];
-    const Corners<T> q = corners(gx, gy, H, W, padding, align != 0);
-    const T* ip = inp + n * C * H * W;
-    T* gp = grad_inp ? grad_inp + n * C * H * W : nullptr;
-    const T* go = gout + n * C * Ho * Wo + (int64_t)h * Wo + w;
-    T gix = T(0), giy = T(0);
-    for (int c = 0; c < C; ++c, ip += (int64_t)H * W, go += (int64_t)Ho * Wo) {
+    q = corners(gx, gy, H, W, padding, align != 0);
+    const int64_t hw = (int64_t)H * W, howo = (int64_t)Ho * Wo;
+    const T* ip = inp + n * C * hw + sl * hw;
+    T* gp = grad_inp ? grad_inp + n * C * hw + sl * hw : nullptr;
+    const T* go = gout + n * C * howo + (int64_t)h * Wo + w + sl * howo;
+    for (int c = sl; c < C; c += S, ip += S * hw, go += S * howo) {
       const T g = *go;
       if (gp) {
-        T* gpc = gp + (int64_t)c * H * W;
+        T* gpc = gp + (int64_t)(c - sl) * hw;
         safe_add(gpc, q.iy_nw, q.ix_nw, H, W, q.nw * g);
         safe_add(gpc, q.iy_ne, q.ix_ne, H, W, q.ne * g);
         safe_add(gpc, q.iy_sw, q.ix_sw, H, W, q.sw * g);
@@ -166,28 +178,46 @@ __global__ __launch_bounds__(256) void gs_bwd(const T* __restrict__ gout,
         }
       }
     }
-    if (grad_grid) {
-      grad_grid[idx * 2] = q.gix_mult * gix;
-      grad_grid[idx * 2 + 1] = q.giy_mult * giy;
+  }
+  if (!grad_grid) return;
+  if (S > 1) {
+    red[0][sl][lp] = gix;
+    red[1][sl][lp] = giy;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      gix += red[0][k][lp];
+      giy += red[1][k][lp];
     }
+  }
+  if (valid) {
+    grad_grid[idx * 2] = q.gix_mult * gix;
+    grad_grid[idx * 2 + 1] = q.giy_mult * giy;
   }
 }
 
-// op/grid_sample_kernel.cu:27-210
-template <typename T>
+// op/grid_sample_kernel.cu:27-210; P output locations x S channel slices per block as gs_bwd
+template <typename T, int S>
 __global__ __launch_bounds__(256) void gs_grad2(
     const T* __restrict__ g2_inp, const T* __restrict__ g2_grid, const T* __restrict__ gout,
     const T* __restrict__ inp, const T* __restrict__ grid, T* __restrict__ gg_out, T* grad_inp,
     T* __restrict__ grad_grid, int N, int C, int H, int W, int Ho, int Wo, int padding,
     int align) {
+  constexpr int P = 256 / S;
+  __shared__ T red[2][S][P];
+  const int lp = threadIdx.x % P, sl = threadIdx.x / P;
   const int64_t total = (int64_t)N * Ho * Wo;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t idx = (int64_t)blockIdx.x * P + lp;
+  const bool valid = idx < total;
+  T gix = T(0), giy = T(0);
+  Corners<T> q{};
+  if (valid) {
     const int w = (int)(idx % Wo);
     const int h = (int)((idx / Wo) % Ho);
     const int64_t n = idx / ((int64_t)Ho * Wo);
     const T gx = grid[idx * 2], gy = grid[idx * 2 + 1];
-    const Corners<T> q = corners(gx, gy, H, W, padding, align != 0);
+    q = corners(gx, gy, H, W, padding, align != 0);
     const T dx = g2_grid[idx * 2] * q.gix_mult;
     const T dy = g2_grid[idx * 2 + 1] * q.giy_mult;
     const T* ip = inp + n * C * H * W;
@@ -200,8 +230,7 @@ __global__ __launch_bounds__(256) void gs_grad2(
     const T ne_tmp = +dx * (q.iy_sw - q.iy) - dy * (q.ix - q.ix_sw);
     const T sw_tmp = -dx * (q.iy - q.iy_ne) + dy * (q.ix_ne - q.ix);
     const T se_tmp = +dx * (q.iy - q.iy_nw) + dy * (q.ix - q.ix_nw);
-    T gix = T(0), giy = T(0);
-    for (int c = 0; c < C; ++c) {
+    for (int c = sl; c < C; c += S) {
       const int64_t pc = (int64_t)c * H * W;
       const T nw_v = b_nw ? ip[pc + q.iy_nw * W + q.ix_nw] : T(0);
       const T ne_v = b_ne ? ip[pc + q.iy_ne * W + q.ix_ne] : T(0);
@@ -229,10 +258,26 @@ __global__ __launch_bounds__(256) void gs_grad2(
                   g2_se * (q.ix - q.ix_nw));
       giy += g * dx * dxy;
     }
+  }
+  if (S > 1) {
+    red[0][sl][lp] = gix;
+    red[1][sl][lp] = giy;
+    __syncthreads();
+    if (sl != 0) return;
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      gix += red[0][k][lp];
+      giy += red[1][k][lp];
+    }
+  }
+  if (valid) {
     grad_grid[idx * 2] = gix * q.gix_mult;
     grad_grid[idx * 2 + 1] = giy * q.giy_mult;
   }
 }
+
+// channel slices per block: S x the threads of one-per-location where C allows
+inline int slices_for(int C) { return C >= 16 ? 8 : (C >= 4 ? 4 : 1); }
 
 unsigned blocks_for(int64_t total) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(bpk::ceil_div(total, 256), 256 * 32));
@@ -263,9 +308,12 @@ int bwd_impl(const T* gout, const T* input, const T* grid, T* gin, T* ggrid, int
   GS_CHECK();
   const int64_t total = (int64_t)N * H_out * W_out;
   if (total == 0) return BPK_OK;
-  hipLaunchKernelGGL(gs_bwd<T>, dim3(blocks_for(total)), dim3(256), 0, bpk::as_stream(stream),
-                     gout, input, grid, gin, ggrid, N, C, H_in, W_in, H_out, W_out, padding_mode,
-                     align_corners);
+  const int S = slices_for(C);
+  const unsigned blocks = (unsigned)bpk::ceil_div(total, 256 / S);
+  BPK_REQUIRE(bpk::ceil_div(total, 256 / S) < (1ll << 31), "grid_sample2d_bwd: too many locations");
+  auto k = S == 8 ? gs_bwd<T, 8> : (S == 4 ? gs_bwd<T, 4> : gs_bwd<T, 1>);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, bpk::as_stream(stream), gout, input, grid,
+                     gin, ggrid, N, C, H_in, W_in, H_out, W_out, padding_mode, align_corners);
   BPK_LAUNCH_CHECK("grid_sample2d_bwd");
   return BPK_OK;
 }
@@ -278,9 +326,13 @@ int grad2_impl(const T* g2i, const T* g2g, const T* gout, const T* input, const 
   BPK_REQUIRE(ggo && gin && ggrid, "grid_sample2d_grad2: all outputs required");
   const int64_t total = (int64_t)N * H_out * W_out;
   if (total == 0) return BPK_OK;
-  hipLaunchKernelGGL(gs_grad2<T>, dim3(blocks_for(total)), dim3(256), 0, bpk::as_stream(stream),
-                     g2i, g2g, gout, input, grid, ggo, gin, ggrid, N, C, H_in, W_in, H_out, W_out,
-                     padding_mode, align_corners);
+  const int S = slices_for(C);
+  const unsigned blocks = (unsigned)bpk::ceil_div(total, 256 / S);
+  BPK_REQUIRE(bpk::ceil_div(total, 256 / S) < (1ll << 31), "grid_sample2d_grad2: too many locations");
+  auto k = S == 8 ? gs_grad2<T, 8> : (S == 4 ? gs_grad2<T, 4> : gs_grad2<T, 1>);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, bpk::as_stream(stream), g2i, g2g, gout, input,
+                     grid, ggo, gin, ggrid, N, C, H_in, W_in, H_out, W_out, padding_mode,
+                     align_corners);
   BPK_LAUNCH_CHECK("grid_sample2d_grad2");
   return BPK_OK;
 }

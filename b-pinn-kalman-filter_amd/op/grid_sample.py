@@ -78,6 +78,9 @@ class _GridSample2dForward(torch.autograd.Function):
         assert input.ndim == 4 and grid.ndim == 4
         assert input.shape[0] == grid.shape[0] and grid.shape[3] == 2
         pm = _PADDING[padding_mode]
+        # the callers' grids are NHWC views of NCHW tensors (flownet.project): made dense
+        # once here and saved dense, not copied again by each backward / double backward
+        input, grid = input.contiguous(), grid.contiguous()
         out = grid_sample2d_fwd_raw(input, grid, pm, align_corners)
         ctx.save_for_backward(input, grid)
         ctx.padding_mode, ctx.align_corners = pm, align_corners
@@ -96,6 +99,7 @@ class _GridSample2dBackward(torch.autograd.Function):
     def forward(ctx, grad_output, input, grid, padding_mode=0, align_corners=True):
         need_in = ctx.needs_input_grad[1]
         need_grid = ctx.needs_input_grad[2]
+        grad_output = grad_output.contiguous()
         gi, gg = grid_sample2d_bwd_raw(grad_output, input, grid, padding_mode, align_corners,
                                        True, True)
         ctx.save_for_backward(grad_output, input, grid)
