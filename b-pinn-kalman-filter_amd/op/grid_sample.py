@@ -78,9 +78,6 @@ class _GridSample2dForward(torch.autograd.Function):
         assert input.ndim == 4 and grid.ndim == 4
         assert input.shape[0] == grid.shape[0] and grid.shape[3] == 2
         pm = _PADDING[padding_mode]
-        # the callers' grids are NHWC views of NCHW tensors (flownet.project): made dense
-        # once here and saved dense, not copied again by each backward / double backward
-        input, grid = input.contiguous(), grid.contiguous()
         out = grid_sample2d_fwd_raw(input, grid, pm, align_corners)
         ctx.save_for_backward(input, grid)
         ctx.padding_mode, ctx.align_corners = pm, align_corners
@@ -89,8 +86,8 @@ class _GridSample2dForward(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         input, grid = ctx.saved_tensors
-        gi, gg = _GridSample2dBackward.apply(grad_output, input, grid, ctx.padding_mode,
-                                             ctx.align_corners)
+        gi, gg = _GridSample2dBackward.apply(grad_output.contiguous(), input, grid,
+                                             ctx.padding_mode, ctx.align_corners)
         return gi, gg, None, None
 
 
@@ -99,7 +96,6 @@ class _GridSample2dBackward(torch.autograd.Function):
     def forward(ctx, grad_output, input, grid, padding_mode=0, align_corners=True):
         need_in = ctx.needs_input_grad[1]
         need_grid = ctx.needs_input_grad[2]
-        grad_output = grad_output.contiguous()
         gi, gg = grid_sample2d_bwd_raw(grad_output, input, grid, padding_mode, align_corners,
                                        True, True)
         ctx.save_for_backward(grad_output, input, grid)
@@ -122,7 +118,14 @@ class _GridSample2dBackward(torch.autograd.Function):
 def grid_sample_2d(input, grid, padding_mode="zeros", align_corners=True):
     assert padding_mode in ["zeros", "border"]
     require_hip(input, grid, what="grid_sample_2d")
-    return _GridSample2dForward.apply(input, grid, padding_mode, align_corners)
+    # The callers' grids are NHWC views of NCHW tensors (flownet.project): made dense once
+    # here, as a recorded (differentiable) copy, so the Functions save dense tensors that are
+    # not copied again by each backward / double backward.  The copy must stay OUTSIDE the
+    # Functions: a tensor made inside forward and saved is cut from the graph, and the
+    # double backward's grad_grid / grad_input (the PINN residual's second-order terms
+    # through the warp) would silently vanish -- likewise grad_output above.
+    return _GridSample2dForward.apply(input.contiguous(), grid.contiguous(), padding_mode,
+                                      align_corners)
 
 
 def _fns3(dtype):

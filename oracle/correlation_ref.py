@@ -7,7 +7,8 @@ tensors allocated :296-306); the forward is `kernel_Correlation_updateOutput`
 (dy+3)*7 + (dx+3), output ceil(H/s) x ceil(W/s), :317-321); the grads follow
 `kernel_Correlation_updateGrad{First,Second}` (:104-231) including their
 ceil/floor range arithmetic.  Sums are accumulated in float64 and rounded once,
-so GPU results are compared with a float32 tolerance.  No runnable reference
+so GPU results are compared with a float32 tolerance (float64 inputs give float64 outputs:
+the float64-truth fixtures, tests/golden/make_golden_pinn_f64.py).  No runnable reference
 exists here (CuPy/CUDA only): pinned by known-answer tests in tests/test_oracle.py.
 """
 from __future__ import annotations
@@ -18,6 +19,10 @@ import numpy as np
 def _pad(a, s):
     p = 3 * s
     return np.pad(a.astype(np.float64), ((0, 0), (0, 0), (p, p), (p, p)))
+
+
+def _out_dtype(a):
+    return np.float64 if a.dtype == np.float64 else np.float32
 
 
 def forward(first, second, stride=1):
@@ -34,7 +39,7 @@ def forward(first, second, stride=1):
         s2p = (tc // 7 - 3) * s
         b = f2[:, :, ys + s2p][:, :, :, xs + s2o]
         out[:, tc] = (a * b).sum(1) / C
-    return out.astype(np.float32)
+    return out.astype(_out_dtype(first))
 
 
 def backward(first, second, gout, stride=1):
@@ -71,4 +76,4 @@ def backward(first, second, gout, stride=1):
                     op = (p + 3) * 7 + (o + 3)
                     acc += g[:, op, oy, ox][:, None] * f1[:, :, yo + 3 * s, xo + 3 * s]
             gs[:, :, m0, l0] = acc / C
-    return gf.astype(np.float32), gs.astype(np.float32)
+    return gf.astype(_out_dtype(first)), gs.astype(_out_dtype(first))

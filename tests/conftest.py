@@ -164,6 +164,34 @@ def record_err(what, err, tol):
     _PARITY.append({"what": what, "err": float(err), "tol": float(tol)})
 
 
+def param_grads_vs_truth(model, d32, d64, tol=5e-3):
+    """Parameter gradients of equation_mse vs the reference's float64 truth
+    (tests/golden/make_golden_pinn_f64.py).  Per tensor, relative to max(|truth|,
+    1e-4 x the largest gradient):  err(ours) <= max(tol, 2 x err(reference float32)) --
+    no worse than the reference's own float32 arithmetic up to a factor 2 (several of
+    these gradients are third-order quantities or mathematically zero, i.e. pure
+    rounding).  Every tensor is checked before failing.  Returns (worst, name, n)."""
+    import numpy as np
+    gscale = max(np.abs(d64[k]).max() for k in d64.files if k.startswith("g:"))
+    worst, wname, n, bad = 0.0, "", 0, []
+    for k, p in model.named_parameters():
+        if "g:" + k not in d64.files:
+            continue
+        truth = np.asarray(d64["g:" + k], np.float64)
+        fl = max(np.abs(truth).max(), 1e-4 * gscale)
+        v = p.grad.reshape(-1).cpu().numpy()[sample_idx(p.numel())].astype(np.float64)
+        e = float(np.abs(v - truth).max() / fl)
+        e_ref = float(np.abs(d32["g:" + k].astype(np.float64) - truth).max() / fl)
+        lim = max(tol, 2 * e_ref)
+        if e / lim > worst:
+            worst, wname = e / lim, k
+        if e > lim:
+            bad.append(f"{k}: {e:.3e} (reference float32 {e_ref:.3e})")
+        n += 1
+    assert not bad, f"{len(bad)} parameter gradients off the float64 truth: {bad[:8]}"
+    return worst, wname, n
+
+
 def pytest_sessionfinish(session, exitstatus):
     out = os.path.join(REPO, "gpurun_out")
     if _PARITY and os.path.isdir(out):

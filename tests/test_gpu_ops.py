@@ -237,6 +237,26 @@ def test_grid_sample_double_backward_gradgradcheck(hip):
     assert torch.autograd.gradgradcheck(f, (inp, grid))
 
 
+def test_grid_sample_double_backward_noncontiguous_views(hip):
+    """As flownet.project calls it: the grid an NHWC permute of an NCHW flow, the input a
+    channel slice -- both non-contiguous.  A dense copy made inside the Function and saved
+    would cut the double backward's grad_grid / grad_input from the graph (caught by the
+    float64-truth PINN fixtures); gradgradcheck through the views pins that it flows."""
+    from op.grid_sample import grid_sample_2d
+    torch.manual_seed(4)
+    base = torch.randn(2, 4, 5, 6, dtype=torch.float64, device=hip, requires_grad=True)
+    flow = (torch.rand(2, 2, 3, 4, dtype=torch.float64, device=hip) * 1.6 - 0.8).requires_grad_(True)
+
+    def f(b, fl):
+        inp = b[:, 1:3]                  # channel slice: non-contiguous
+        g = (fl * 0.9).permute(0, 2, 3, 1)  # NHWC view of NCHW
+        assert not inp.is_contiguous() and not g.is_contiguous()
+        return grid_sample_2d(inp, g, "border", True)
+
+    assert torch.autograd.gradcheck(f, (base, flow))
+    assert torch.autograd.gradgradcheck(f, (base, flow))
+
+
 # ------------------------------------------------------------------ Winograd conv3x3
 @pytest.mark.parametrize("N,cin,cout,hw", [(1, 8, 128, 16), (3, 24, 128, 32), (2, 128, 256, 64),
                                            (2, 256, 128, 16), (1, 512, 256, 32),
