@@ -108,6 +108,21 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 // pre[n][cin] = (s, t) (bpk_group_norm_affine_f32): the patch load applies silu(x s + t)
 // (zero padding stays zero), so the normalized tensor is never written to HBM.
 // fast exp / reciprocal: a few ulp, far inside the network tolerance (1e-4)
+// Pipelined kernel's instruction schedule (A/B switch): 0 = side work fenced off between
+// the MFMA groups, 1 = free (compiler), 2 = interleaved, WINO_VPM VALU per MFMA
+#ifndef WINO_SCHED
+#define WINO_SCHED 0
+#endif
+#ifndef WINO_STAGGER
+#define WINO_STAGGER 0
+#endif
+#ifndef WINO_STAGGER_MODE
+#define WINO_STAGGER_MODE 0
+#endif
+#ifndef WINO_VPM
+#define WINO_VPM 4
+#endif
+
 __device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 
 // q = a / d, r = a % d for a block index: a shift when d is a power of two (every NCSN++ /
@@ -450,6 +465,14 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   // grid < 2^31 blocks (host check): 32-bit block arithmetic
   const unsigned nblk = gridDim.x;
   unsigned b = blockIdx.x;
+#if WINO_STAGGER > 0
+  // first-round stagger (A/B): the two workgroups resident on a CU otherwise start, and
+  // keep running, in phase -- both in prologue / epilogue at once
+  if (nblk >= 1024 && (WINO_STAGGER_MODE == 0 ? (b >= 256u && b < 512u)
+                                               : (b < 512u && ((b >> 3) & 1u)))) {
+    for (int i = 0; i < WINO_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
   unsigned cb, rx, ry;
   unsigned r = udivmod(b, (unsigned)g.cout_blocks, cb);
@@ -611,12 +634,16 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
     for (int grp = 0; grp < 4; ++grp) {
       const int ks = grp >> 1, mb = grp & 1;
       // side work of the next chunks, spread over the four MFMA groups
+#if WINO_SCHED == 0 || WINO_SCHED == 4
       __builtin_amdgcn_sched_barrier(0);
+#endif
       if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                // patch(k+1)
       if (grp == 1) write_v(s_v[SB ^ 1]);                       // V(k+1)
       if (grp == 2) store_patch(s_patch_raw[SB], k + 2);        // patch(k+2)
       if (grp == 3) load_patch(k + 3);
+#if WINO_SCHED == 0
       __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -639,6 +666,19 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
           }
         }
       }
+#if WINO_SCHED >= 2
+      // the group's side work interleaved into its MFMA stream: each MFMA's 32-cycle
+      // issue shadow covers a few of the wave's own VALU / LDS instructions
+#pragma unroll
+      for (int i = 0; i < 16 * NB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, WINO_VPM, 0);  // VALU
+#if WINO_SCHED == 2
+        __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);  // DS
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM
+#endif
+      }
+#endif
     }
     __syncthreads();
     {

@@ -1,0 +1,246 @@
+// InstanceNorm2d (affine=False) + ELU(alpha=1), twice differentiable, for PressureNet's
+// ResidualBlocks (reference models/layers.py:438-491: conv(act(normalize(x))) with
+// normalization=nn.InstanceNorm2d, act=nn.ELU()).
+//
+// The PINN residual differentiates PressureNet w.r.t. its inputs with create_graph=True and
+// then backpropagates through that derivative, so each norm+act runs forward, backward and
+// double backward every step.  On aten that is batch_norm statistics / transform, the ELU,
+// native_batch_norm_backward, elu_backward and a composite batchnorm double backward of
+// ~25 small kernels per norm; here it is one kernel per order.
+//
+// Per plane p = (n, c) of M = H*W elements: mu = mean(x), r = 1 / sqrt(var + eps) (biased
+// variance), z = (x - mu) r, y = e(z) with e = ELU (act = 1) or identity (act = 0).
+//   backward     g = dy e'(z);  dx = r (g - mean(g) - z mean(g z))
+//   double bwd   for v = dL/d(dx):  w = r (v - mean(v) - z mean(v z))
+//                d/d(dy) = w e'(z)
+//                q = dy e''(z) w - r (g mean(v z) + v mean(g z))
+//                S = mean(g v) - mean(g) mean(v) - mean(g z) mean(v z)
+//                d/dx = r (q - mean(q) - z mean(q z)) - r^2 z S
+// (derivation: DESIGN.md section 4b; e'(z) = exp(z), e''(z) = exp(z) for z <= 0, else 1, 0,
+// the branch aten's elu_backward takes at z = 0.)
+//
+// One wave per plane (4 planes per 256-thread block): reductions are lane-strided sums in a
+// fixed order followed by a butterfly, so results are deterministic; no LDS, no barriers.
+#include "bpk_common.h"
+
+#include <cmath>
+
+namespace {
+
+constexpr int kWaves = 4;
+
+template <typename T>
+__device__ inline T wsum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ inline T act_f(T z, int act) {
+  if (!act) return z;
+  return z <= T(0) ? expm1(z) : z;
+}
+template <typename T>
+__device__ inline T act_d1(T z, int act) {
+  if (!act) return T(1);
+  return z <= T(0) ? exp(z) : T(1);
+}
+template <typename T>
+__device__ inline T act_d2(T z, int act) {
+  if (!act) return T(0);
+  return z <= T(0) ? exp(z) : T(0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void in_fwd(const T* __restrict__ x, T* __restrict__ y,
+                                              T* __restrict__ mean, T* __restrict__ rstd,
+                                              int64_t planes, int64_t M, T eps, int act) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (p >= planes) return;
+  const T* xp = x + p * M;
+  T s = T(0);
+  for (int64_t i = lane; i < M; i += 64) s += xp[i];
+  const T mu = wsum(s) / T(M);
+  T s2 = T(0);
+  for (int64_t i = lane; i < M; i += 64) {
+    const T d = xp[i] - mu;
+    s2 += d * d;
+  }
+  const T r = T(1) / sqrt(wsum(s2) / T(M) + eps);
+  T* yp = y + p * M;
+  for (int64_t i = lane; i < M; i += 64) yp[i] = act_f((xp[i] - mu) * r, act);
+  if (lane == 0) {
+    mean[p] = mu;
+    rstd[p] = r;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void in_bwd(const T* __restrict__ dy, const T* __restrict__ x,
+                                              const T* __restrict__ mean,
+                                              const T* __restrict__ rstd, T* __restrict__ dx,
+                                              int64_t planes, int64_t M, int act) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (p >= planes) return;
+  const T* xp = x + p * M;
+  const T* dp = dy + p * M;
+  const T mu = mean[p], r = rstd[p];
+  T sg = T(0), sgz = T(0);
+  for (int64_t i = lane; i < M; i += 64) {
+    const T z = (xp[i] - mu) * r;
+    const T g = dp[i] * act_d1(z, act);
+    sg += g;
+    sgz += g * z;
+  }
+  const T mg = wsum(sg) / T(M), mgz = wsum(sgz) / T(M);
+  T* op = dx + p * M;
+  for (int64_t i = lane; i < M; i += 64) {
+    const T z = (xp[i] - mu) * r;
+    const T g = dp[i] * act_d1(z, act);
+    op[i] = r * (g - mg - z * mgz);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void in_bwd2(const T* __restrict__ v, const T* __restrict__ dy,
+                                               const T* __restrict__ x,
+                                               const T* __restrict__ mean,
+                                               const T* __restrict__ rstd, T* __restrict__ gdy,
+                                               T* __restrict__ gx, int64_t planes, int64_t M,
+                                               int act) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (p >= planes) return;
+  const T* xp = x + p * M;
+  const T* dp = dy + p * M;
+  const T* vp = v + p * M;
+  const T mu = mean[p], r = rstd[p];
+  // pass 1: mean(v), mean(v z), mean(g), mean(g z), mean(g v)
+  T sv = T(0), svz = T(0), sg = T(0), sgz = T(0), sgv = T(0);
+  for (int64_t i = lane; i < M; i += 64) {
+    const T z = (xp[i] - mu) * r;
+    const T g = dp[i] * act_d1(z, act);
+    const T vi = vp[i];
+    sv += vi;
+    svz += vi * z;
+    sg += g;
+    sgz += g * z;
+    sgv += g * vi;
+  }
+  const T inv = T(1) / T(M);
+  const T mv = wsum(sv) * inv, mvz = wsum(svz) * inv, mg = wsum(sg) * inv;
+  const T mgz = wsum(sgz) * inv, mgv = wsum(sgv) * inv;
+  const T S = mgv - mg * mv - mgz * mvz;
+  // pass 2: mean(q), mean(q z)  (only when d/dx is wanted)
+  T mq = T(0), mqz = T(0);
+  if (gx) {
+    T sq = T(0), sqz = T(0);
+    for (int64_t i = lane; i < M; i += 64) {
+      const T z = (xp[i] - mu) * r;
+      const T d1 = act_d1(z, act);
+      const T g = dp[i] * d1;
+      const T vi = vp[i];
+      const T w = r * (vi - mv - z * mvz);
+      const T q = dp[i] * act_d2(z, act) * w - r * (g * mvz + vi * mgz);
+      sq += q;
+      sqz += q * z;
+    }
+    mq = wsum(sq) * inv;
+    mqz = wsum(sqz) * inv;
+  }
+  // pass 3: outputs
+  for (int64_t i = lane; i < M; i += 64) {
+    const T z = (xp[i] - mu) * r;
+    const T d1 = act_d1(z, act);
+    const T vi = vp[i];
+    const T w = r * (vi - mv - z * mvz);
+    if (gdy) gdy[p * M + i] = w * d1;
+    if (gx) {
+      const T g = dp[i] * d1;
+      const T q = dp[i] * act_d2(z, act) * w - r * (g * mvz + vi * mgz);
+      gx[p * M + i] = r * (q - mq - z * mqz) - r * r * z * S;
+    }
+  }
+}
+
+unsigned blocks_for(int64_t planes) { return (unsigned)bpk::ceil_div(planes, kWaves); }
+
+#define IN_CHECK(what)                                                                   \
+  BPK_REQUIRE(planes >= 0 && M > 0, "%s: bad geometry planes=%lld M=%lld", what,         \
+              (long long)planes, (long long)M);                                          \
+  BPK_REQUIRE(act == 0 || act == 1, "%s: act must be 0 (none) or 1 (ELU), got %d", what, act); \
+  BPK_REQUIRE(bpk::ceil_div(planes, kWaves) < (1ll << 31), "%s: too many planes", what)
+
+template <typename T>
+int fwd_impl(const T* x, T* y, T* mean, T* rstd, int64_t planes, int64_t M, double eps, int act,
+             void* stream) {
+  IN_CHECK("instance_norm_act_fwd");
+  BPK_REQUIRE(x && y && mean && rstd, "instance_norm_act_fwd: null pointer");
+  if (planes == 0) return BPK_OK;
+  hipLaunchKernelGGL(in_fwd<T>, dim3(blocks_for(planes)), dim3(256), 0, bpk::as_stream(stream),
+                     x, y, mean, rstd, planes, M, (T)eps, act);
+  BPK_LAUNCH_CHECK("instance_norm_act_fwd");
+  return BPK_OK;
+}
+
+template <typename T>
+int bwd_impl(const T* dy, const T* x, const T* mean, const T* rstd, T* dx, int64_t planes,
+             int64_t M, int act, void* stream) {
+  IN_CHECK("instance_norm_act_bwd");
+  BPK_REQUIRE(dy && x && mean && rstd && dx, "instance_norm_act_bwd: null pointer");
+  if (planes == 0) return BPK_OK;
+  hipLaunchKernelGGL(in_bwd<T>, dim3(blocks_for(planes)), dim3(256), 0, bpk::as_stream(stream),
+                     dy, x, mean, rstd, dx, planes, M, act);
+  BPK_LAUNCH_CHECK("instance_norm_act_bwd");
+  return BPK_OK;
+}
+
+template <typename T>
+int bwd2_impl(const T* v, const T* dy, const T* x, const T* mean, const T* rstd, T* gdy, T* gx,
+              int64_t planes, int64_t M, int act, void* stream) {
+  IN_CHECK("instance_norm_act_bwd2");
+  BPK_REQUIRE(v && dy && x && mean && rstd, "instance_norm_act_bwd2: null input pointer");
+  if (planes == 0 || (!gdy && !gx)) return BPK_OK;
+  hipLaunchKernelGGL(in_bwd2<T>, dim3(blocks_for(planes)), dim3(256), 0, bpk::as_stream(stream),
+                     v, dy, x, mean, rstd, gdy, gx, planes, M, act);
+  BPK_LAUNCH_CHECK("instance_norm_act_bwd2");
+  return BPK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bpk_instance_norm_act_fwd_f32(const float* x, float* y, float* mean, float* rstd,
+                                  int64_t planes, int64_t M, double eps, int act, void* stream) {
+  return fwd_impl(x, y, mean, rstd, planes, M, eps, act, stream);
+}
+int bpk_instance_norm_act_fwd_f64(const double* x, double* y, double* mean, double* rstd,
+                                  int64_t planes, int64_t M, double eps, int act, void* stream) {
+  return fwd_impl(x, y, mean, rstd, planes, M, eps, act, stream);
+}
+int bpk_instance_norm_act_bwd_f32(const float* dy, const float* x, const float* mean,
+                                  const float* rstd, float* dx, int64_t planes, int64_t M, int act,
+                                  void* stream) {
+  return bwd_impl(dy, x, mean, rstd, dx, planes, M, act, stream);
+}
+int bpk_instance_norm_act_bwd_f64(const double* dy, const double* x, const double* mean,
+                                  const double* rstd, double* dx, int64_t planes, int64_t M,
+                                  int act, void* stream) {
+  return bwd_impl(dy, x, mean, rstd, dx, planes, M, act, stream);
+}
+int bpk_instance_norm_act_bwd2_f32(const float* v, const float* dy, const float* x,
+                                   const float* mean, const float* rstd, float* gdy, float* gx,
+                                   int64_t planes, int64_t M, int act, void* stream) {
+  return bwd2_impl(v, dy, x, mean, rstd, gdy, gx, planes, M, act, stream);
+}
+int bpk_instance_norm_act_bwd2_f64(const double* v, const double* dy, const double* x,
+                                   const double* mean, const double* rstd, double* gdy, double* gx,
+                                   int64_t planes, int64_t M, int act, void* stream) {
+  return bwd2_impl(v, dy, x, mean, rstd, gdy, gx, planes, M, act, stream);
+}
+
+}  // extern "C"

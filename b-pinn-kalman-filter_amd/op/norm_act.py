@@ -5,12 +5,15 @@ These are the build's fusions of the NCSN++/DDPM++ block arithmetic
   * `group_norm_act(x, gn, act, bias_nc)`  = act(GroupNorm(x + bias_nc[:, :, None, None]))
     -- one HIP launch (csrc/group_norm.hip) instead of add + group_norm + silu;
   * `residual_rescale(x, h, bias, div)`    = (x + (h + bias[c])) / div
-    -- folds Conv_1's bias and the skip connection into one pass.
+    -- folds Conv_1's bias and the skip connection into one pass;
+  * `instance_norm_act(x)` = ELU(InstanceNorm2d(x)) of PressureNet's ResidualBlock
+    (models/layers.py:438-491), forward / backward / double backward one kernel each.
 """
 from __future__ import annotations
 
 import torch
 from torch.autograd import Function
+from torch.autograd.function import once_differentiable
 
 from ._lib import check, lib, require_hip, stream_ptr, mark_inputs, want_grad
 
@@ -167,3 +170,88 @@ class _Residual(Function):
 
 def residual_rescale(x, h, bias=None, div=2 ** 0.5):
     return _Residual.apply(x, h, bias, div)
+
+
+# ------------------------------------------------ InstanceNorm2d + ELU, twice differentiable
+
+ACT_ELU = 1
+
+
+def _in_fns(dtype):
+    if dtype == torch.float32:
+        return (lib.bpk_instance_norm_act_fwd_f32, lib.bpk_instance_norm_act_bwd_f32,
+                lib.bpk_instance_norm_act_bwd2_f32)
+    if dtype == torch.float64:
+        return (lib.bpk_instance_norm_act_fwd_f64, lib.bpk_instance_norm_act_bwd_f64,
+                lib.bpk_instance_norm_act_bwd2_f64)
+    raise RuntimeError(f"instance_norm_act: float32 / float64 only, got {dtype}")
+
+
+def _planes(x):
+    if x.dim() < 3:
+        raise RuntimeError(f"instance_norm_act: expected [N, C, ...], got {tuple(x.shape)}")
+    return x.shape[0] * x.shape[1], x[0, 0].numel()
+
+
+class _InstanceNormAct(Function):
+    """y = act(InstanceNorm(x)) (affine=False, instance statistics).  Its backward is
+    _InstanceNormActBackward, whose own backward is the analytic double backward -- the
+    PINN residual's second derivatives through PressureNet (csrc/instance_norm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, eps, act):
+        require_hip(x, what="instance_norm_act")
+        P, M = _planes(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(P, device=x.device, dtype=x.dtype)
+        rstd = torch.empty_like(mean)
+        check(_in_fns(x.dtype)[0](x.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                  P, M, float(eps), act, stream_ptr(x.device)),
+              "instance_norm_act_fwd")
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.saved_tensors
+        return _InstanceNormActBackward.apply(dy.contiguous(), x, mean, rstd, ctx.act), None, None
+
+
+class _InstanceNormActBackward(Function):
+    """dx = d act(IN(x)) / dx applied to dy; differentiable once more (w.r.t. dy and x; mean
+    and rstd are functions of x already accounted for by the double-backward kernel)."""
+
+    @staticmethod
+    def forward(ctx, dy, x, mean, rstd, act):
+        P, M = _planes(x)
+        dx = torch.empty_like(x)
+        check(_in_fns(x.dtype)[1](dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                  dx.data_ptr(), P, M, act, stream_ptr(x.device)),
+              "instance_norm_act_bwd")
+        ctx.save_for_backward(dy, x, mean, rstd)
+        ctx.act = act
+        return dx
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, v):
+        dy, x, mean, rstd = ctx.saved_tensors
+        need_dy, need_x = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        P, M = _planes(x)
+        v = v.contiguous()
+        gdy = torch.empty_like(x) if need_dy else None
+        gx = torch.empty_like(x) if need_x else None
+        check(_in_fns(x.dtype)[2](v.data_ptr(), dy.data_ptr(), x.data_ptr(), mean.data_ptr(),
+                                  rstd.data_ptr(), gdy.data_ptr() if gdy is not None else None,
+                                  gx.data_ptr() if gx is not None else None, P, M, ctx.act,
+                                  stream_ptr(x.device)), "instance_norm_act_bwd2")
+        return gdy, gx, None, None, None
+
+
+def instance_norm_act(x, eps=1e-5, act=ACT_ELU):
+    """act(F.instance_norm(x, eps=eps)) for x [N, C, H, W] on HIP (act: ACT_ELU or 0).
+    The input is made dense as a recorded op, outside the Function (a copy made inside
+    and saved would cut the double backward from the graph)."""
+    require_hip(x, what="instance_norm_act")
+    return _InstanceNormAct.apply(x.contiguous(), float(eps), int(act))

@@ -462,6 +462,33 @@ int bpk_conv2d_igemm_wgrad_f32(const float* x, const float* gy, float* dw, float
                                int KW, int sh, int sw, int ph, int pw, int Ho, int Wo,
                                void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * InstanceNorm2d (affine=False) + activation, forward / backward / double backward:
+ * replaces aten's batch_norm statistics + transform, ELU, native_batch_norm_backward,
+ * elu_backward and the composite batchnorm double backward behind PressureNet's
+ * ResidualBlock `conv(act(normalize(x)))` (reference models/layers.py:438-491, used by
+ * models/flownet.py:219-224 get_double_res), differentiated twice by the PINN residual
+ * (pinn_kalman/pinn.py:72-111).  x [planes = N*C, M = H*W] contiguous; act 0 = identity,
+ * 1 = ELU(alpha=1).  fwd writes y and per-plane mean / rstd (1/sqrt(biased var + eps));
+ * bwd: dx for upstream dy; bwd2: for v = dL/d(dx), gdy = dL/d(dy) and gx = dL/dx (either
+ * may be NULL).  Deterministic (fixed-order per-plane reductions). */
+int bpk_instance_norm_act_fwd_f32(const float* x, float* y, float* mean, float* rstd,
+                                  int64_t planes, int64_t M, double eps, int act, void* stream);
+int bpk_instance_norm_act_fwd_f64(const double* x, double* y, double* mean, double* rstd,
+                                  int64_t planes, int64_t M, double eps, int act, void* stream);
+int bpk_instance_norm_act_bwd_f32(const float* dy, const float* x, const float* mean,
+                                  const float* rstd, float* dx, int64_t planes, int64_t M, int act,
+                                  void* stream);
+int bpk_instance_norm_act_bwd_f64(const double* dy, const double* x, const double* mean,
+                                  const double* rstd, double* dx, int64_t planes, int64_t M,
+                                  int act, void* stream);
+int bpk_instance_norm_act_bwd2_f32(const float* v, const float* dy, const float* x,
+                                   const float* mean, const float* rstd, float* gdy, float* gx,
+                                   int64_t planes, int64_t M, int act, void* stream);
+int bpk_instance_norm_act_bwd2_f64(const double* v, const double* dy, const double* x,
+                                   const double* mean, const double* rstd, double* gdy, double* gx,
+                                   int64_t planes, int64_t M, int act, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

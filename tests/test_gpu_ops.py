@@ -1024,3 +1024,76 @@ def test_conv_transpose2d_general_vs_torch(hip, cin, cout, k, s, p, op, groups):
     for a, r in zip(*outs):
         assert a.shape == r.shape
         assert float((a - r).abs().max()) <= 1e-4 * max(1.0, float(r.abs().max()))
+
+
+# ------------------------------------------------------------------ InstanceNorm + ELU
+
+@pytest.mark.parametrize("shape", [(4, 16, 64, 64), (4, 128, 4, 4), (3, 5, 2, 2), (2, 3, 7, 5),
+                                   (1, 1, 1, 1)])
+def test_instance_norm_elu_matches_oracle(hip, shape):
+    """csrc/instance_norm.hip forward / backward / double backward vs the float64 numpy
+    restatement (pinned against torch's CPU composite in tests/test_oracle.py).  fp32:
+    1e-5 relative to max|ref| (per-plane reductions in a different order)."""
+    from oracle import instance_norm_ref as inr
+    from op.norm_act import instance_norm_act
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(*shape, generator=g) * 2 + 0.3
+    dy = torch.randn(*shape, generator=g)
+    v = torch.randn(*shape, generator=g)
+    xd = x.to(hip).requires_grad_()
+    dyd = dy.to(hip).requires_grad_()
+    y = instance_norm_act(xd)
+    (dx,) = torch.autograd.grad(y, xd, dyd, create_graph=True)
+    gdy, gx = torch.autograd.grad(dx, (dyd, xd), v.to(hip))
+
+    def close(a, ref, tol=1e-5):
+        ref = np.asarray(ref)
+        err = np.abs(a.detach().cpu().double().numpy() - ref).max() / max(np.abs(ref).max(), 1e-6)
+        assert err <= tol, err
+
+    xn, dyn, vn = x.double().numpy(), dy.double().numpy(), v.double().numpy()
+    close(y, inr.forward(xn))
+    close(dx, inr.backward(dyn, xn))
+    o_gdy, o_gx = inr.double_backward(vn, dyn, xn)
+    close(gdy, o_gdy)
+    close(gx, o_gx, 5e-5 if shape[-1] * shape[-2] > 1 else 1e-5)
+
+
+def test_instance_norm_elu_gradgradcheck_and_third_order_refused(hip):
+    from op.norm_act import instance_norm_act
+    torch.manual_seed(5)
+    x = torch.randn(2, 3, 4, 5, dtype=torch.float64, device=hip, requires_grad=True)
+    f = lambda a: instance_norm_act(a[:, :, 1:])  # non-contiguous input, as a slice
+    assert torch.autograd.gradcheck(f, (x,))
+    assert torch.autograd.gradgradcheck(f, (x,))
+    y = f(x)
+    (dx,) = torch.autograd.grad(y.sum(), x, create_graph=True)
+    (ddx,) = torch.autograd.grad((dx ** 2).sum(), x, create_graph=True)
+    with pytest.raises(RuntimeError):
+        ddx.sum().backward()
+
+
+def test_instance_norm_elu_residual_block_matches_aten(hip, monkeypatch):
+    """PressureNet's ResidualBlock with the fused kernels vs the same block on aten
+    (BPK_IN_FUSED off): output, input derivative with create_graph, and the parameter
+    gradients of a loss on that derivative (the PINN residual's pattern)."""
+    from models import layers
+    torch.manual_seed(2)
+    blk = layers.ResidualBlock(16, 32).to(hip)
+    x0 = torch.randn(4, 16, 16, 16, device=hip)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(layers, "_IN_FUSED", fused)
+        blk.zero_grad()
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        (gx,) = torch.autograd.grad((y ** 2).sum(), x, create_graph=True)
+        (gx.square().sum() + y.sum()).backward()
+        outs.append([y.detach(), gx.detach()] + [p.grad.detach().clone() for p in blk.parameters()])
+    # outputs 1e-4; parameter gradients 1e-3 of max(|ref|, 1e-3 x the largest gradient):
+    # conv1.bias feeds normalize2, so its exact gradient is zero and both sides hold rounding
+    gmax = max(b.abs().max().item() for b in outs[1][2:])
+    for i, (a, b) in enumerate(zip(*outs)):
+        floor, tol = (1e-3 * gmax, 1e-3) if i >= 2 else (1e-6, 1e-4)
+        err = (a - b).abs().max().item() / max(b.abs().max().item(), floor)
+        assert err < tol, (i, err)
