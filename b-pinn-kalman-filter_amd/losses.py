@@ -344,7 +344,11 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                      * config.training.pinn_loss_weight)
         return pinn_loss + data_loss, pinn_loss, data_loss
 
-    # graph=True (training): after two eager steps, the forward, the residual's first and
+    # graph=True (training, EXPERIMENTAL -- not used by bench.py by default): in the full
+    # configs[3] setup (B = 64, 64x64) the replayed step turns to garbage / NaN after ~4
+    # replays, while a capture of the model alone replays correctly (tools/diag_pinn_graph*.py,
+    # DESIGN.md section 8); tests/test_gpu_pinn.py covers two replays of the small config.
+    # After two eager steps, the forward, the residual's first and
     # second derivatives and the backward are captured once in a hipGraph and replayed with
     # the step's batch / mask copied into static buffers -- the ~17k small kernel launches
     # of a step are issued by the device instead of the host.  Gradient all-reduce, the NaN

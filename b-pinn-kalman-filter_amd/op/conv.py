@@ -52,7 +52,11 @@ def filter_transform(weight, ft=False):
     version counter is unchanged.  ft=True: the transform of _flip_t(weight) (the filter of
     the backward-data conv, Cin = weight.shape[0]), read from `weight` in place."""
     attr = "_bpk_wino_u_ft" if ft else "_bpk_wino_u"
-    cached = getattr(weight, attr, None)
+    # under hipGraph capture the transform is always recorded (and the cache left alone):
+    # replays run after optimizer steps have rewritten the weight in place, so a cached U
+    # baked into the graph would be stale from the second replay on
+    capturing = torch.cuda.is_current_stream_capturing()
+    cached = None if capturing else getattr(weight, attr, None)
     if cached is not None and cached[0] == weight._version:
         return cached[1]
     w = weight.detach().contiguous()
@@ -62,7 +66,8 @@ def filter_transform(weight, ft=False):
     U = torch.empty((Cin, CoutP, 16), dtype=torch.float32, device=w.device)
     fn = lib.bpk_conv3x3_wino_filter_ft_f32 if ft else lib.bpk_conv3x3_wino_filter_f32
     check(fn(w.data_ptr(), U.data_ptr(), Cin, Cout, stream_ptr(w.device)), "conv3x3 filter")
-    setattr(weight, attr, (weight._version, U))
+    if not capturing:
+        setattr(weight, attr, (weight._version, U))
     return U
 
 

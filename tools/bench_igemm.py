@@ -91,7 +91,7 @@ def measure(tag):
 
 
 a = A()
-a.batch, a.pinn_warmup, a.pinn_steps, a.pinn_graph, a.pinn_eager_only = 64, 0, 1, False, True
+a.batch, a.pinn_warmup, a.pinn_steps, a.pinn_graph = 64, 0, 1, False
 bench.bench_pinn(a, DistContext(), dev)
 measure("pinn (configs[3], B=64, 64x64), one train step")
 rec.clear()

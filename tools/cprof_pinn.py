@@ -8,7 +8,7 @@ import bench
 from dist import DistContext
 
 class A: pass
-args = A(); args.batch = 64; args.pinn_warmup = 2; args.pinn_steps = 2; args.pinn_graph = False; args.pinn_eager_only = True
+args = A(); args.batch = 64; args.pinn_warmup = 2; args.pinn_steps = 2; args.pinn_graph = False
 dev = torch.device("cuda:0")
 bench.bench_pinn(args, DistContext(), dev)  # warm-up incl. MIOpen finds
 pr = cProfile.Profile()

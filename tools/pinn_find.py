@@ -7,7 +7,7 @@ import bench
 from dist import DistContext
 torch.backends.cudnn.benchmark = bool(int(sys.argv[1]))
 class A: pass
-args = A(); args.batch = 64; args.pinn_warmup = 2; args.pinn_steps = 5; args.pinn_graph = False; args.pinn_eager_only = True
+args = A(); args.batch = 64; args.pinn_warmup = 2; args.pinn_steps = 5; args.pinn_graph = False
 t0 = time.time()
 r = bench.bench_pinn(args, DistContext(), torch.device("cuda:0"))
 print(sys.argv[1], round(time.time() - t0, 1), "s total", r["pinn_ms_per_step"], "ms/step", flush=True)

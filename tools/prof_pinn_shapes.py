@@ -6,7 +6,7 @@ import torch
 import bench
 from dist import DistContext
 class A: pass
-args = A(); args.batch = 64; args.pinn_warmup = 3; args.pinn_steps = 1; args.pinn_graph = False; args.pinn_eager_only = True
+args = A(); args.batch = 64; args.pinn_warmup = 3; args.pinn_steps = 1; args.pinn_graph = False
 dev = torch.device("cuda:0")
 bench.bench_pinn(args, DistContext(), dev)
 from torch.profiler import profile, ProfilerActivity
