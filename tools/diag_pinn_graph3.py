@@ -46,14 +46,17 @@ side.wait_stream(torch.cuda.current_stream(dev))
 with torch.cuda.stream(side):
     model.zero_grad(set_to_none=True)
     w = loss_fn()
-    w[0].backward(inputs=params)
+    w[0].backward()
     del w
 torch.cuda.current_stream(dev).wait_stream(side)
 model.zero_grad(set_to_none=True)
 g = torch.cuda.CUDAGraph()
 with torch.cuda.graph(g):
     out = loss_fn()
-    out[0].backward(inputs=params)
+    for p in params:
+        if p.grad is not None:
+            p.grad.zero_()
+    out[0].backward()
 out = [o.detach() for o in out]
 for i in range(10):
     if "copy" in T:
