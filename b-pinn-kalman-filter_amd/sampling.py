@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import abc
 import functools
+import os
 
 import numpy as np
 import torch
@@ -401,6 +402,17 @@ def pc_timesteps(sde, eps):
     return torch.linspace(sde.T, eps, sde.N)
 
 
+def _graph_collective(ctx) -> bool:
+    """Capture the sharded PC step's RCCL all-reduce inside the step graph (opt-in,
+    BPK_PC_GRAPH_ALLREDUCE=1): one graph replay per step instead of segments with a
+    host-issued all-reduce between them.  Off by default: the split form is what the 8-GPU
+    runs have exercised; tests/test_gpu_dist.py checks RCCL capture on one device."""
+    import torch.distributed as tdist
+    if os.environ.get("BPK_PC_GRAPH_ALLREDUCE", "0") != "1" or ctx is None:
+        return False
+    return tdist.is_initialized() and tdist.get_backend(ctx.group) == "nccl"
+
+
 class PCEngine:
     """Fused, graph-captured PC sampler for the built-in predictor/corrector pairs.
 
@@ -577,6 +589,16 @@ class PCEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.step.zero_()
         try:
+            if self.world > 1 and _graph_collective(self.dist):
+                # the whole PC step as ONE graph, the Langevin norm all-reduce (RCCL) captured
+                # inside it (BPK_PC_GRAPH_ALLREDUCE=1; needs the nccl backend, whose
+                # communicator the warm-up above has initialised)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in self._segments(model, self._gx, self._gxm):
+                        self.dist.all_reduce_sum_(self.red)
+                self.graph = [g]
+                return
             # one graph per segment between exchange points (a single graph when unsharded);
             # the segments share one memory pool and the generator keeps the tensors that
             # cross a segment boundary (the model output) alive

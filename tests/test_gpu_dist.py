@@ -251,3 +251,43 @@ def test_nan_on_one_rank_makes_every_rank_skip():
     for _, (step, g, p1, p0, _), _ in two:
         assert step == 50
         np.testing.assert_array_equal(p1, p0)
+
+
+def _rccl_capture_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                          WORLD_SIZE="1", LOCAL_RANK="0")
+        import torch.distributed as tdist
+        torch.cuda.set_device(0)
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        t = torch.zeros(2, device="cuda:0")
+        tdist.all_reduce(t)  # communicator up before the capture (as the PC warm-up does)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            t.add_(1.0)
+            tdist.all_reduce(t)
+        torch.cuda.current_stream().wait_stream(s)
+        t.zero_()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            t.add_(1.0)
+            tdist.all_reduce(t)
+        t.zero_()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        q.put((0, t.cpu().numpy(), None))
+        tdist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((0, None, traceback.format_exc()))
+
+
+def test_rccl_all_reduce_captures_in_a_hip_graph():
+    """The mechanics behind BPK_PC_GRAPH_ALLREDUCE=1 (sampling._graph_collective: the sharded
+    PC step as one graph with the Langevin all-reduce inside): an RCCL all-reduce captured in
+    a hipGraph replays (one rank: two ranks cannot share a device under RCCL)."""
+    (r,) = _run(_rccl_capture_worker, 1)
+    np.testing.assert_array_equal(r[1], np.full(2, 3.0, np.float32))
