@@ -306,6 +306,32 @@ def _time_us(fn, reps=3):
     return s.elapsed_time(e) * 1e3 / reps
 
 
+# Small images (H * W <= 32 x 32, the PINN pyramids' lower levels, CIFAR's 8^2 / 4^2): the
+# Winograd kernels' per-workgroup set-up is a large share of a short launch, so 3x3 convs
+# there are timed against the implicit-GEMM kernel once per distinct call and the faster
+# kept (BPK_CONV3_SELECT=0: Winograd whenever it fits).
+_SEL3 = os.environ.get("BPK_CONV3_SELECT", "1") != "0"
+_SEL3_MAX_HW = 32 * 32
+
+
+def _small_img(x):
+    return _SEL3 and _IG_MODE != "0" and x.shape[2] * x.shape[3] <= _SEL3_MAX_HW
+
+
+def _pick_any(key, cands):
+    """cands[i]() for the candidate the cached per-key timing says is fastest (the first
+    one under graph capture for a key never timed eagerly)."""
+    c = _CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return cands[0]()
+        with torch.no_grad():
+            ts = [_time_us(f) for f in cands]
+        c = min(range(len(cands)), key=ts.__getitem__)
+        _CHOICE[key] = c
+    return cands[c]()
+
+
 def _pick(key, run_ig, run_mi):
     """run_ig() or run_mi(), whichever the cached per-key timing says is faster."""
     if _IG_MODE == "2":
@@ -359,6 +385,15 @@ def _fwd_impl(x, w, bias=None, skip=None, div=1.0):
     small-channel kernel, or MIOpen for the other shapes."""
     w = w.detach().contiguous()
     if wino_supported(x, w):
+        if _small_img(x) and igemm_supported(x, w, 1, 1):
+            def ig():
+                y = conv2d_igemm_raw(x, w, None if bias is None else bias.detach(), 1, 1)
+                if skip is not None:
+                    from .norm_act import residual_rescale
+                    y = residual_rescale(skip.detach(), y, None, div)
+                return y
+            key = ("f3", tuple(x.shape), tuple(w.shape), bias is not None, skip is not None)
+            return _pick_any(key, [lambda: conv3x3_fwd_raw(x.detach(), w, bias, skip, div), ig])
         return conv3x3_fwd_raw(x.detach(), w, bias, skip, div)
     with torch.no_grad():
         if small_supported(x, w):
@@ -377,6 +412,13 @@ def _wgrad_impl(x, gy, wshape, want_b):
     """(dw, db or None) without autograd: the Winograd weight gradient (+ bias) when the
     shape qualifies, MIOpen backward-weights otherwise."""
     if wgrad_supported(x, tuple(wshape)):
+        if (_small_img(x) and _WGRAD_PIPE and x.is_cuda and x.dtype == torch.float32
+                and igemm_supported(x, tuple(wshape), 1, 1)):
+            key = ("w3", tuple(x.shape), tuple(wshape))
+            dw, db = _pick_any(key, [
+                lambda: conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True),
+                lambda: conv2d_weight_igemm_raw(x, tuple(wshape), gy, 1, 1, True)])
+            return dw, (db if want_b else None)
         if _WGRAD_PIPE:
             dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
             return dw, (db if want_b else None)
@@ -396,6 +438,10 @@ def _fwd_ft_impl(x, w):
     N, C, H, W = x.shape
     if (C == w.shape[0] and x.is_cuda and x.dtype == torch.float32
             and bool(lib.bpk_conv3x3_wino_supported(N, C, w.shape[1], H, W))):
+        if _small_img(x) and _IGEMM and w.dtype == torch.float32:  # (igemm: any 3x3 / pad 1)
+            key = ("d3", tuple(x.shape), tuple(w.shape))
+            return _pick_any(key, [lambda: conv3x3_fwd_raw(x.detach(), w, ft=True),
+                                   lambda: conv2d_input_igemm_raw((N, w.shape[1], H, W), w, x, 1, 1)])
         return conv3x3_fwd_raw(x.detach(), w, ft=True)
     if _IGEMM and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32:
         # conv3x3(x, flip_t(w)) is the adjoint of conv3x3(., w): the dgrad kernel, no flip
