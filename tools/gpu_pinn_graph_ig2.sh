@@ -1,0 +1,14 @@
+#!/bin/bash
+# PINN hipGraph replay with / without MIOpen convs inside the capture (BPK_IGEMM=2: every
+# non-Winograd conv on the implicit-GEMM kernels), plus the eager PINN / CIFAR steps with
+# BPK_IGEMM=1 (timed selection, MIOpen allowed) vs 2 (native only).
+mkdir -p gpurun_out; export TMPDIR=/tmp
+B="--no-cpu-baseline --no-train --no-dps --ns-steps 0 --ncddpmpp-steps 0 --steps 1 --warmup 1"
+for ig in 1 2; do
+  BPK_IGEMM=$ig timeout -k 10 400 python bench.py $B --no-cifar --pinn-graph --pinn-steps 30 > gpurun_out/pg_$ig.log 2> gpurun_out/pg_$ig.err || { tail -5 gpurun_out/pg_$ig.err; exit 1; }
+  echo "graph ig=$ig $(grep -o '"pinn_train_steps_per_s": [0-9.]*' gpurun_out/pg_$ig.log) $(grep -o '"pinn_losses": [^]]*' gpurun_out/pg_$ig.log)"
+done
+for ig in 1 2; do
+  BPK_IGEMM=$ig timeout -k 10 400 python bench.py $B --pinn-steps 20 --cifar-steps 6 > gpurun_out/pe_$ig.log 2> gpurun_out/pe_$ig.err || { tail -5 gpurun_out/pe_$ig.err; exit 1; }
+  echo "eager ig=$ig $(grep -o '"pinn_train_steps_per_s": [0-9.]*' gpurun_out/pe_$ig.log) $(grep -o '"cifar_train_steps_per_s": [0-9.]*' gpurun_out/pe_$ig.log) $(grep -o '"pinn_losses": [^]]*' gpurun_out/pe_$ig.log)"
+done
