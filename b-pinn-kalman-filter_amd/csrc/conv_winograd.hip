@@ -122,6 +122,20 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 #ifndef WINO_VPM
 #define WINO_VPM 4
 #endif
+// 8-wave form: waves 4-7 run their side work two MFMA groups after waves 0-3 (A/B)
+#ifndef WINO_W8ROT
+#define WINO_W8ROT 0
+#endif
+// prologue load order (A/B): 0 = patches 0-2, U(0), GroupNorm table; 1 = in consumption order
+#ifndef WINO_PRO
+#define WINO_PRO 0
+#endif
+// wave priority (A/B): 1 = s_setprio 2 through the prologue and the epilogue, 0 in the chunk
+// loop, so a starting / finishing workgroup's VALU is not starved by its co-resident
+// partner's loop (MI355X_MICROARCH.md: VALU issue is arbitrated by priority, then age)
+#ifndef WINO_PRIO
+#define WINO_PRIO 0
+#endif
 
 __device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 
@@ -439,6 +453,29 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
   store_tile<kWN>(&s_out[wave * kWN * kOS], skip, y, stats, g, n, cout_w, oy0, ox0, lane);
 }
 
+// Per-workgroup phase timestamps (diagnostic build only, -DWINO_TIMING; tools/wino_timing.py):
+// wall clock (100 MHz) at entry, once the prologue's loads have landed, after the first patch
+// stores, at the start of the chunk loop, after it and after the epilogue (wave 0's view), the
+// shader clock at entry and exit (s_memtime, for the clock rate), and the XCC / SE / CU.
+#ifdef WINO_TIMING
+constexpr unsigned kTsMax = 1u << 17;
+__device__ long long g_wino_ts[kTsMax][8];
+__device__ unsigned g_wino_cu[kTsMax];
+#define WINO_TS(slot)                                                              \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < kTsMax) {                                 \
+      g_wino_ts[blockIdx.x][slot] = wall_clock64();                                \
+      if (slot == 0) g_wino_cu[blockIdx.x] = __smid();                             \
+      if (slot == 0 || slot == 5)                                                  \
+        g_wino_ts[blockIdx.x][6 + slot / 5] = (long long)__builtin_amdgcn_s_memtime(); \
+    }                                                                              \
+  } while (0)
+#else
+#define WINO_TS(slot) \
+  do {                \
+  } while (0)
+#endif
+
 // Software-pipelined form (one workgroup per CU, 4 waves x 32 couts = 128 couts, 32 tiles).
 // The serial form above runs store-patch | barrier | transform | barrier | MFMAs per chunk,
 // so a wave's MFMA pipe idles through the transform phase unless a second workgroup
@@ -448,8 +485,12 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_kernel(const fl
 // into the free patch buffer and issues the global loads of patch(k+3) and of U(k+1) into
 // a second register set -- one barrier per chunk.  The VALU / LDS work (~70 instructions
 // per chunk) fills MFMA issue gaps (128 MFMAs of 32 cycles per chunk per wave).
-template <int NB, bool PRE>
-__global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
+// WG = waves per workgroup: 4 (64 couts, two workgroups per CU) or 8 (128 couts, one
+// workgroup per CU, NB = 1): the eight waves share one patch / V stream, so the GroupNorm+SiLU
+// patch stores (4 channels per thread instead of 8: half the SiLU work per SIMD per MFMA of the
+// two-workgroup form).
+template <int NB, bool PRE, int WG = 4>
+__global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino_f23_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
     float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2) {
@@ -460,6 +501,10 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];              // V double buffer
   __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];  // PRE: (s, t) of every input channel
 
+  WINO_TS(0);
+#if WINO_PRIO
+  __builtin_amdgcn_s_setprio(2);
+#endif
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   // grid < 2^31 blocks (host check): 32-bit block arithmetic
@@ -479,7 +524,15 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   r = udivmod(r, (unsigned)g.regions_x, rx);
   const int n = (int)udivmod(r, (unsigned)g.regions_y, ry);
   const int oy0 = (int)ry * kOutRows, ox0 = (int)rx * kOutCols;
-  const int cout_w = (int)cb * (4 * kWN) + wave * kWN;
+  const int cout_w = (int)cb * (WG * kWN) + wave * kWN;
+  static_assert(WG == 4 || (WG == 8 && NB == 1), "8-wave form: NB = 1");
+  // 8 waves: waves 0-3 stage channels 0-3 of a chunk and transform V, waves 4-7 stage
+  // channels 4-7 (wave-uniform, in SGPRs)
+  constexpr int kCT = kCK * 4 / WG;  // channels staged per thread
+  const int ph = WG == 8 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
+  // every wave transforms (waves w and w + 4 write the same V records, identical values): a
+  // wave-uniform branch around the transform made the compiler spill
+  constexpr bool xf = true;
 
   // accumulators: the first chunk's k-step 0 MFMAs take an inline-constant zero C operand
   // (no 128 register clears in the prologue)
@@ -513,28 +566,29 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   int poff, pdst;
   bool pin;
   {
-    const int t = tid < kPos ? tid : 0;
+    const int t8 = tid & 255;
+    const int t = t8 < kPos ? t8 : 0;
     const int py = t / kPC, px = t - py * kPC;
     const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
     pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
     const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
     poff = (cy * g.W + cx) * 4;
-    pdst = py * kPCp + px;
+    pdst = py * kPCp + px + ph * kCT * (kPR * kPCp);
   }
-  float pv[kCK];
+  float pv[kCT];
   auto load_patch = [&](int k) {
     const int cc = min(k, nch - 1) * kCK;
     const bool second = cc >= g.C1;
-    const int soff = (second ? cc - g.C1 : cc) * (int)plane * 4;
+    const int soff = ((second ? cc - g.C1 : cc) + ph * kCT) * (int)plane * 4;
 #pragma unroll
-    for (int c = 0; c < kCK; ++c)
+    for (int c = 0; c < kCT; ++c)
       pv[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
           second ? xrs2 : xrs, poff, soff + c * (int)plane * 4, 0));
   };
   auto store_patch_from = [&](const float* src, float* sp, int k) {
-    const int c0 = min(k, nch - 1) * kCK;
+    const int c0 = min(k, nch - 1) * kCK + ph * kCT;
 #pragma unroll
-    for (int c = 0; c < kCK; ++c) {
+    for (int c = 0; c < kCT; ++c) {
       float v = src[c];
       if (PRE) {
         const float2 st = s_ss[c0 + c];
@@ -559,7 +613,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       }
   };
   // V = B^T d B of one (cin, tile) per thread
-  const int tc = tid >> 5, tm = tid & 31;
+  const int tc = (tid & 255) >> 5, tm = tid & 31;
   const int tty = tm / kTC, ttx = tm - tty * kTC;
   float d[4][4];
   auto read_d = [&](const float* sp) {
@@ -591,25 +645,55 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight.  The
   // global loads of patches 0-2, U(0) and the GroupNorm table are all issued before the
   // first wait, so a workgroup pays one memory latency here, not four.
-  float pv0[kCK], pv1[kCK];
+  float pv0[kCT], pv1[kCT];
+#if WINO_PRO == 1
+  // loads in the order they are consumed (vmcnt is in order): GroupNorm table, patches 0 / 1,
+  // U(0), patch 2 -- the patch stores and the first transform wait only for what they read
+  float2 ssv[PRE ? kPreMaxCin / 256 : 1];
+  if (PRE) {
+#pragma unroll
+    for (int i = 0; i < kPreMaxCin / 256; ++i)
+      if (tid + 256 * i < g.Cin) ssv[i] = pre_n[tid + 256 * i];  // (WG = 4 only)
+  }
   load_patch(0);
 #pragma unroll
-  for (int c = 0; c < kCK; ++c) pv0[c] = pv[c];
+  for (int c = 0; c < kCT; ++c) pv0[c] = pv[c];
   load_patch(1);
 #pragma unroll
-  for (int c = 0; c < kCK; ++c) pv1[c] = pv[c];
+  for (int c = 0; c < kCT; ++c) pv1[c] = pv[c];
+  load_u(0, 0);
+  load_u(1, 0);
+  load_patch(2);
+  if (PRE) {
+#pragma unroll
+    for (int i = 0; i < kPreMaxCin / 256; ++i)
+      if (tid + 256 * i < g.Cin) s_ss[tid + 256 * i] = ssv[i];
+    __syncthreads();
+  }
+#else
+  load_patch(0);
+#pragma unroll
+  for (int c = 0; c < kCT; ++c) pv0[c] = pv[c];
+  load_patch(1);
+#pragma unroll
+  for (int c = 0; c < kCT; ++c) pv1[c] = pv[c];
   load_patch(2);
   load_u(0, 0);
   load_u(1, 0);
   if (PRE) {
-    for (int c = tid; c < g.Cin; c += 256) s_ss[c] = pre_n[c];
+    for (int c = tid; c < g.Cin; c += 64 * WG) s_ss[c] = pre_n[c];
     __syncthreads();
   }
+#endif
+  WINO_TS(1);
   store_patch_from(pv0, s_patch_raw[0], 0);
   store_patch_from(pv1, s_patch_raw[1], 1);
   __syncthreads();
-  read_d(s_patch_raw[0]);
-  write_v(s_v[0]);
+  WINO_TS(2);
+  if (xf) {
+    read_d(s_patch_raw[0]);
+    write_v(s_v[0]);
+  }
   __syncthreads();
 
   // A operands a[q] = V[pos 4q..4q+3] of (ks, mb) = this lane's tile row of one LDS record;
@@ -626,21 +710,27 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) a[q] = src[q];
   }
-  auto step = [&](int k, auto sb_c, auto first_c) {
+  // ROT: the side work of the 8-wave form's waves 4-7 runs two MFMA groups later than that of
+  // waves 0-3 (store + load of the patches first, then the V transform), so the two waves of a
+  // SIMD -- one from each half, in step through the same barriers -- never run their
+  // GroupNorm+SiLU patch stores at the same time
+  auto step = [&](int k, auto sb_c, auto first_c, auto rot_c) __attribute__((always_inline)) {
     constexpr int SB = decltype(sb_c)::value;
     constexpr bool FIRST = decltype(first_c)::value;
+    constexpr int ROT = decltype(rot_c)::value;
     const float* sv = s_v[SB];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
       const int ks = grp >> 1, mb = grp & 1;
+      const int sw = (grp + ROT) & 3;
       // side work of the next chunks, spread over the four MFMA groups
 #if WINO_SCHED == 0 || WINO_SCHED == 4
       __builtin_amdgcn_sched_barrier(0);
 #endif
-      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                // patch(k+1)
-      if (grp == 1) write_v(s_v[SB ^ 1]);                       // V(k+1)
-      if (grp == 2) store_patch(s_patch_raw[SB], k + 2);        // patch(k+2)
-      if (grp == 3) load_patch(k + 3);
+      if (sw == 0 && xf) read_d(s_patch_raw[SB ^ 1]);           // patch(k+1)
+      if (sw == 1 && xf) write_v(s_v[SB ^ 1]);                  // V(k+1)
+      if (sw == 2) store_patch(s_patch_raw[SB], k + 2);         // patch(k+2)
+      if (sw == 3) load_patch(k + 3);
 #if WINO_SCHED == 0
       __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -690,13 +780,33 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
   using F = std::false_type;
-  step(0, C0{}, std::true_type{});
-  int k = 1;
-  for (; k + 1 < nch; k += 2) {
-    step(k, C1{}, F{});
-    step(k + 1, C0{}, F{});
+  WINO_TS(3);
+#if WINO_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+  auto run = [&](auto rot_c) __attribute__((always_inline)) {
+    step(0, C0{}, std::true_type{}, rot_c);
+    int k = 1;
+    for (; k + 1 < nch; k += 2) {
+      step(k, C1{}, F{}, rot_c);
+      step(k + 1, C0{}, F{}, rot_c);
+    }
+    if (k < nch) step(k, C1{}, F{}, rot_c);
+  };
+  // (one call site per instantiation: a second, dead one stopped the inliner and put the
+  // accumulators in scratch)
+  if constexpr (WG == 8 && WINO_W8ROT) {
+    if (ph)
+      run(std::integral_constant<int, 2>{});
+    else
+      run(std::integral_constant<int, 0>{});
+  } else {
+    run(std::integral_constant<int, 0>{});
   }
-  if (k < nch) step(k, C1{}, F{});
+  WINO_TS(4);
+#if WINO_PRIO
+  __builtin_amdgcn_s_setprio(2);
+#endif
 
   // output transform straight from registers to global memory (no LDS staging, no
   // barrier).  Per M-block a lane holds tiles m = 16 mb + 4 kq + rg, rg = 0..3: tile row
@@ -763,6 +873,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_f23_pipe_kernel(
       }
     }
   }
+  WINO_TS(5);
 }
 
 // Persistent form of the pipelined kernel (NB = 1: 4 waves x 16 couts = 64 couts, 32
@@ -1191,8 +1302,18 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
   if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
     // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup
     const int pnb = (pipe_env == 2 && Cout % 128 == 0) ? 2 : 1;
-    WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * pnb), div, C1,
-              Cout};
+    // the 8-wave, 128-cout workgroup form (CoutP % 128 == 0) for the GroupNorm-prologue convs
+    // without a residual tail: +2-3 % on those NCSN++ shapes, while the residual-tail form
+    // loses 1-3 % (its epilogue reads skip with no co-resident workgroup to cover it;
+    // profiles/r02_wino_w8.txt).  BPK_WINO_W8=0: never, 2: every pipelined launch.
+    static const int w8_env = [] {
+      const char* e = getenv("BPK_WINO_W8");
+      return e ? atoi(e) : 1;
+    }();
+    const bool w8_case = w8_env == 2 || (w8_env == 1 && pre && !skip);
+    const int wg = (w8_case && pnb == 1 && CoutP % 128 == 0) ? 8 : 4;
+    WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * pnb * wg / 4), div,
+              C1, Cout};
     const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
     BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
     const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -1201,7 +1322,14 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
 #define WINO_PIPE(NB_, PRE_)                                                                  \
   hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, \
                      x, U, bias, skip, pre2, y, stats2, g, remap, x2)
-    if (pnb == 2) {
+    if (wg == 8) {
+      if (pre)
+        hipLaunchKernelGGL((wino_f23_pipe_kernel<1, true, 8>), dim3((unsigned)blocks), dim3(512),
+                           0, st, x, U, bias, skip, pre2, y, stats2, g, remap, x2);
+      else
+        hipLaunchKernelGGL((wino_f23_pipe_kernel<1, false, 8>), dim3((unsigned)blocks), dim3(512),
+                           0, st, x, U, bias, skip, pre2, y, stats2, g, remap, x2);
+    } else if (pnb == 2) {
       if (pre) WINO_PIPE(2, true); else WINO_PIPE(2, false);
     } else {
       if (pre) WINO_PIPE(1, true); else WINO_PIPE(1, false);
@@ -1248,3 +1376,12 @@ extern "C" int bpk_conv3x3_wino_f32(const float* x, const float* U, const float*
   return bpk_conv3x3_wino_pre_f32(x, nullptr, U, bias, nullptr, 1.0f, y, N, Cin, Cout, H, W,
                                   stream);
 }
+
+#ifdef WINO_TIMING
+extern "C" int bpk_wino_timing_read(long long* ts, unsigned* cu, int n) {
+  if (n > (int)kTsMax) n = (int)kTsMax;
+  if (hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_wino_ts), sizeof(long long) * 8 * n) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(cu, HIP_SYMBOL(g_wino_cu), sizeof(unsigned) * n) != hipSuccess) return -1;
+  return n;
+}
+#endif

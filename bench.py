@@ -101,7 +101,7 @@ def time_kernel(fn, stream, reps=10):
 
 
 # The sampler's dominant kernel: the Winograd conv with the GroupNorm+SiLU prologue
-# (csrc/conv_winograd.hip wino_f23_pipe_kernel<1, true>), ~75 % of a PC step.  Its roofline
+# (csrc/conv_winograd.hip wino_f23_pipe_kernel<1, true, 8 | 4>), ~75 % of a PC step.  Its roofline
 # is taken over the NCSN++ 128x128 shape mix it runs in the sampler: per (cin, cout, hw) the
 # PRE form with bias + GroupNorm partial statistics (Conv_0 of a BigGAN block) and with the
 # residual tail (Conv_1), weighted by their counts per forward.
@@ -161,9 +161,10 @@ def conv_roofline(dev, batch):
             "traffic_unit": "HBM bytes per forward mix (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
             "algorithmic_bytes": sum((r["n_pre"] + r["n_res"]) * 4.0 * batch * (r["cin"] + r["cout"]) * r["hw"] ** 2
                                      + r["n_res"] * 4.0 * batch * r["cout"] * r["hw"] ** 2 for r in rows),
-            "kernel": "wino_f23_pipe_kernel<1,true> (GroupNorm+SiLU prologue; bias + GN partial "
-                      "statistics or residual tail): the NCSN++ 128x128 forward's PRE-conv mix, "
-                      f"{n_launch} launches, B={batch}",
+            "kernel": "wino_f23_pipe_kernel<1,true,WG> (GroupNorm+SiLU prologue): the NCSN++ "
+                      "128x128 forward's PRE-conv mix -- bias + GN partial statistics on the 8-wave "
+                      "128-cout workgroup form (WG=8), residual tail on the 4-wave 64-cout form "
+                      f"(WG=4); {n_launch} launches, B={batch}",
             "flop_basis": "executed (Winograd, 4/9 of direct)",
             "ms_per_mix": round(t * 1e3, 3), "flop_per_mix": fl,
             "direct_equivalent_tflops": round(fl * 9 / 4 / t / 1e12, 2),
