@@ -122,6 +122,9 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 #ifndef WINO_VPM
 #define WINO_VPM 4
 #endif
+#ifndef WINO_W8SPLIT
+#define WINO_W8SPLIT 0
+#endif
 // 8-wave form: waves 4-7 run their side work two MFMA groups after waves 0-3 (A/B)
 #ifndef WINO_W8ROT
 #define WINO_W8ROT 0
@@ -528,11 +531,17 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
   static_assert(WG == 4 || (WG == 8 && NB == 1), "8-wave form: NB = 1");
   // 8 waves: waves 0-3 stage channels 0-3 of a chunk and transform V, waves 4-7 stage
   // channels 4-7 (wave-uniform, in SGPRs)
-  constexpr int kCT = kCK * 4 / WG;  // channels staged per thread
+  // WINO_W8SPLIT (A/B): waves 0-3 only transform V and waves 4-7 only stage the patches (all 8
+  // channels per thread) inside the chunk loop, so the two waves of a SIMD do different side
+  // work -- as written the role branches make the compiler spill (118 VGPRs), so it is off
+  constexpr bool kSplit = WG == 8 && WINO_W8SPLIT;
+  constexpr int kCT = kSplit ? kCK : kCK * 4 / WG;  // channels staged per thread
   const int ph = WG == 8 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
+  const int phc = kSplit ? 0 : ph;  // channel half staged by this thread
   // every wave transforms (waves w and w + 4 write the same V records, identical values): a
   // wave-uniform branch around the transform made the compiler spill
-  constexpr bool xf = true;
+  const bool xf = !kSplit || ph == 0;
+  const bool pw = !kSplit || ph != 0;
 
   // accumulators: the first chunk's k-step 0 MFMAs take an inline-constant zero C operand
   // (no 128 register clears in the prologue)
@@ -573,20 +582,20 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
     pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
     const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
     poff = (cy * g.W + cx) * 4;
-    pdst = py * kPCp + px + ph * kCT * (kPR * kPCp);
+    pdst = py * kPCp + px + phc * kCT * (kPR * kPCp);
   }
   float pv[kCT];
   auto load_patch = [&](int k) {
     const int cc = min(k, nch - 1) * kCK;
     const bool second = cc >= g.C1;
-    const int soff = ((second ? cc - g.C1 : cc) + ph * kCT) * (int)plane * 4;
+    const int soff = ((second ? cc - g.C1 : cc) + phc * kCT) * (int)plane * 4;
 #pragma unroll
     for (int c = 0; c < kCT; ++c)
       pv[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
           second ? xrs2 : xrs, poff, soff + c * (int)plane * 4, 0));
   };
   auto store_patch_from = [&](const float* src, float* sp, int k) {
-    const int c0 = min(k, nch - 1) * kCK + ph * kCT;
+    const int c0 = min(k, nch - 1) * kCK + phc * kCT;
 #pragma unroll
     for (int c = 0; c < kCT; ++c) {
       float v = src[c];
@@ -729,8 +738,8 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
 #endif
       if (sw == 0 && xf) read_d(s_patch_raw[SB ^ 1]);           // patch(k+1)
       if (sw == 1 && xf) write_v(s_v[SB ^ 1]);                  // V(k+1)
-      if (sw == 2) store_patch(s_patch_raw[SB], k + 2);         // patch(k+2)
-      if (sw == 3) load_patch(k + 3);
+      if (sw == 2 && pw) store_patch(s_patch_raw[SB], k + 2);   // patch(k+2)
+      if (sw == 3 && pw) load_patch(k + 3);
 #if WINO_SCHED == 0
       __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1305,12 +1314,13 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     // the 8-wave, 128-cout workgroup form (CoutP % 128 == 0) for the GroupNorm-prologue convs
     // without a residual tail: +2-3 % on those NCSN++ shapes, while the residual-tail form
     // loses 1-3 % (its epilogue reads skip with no co-resident workgroup to cover it;
-    // profiles/r02_wino_w8.txt).  BPK_WINO_W8=0: never, 2: every pipelined launch.
+    // profiles/r02_wino_w8.txt).  BPK_WINO_W8=0: never, 2: every pipelined launch, 3: every
+    // launch without a residual tail.
     static const int w8_env = [] {
       const char* e = getenv("BPK_WINO_W8");
       return e ? atoi(e) : 1;
     }();
-    const bool w8_case = w8_env == 2 || (w8_env == 1 && pre && !skip);
+    const bool w8_case = w8_env == 2 || (w8_env == 1 && pre && !skip) || (w8_env == 3 && !skip);
     const int wg = (w8_case && pnb == 1 && CoutP % 128 == 0) ? 8 : 4;
     WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * pnb * wg / 4), div,
               C1, Cout};
