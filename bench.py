@@ -104,11 +104,15 @@ def time_kernel(fn, stream, reps=10):
 # (csrc/conv_winograd.hip wino_f23_pipe_kernel<1, true, 8 | 4>), ~75 % of a PC step.  Its roofline
 # is taken over the NCSN++ 128x128 shape mix it runs in the sampler: per (cin, cout, hw) the
 # PRE form with bias + GroupNorm partial statistics (Conv_0 of a BigGAN block) and with the
-# residual tail (Conv_1), weighted by their counts per forward.
-WINO_MIX = [  # (cin, cout, hw, PRE+stats convs per forward, PRE+residual convs per forward)
-    (128, 128, 128, 7, 6), (256, 128, 128, 4, 0), (256, 256, 128, 1, 1),
-    (256, 256, 64, 7, 7), (512, 256, 64, 4, 0), (128, 256, 64, 1, 0),
-    (256, 256, 32, 9, 8)]
+# residual tail (Conv_1), weighted by their counts per forward: the
+# census of one forward of the bench model (tools/conv_census.py, profiles/r02_conv_census.txt;
+# the up path's two-source convs are timed as one source of Cin = C1 + C2, same kernel and
+# FLOPs).
+WINO_MIX = [  # (cin, cout, hw, PRE+stats convs per forward, PRE+residual+stats convs per forward)
+    (128, 128, 128, 4, 9), (256, 128, 128, 4, 0), (384, 128, 128, 1, 0), (256, 256, 128, 0, 1),
+    (128, 128, 64, 0, 1), (128, 256, 64, 1, 0), (256, 256, 64, 3, 10), (384, 256, 64, 1, 0),
+    (512, 256, 64, 4, 0), (256, 256, 32, 4, 11), (512, 256, 32, 5, 0), (256, 256, 16, 6, 12),
+    (512, 256, 16, 5, 0)]
 
 
 def _pmc(key):
@@ -137,7 +141,8 @@ def wino_mix_times(dev, batch, reps=10):
         with torch.cuda.stream(st):
             filter_transform(w)
             t_pre = time_kernel(lambda: conv3x3(x, w, b, pre=pre, stats=True), st, reps)
-            t_res = time_kernel(lambda: conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre), st, reps)
+            t_res = time_kernel(lambda: conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre, stats=True),
+                                st, reps)
         fl = 2.0 * batch * cin * cout * 16 * (hw // 2) ** 2  # executed MFMA FLOPs (Winograd)
         out.append(dict(cin=cin, cout=cout, hw=hw, n_pre=n_pre, n_res=n_res, t_pre=t_pre,
                         t_res=t_res, flop=fl))

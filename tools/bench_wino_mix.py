@@ -14,9 +14,7 @@ import torch  # noqa: E402
 from op.conv import conv3x3, filter_transform  # noqa: E402
 
 # (cin, cout, hw, PRE+stats convs per forward, PRE+residual convs per forward)
-MIX = [(128, 128, 128, 7, 6), (256, 128, 128, 4, 0), (256, 256, 128, 1, 1),
-       (256, 256, 64, 7, 7), (512, 256, 64, 4, 0), (128, 256, 64, 1, 0),
-       (256, 256, 32, 9, 8)]
+from bench import WINO_MIX as MIX  # noqa: E402  (the census of one forward)
 B = int(os.environ.get("B", 64))
 REPS = int(os.environ.get("REPS", 10))
 
@@ -48,7 +46,7 @@ def main():
         skip = torch.randn(B, cout, hw, hw, device=dev, generator=g)
         filter_transform(w)
         t_pre = t_of(lambda: conv3x3(x, w, b, pre=pre, stats=True), st)
-        t_res = t_of(lambda: conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre), st)
+        t_res = t_of(lambda: conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre, stats=True), st)
         fl = 2.0 * B * cin * cout * 16 * (hw // 2) ** 2  # executed (Winograd) MFMA FLOPs
         tot_t += n_pre * t_pre + n_res * t_res
         tot_f += (n_pre + n_res) * fl

@@ -37,7 +37,7 @@ if mode in ("wino_one", "mix"):
             for _ in range(n_pre):
                 conv3x3(x, w, b, pre=pre, stats=True)
             for _ in range(n_res):
-                conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre)
+                conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre, stats=True)
         torch.cuda.synchronize()
         del x, skip
 elif mode == "ns":

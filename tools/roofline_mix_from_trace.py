@@ -1,5 +1,5 @@
 """Weighted PRE-conv mix time from a rocprofv3 kernel trace of tools/bench_wino_mix.py:
-per shape, the mean duration of the wino_f23_pipe_kernel<1, true> launches of its PRE+stats
+per shape, the mean duration of the wino_f23_pipe_kernel<1, true, 8 | 4> launches of its PRE+stats
 and PRE+residual runs (3 warm-up + REPS each, in launch order), weighted by the per-forward
 counts of bench_wino_mix.MIX -- to compare with the HIP-event figure the bench prints.
 usage: roofline_mix_from_trace.py kernel_trace.csv [REPS]"""
@@ -13,7 +13,7 @@ from bench_wino_mix import MIX  # noqa: E402
 
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 rows = sorted((r for r in csv.DictReader(open(sys.argv[1]))
-               if "wino_f23_pipe_kernel<1, true>" in r["Kernel_Name"]),
+               if "wino_f23_pipe_kernel<1, true," in r["Kernel_Name"]),
               key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
 per = 3 + reps
