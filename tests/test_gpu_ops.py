@@ -377,6 +377,44 @@ def test_conv3x3_winograd_fused_groupnorm_silu_prologue(hip):
     assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("cin,cout,hw,two", [(128, 128, 32, False), (256, 256, 16, False),
+                                             (384, 128, 32, True), (64, 192, 16, False)])
+def test_conv3x3_winograd_prologue_8wave_form(hip, cin, cout, hw, two):
+    """The GroupNorm+SiLU prologue conv without a residual tail runs on the 8-wave, 128-cout
+    workgroup form when Cout % 128 == 0 (csrc/conv_winograd.hip wino_f23_pipe_kernel<1, true,
+    8>; Cout = 192 pads to 256): output and GroupNorm partial statistics vs SiLU(GroupNorm(x))
+    through the plain 4-wave kernel and vs F.conv2d in fp32 (1e-5 relative), incl. the up
+    path's two-source form."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3, conv3x3_fwd_raw, gn_partials
+    from op.norm_act import ACT_SILU, group_norm_act, group_norm_affine
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(3, cin, hw, hw, generator=g) * 2 + 0.5).to(hip)
+    gn = torch.nn.GroupNorm(32, cin, eps=1e-6).to(hip)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(cin, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(cin, generator=g))
+        w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(hip)
+        b = torch.randn(cout, generator=g).to(hip)
+        a = group_norm_act(x, gn, ACT_SILU)
+        ref = F.conv2d(a, w, b, padding=1)
+        plain = conv3x3(a, w, b)
+        pre = group_norm_affine(x, gn)
+        if two:
+            c1 = cin // 3
+            out = conv3x3_fwd_raw(x[:, :c1].contiguous(), w, b, pre=pre, stats=True,
+                                  x2=x[:, c1:].contiguous())
+        else:
+            out = conv3x3(x, w, b, pre=pre, stats=True)
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() <= 1e-5 * scale
+    assert (out - plain).abs().max().item() <= 1e-5 * scale
+    part, R, cnt = gn_partials(out)
+    assert R == (hw // 8) * (hw // 16) and cnt == 128
+    m = out.reshape(3, cout, hw // 8, 8, hw // 16, 16).mean((3, 5)).reshape(3, cout, R)
+    assert (part[..., 0] - m).abs().max().item() <= 1e-5 * scale
+
+
 # ------------------------------------------------------------------ small-channel conv3x3
 @pytest.mark.parametrize("N,cin,cout,h,w", [(2, 1, 128, 128, 128), (3, 3, 64, 20, 36),
                                              (2, 128, 1, 64, 64), (2, 256, 1, 16, 16),
