@@ -492,7 +492,10 @@ __device__ unsigned g_wino_cu[kTsMax];
 // workgroup per CU, NB = 1): the eight waves share one patch / V stream, so the GroupNorm+SiLU
 // patch stores (4 channels per thread instead of 8: half the SiLU work per SIMD per MFMA of the
 // two-workgroup form).
-template <int NB, bool PRE, int WG = 4>
+// TAIL (nch = Cin / 8 even and >= 4): the last three chunks are peeled so they skip the side
+// work of chunks that do not exist (patch loads / stores, the V transform and the filter
+// prefetch past the last chunk, and the last barrier) instead of redoing the last chunk's.
+template <int NB, bool PRE, int WG = 4, bool TAIL = false>
 __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino_f23_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
     const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
@@ -723,10 +726,14 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
   // waves 0-3 (store + load of the patches first, then the V transform), so the two waves of a
   // SIMD -- one from each half, in step through the same barriers -- never run their
   // GroupNorm+SiLU patch stores at the same time
-  auto step = [&](int k, auto sb_c, auto first_c, auto rot_c) __attribute__((always_inline)) {
+  // TM: 0 = full side work, 1 = no patch load (chunk nch - 3), 2 = no patch load / store
+  // (nch - 2), 3 = the last chunk: no side work, no filter prefetch, no barrier
+  auto step = [&](int k, auto sb_c, auto first_c, auto rot_c,
+                  auto tm_c) __attribute__((always_inline)) {
     constexpr int SB = decltype(sb_c)::value;
     constexpr bool FIRST = decltype(first_c)::value;
     constexpr int ROT = decltype(rot_c)::value;
+    constexpr int TM = decltype(tm_c)::value;
     const float* sv = s_v[SB];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
@@ -736,10 +743,10 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
 #if WINO_SCHED == 0 || WINO_SCHED == 4
       __builtin_amdgcn_sched_barrier(0);
 #endif
-      if (sw == 0 && xf) read_d(s_patch_raw[SB ^ 1]);           // patch(k+1)
-      if (sw == 1 && xf) write_v(s_v[SB ^ 1]);                  // V(k+1)
-      if (sw == 2 && pw) store_patch(s_patch_raw[SB], k + 2);   // patch(k+2)
-      if (sw == 3 && pw) load_patch(k + 3);
+      if (TM < 3 && sw == 0 && xf) read_d(s_patch_raw[SB ^ 1]);  // patch(k+1)
+      if (TM < 3 && sw == 1 && xf) write_v(s_v[SB ^ 1]);         // V(k+1)
+      if (TM < 2 && sw == 2 && pw) store_patch(s_patch_raw[SB], k + 2);  // patch(k+2)
+      if (TM < 1 && sw == 3 && pw) load_patch(k + 3);
 #if WINO_SCHED == 0
       __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -754,7 +761,7 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
                 (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb][nb], 0, 0, 0);
         // refill: A of the next group (the next chunk's group 0 comes after the barrier)
         if (grp < 3) a[q] = a_src(sv, grp + 1)[q];
-        if (mb == 1) {
+        if (TM < 3 && mb == 1) {
           const int soff = ((min(k + 1, nch - 1) * kCK + 4 * ks) * g.Cout) * 64;
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb) {
@@ -779,8 +786,8 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
       }
 #endif
     }
-    __syncthreads();
-    {
+    if constexpr (TM < 3) {
+      __syncthreads();
       const f4* src = a_src(s_v[SB ^ 1], 0);
 #pragma unroll
       for (int q = 0; q < 4; ++q) a[q] = src[q];
@@ -793,14 +800,25 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
 #if WINO_PRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
+  using T0 = std::integral_constant<int, 0>;
   auto run = [&](auto rot_c) __attribute__((always_inline)) {
-    step(0, C0{}, std::true_type{}, rot_c);
+    step(0, C0{}, std::true_type{}, rot_c, T0{});
     int k = 1;
-    for (; k + 1 < nch; k += 2) {
-      step(k, C1{}, F{}, rot_c);
-      step(k + 1, C0{}, F{}, rot_c);
+    if constexpr (TAIL) {  // nch even, >= 4: chunks nch - 3, nch - 2, nch - 1 have SB 1, 0, 1
+      for (; k + 1 <= nch - 4; k += 2) {
+        step(k, C1{}, F{}, rot_c, T0{});
+        step(k + 1, C0{}, F{}, rot_c, T0{});
+      }
+      step(k, C1{}, F{}, rot_c, std::integral_constant<int, 1>{});
+      step(k + 1, C0{}, F{}, rot_c, std::integral_constant<int, 2>{});
+      step(k + 2, C1{}, F{}, rot_c, std::integral_constant<int, 3>{});
+    } else {
+      for (; k + 1 < nch; k += 2) {
+        step(k, C1{}, F{}, rot_c, T0{});
+        step(k + 1, C0{}, F{}, rot_c, T0{});
+      }
+      if (k < nch) step(k, C1{}, F{}, rot_c, T0{});
     }
-    if (k < nch) step(k, C1{}, F{}, rot_c);
   };
   // (one call site per instantiation: a second, dead one stopped the inliner and put the
   // accumulators in scratch)
@@ -1329,21 +1347,34 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     const int remap = (blocks % 8 == 0) ? 1 : 0;
     const float2* pre2 = reinterpret_cast<const float2*>(pre);
     hipStream_t st = bpk::as_stream(stream);
-#define WINO_PIPE(NB_, PRE_)                                                                  \
-  hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, \
+#define WINO_PIPE(NB_, PRE_, TAIL_)                                                           \
+  hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_, 4, TAIL_>), dim3((unsigned)blocks), dim3(256), 0, st, \
                      x, U, bias, skip, pre2, y, stats2, g, remap, x2)
+    // BPK_WINO_TAIL=0: no peeled tail chunks (A/B)
+    static const int tail_env = [] {
+      const char* e = getenv("BPK_WINO_TAIL");
+      return e ? atoi(e) : 1;
+    }();
+    const int nch = Cin / kCK;
+    // (GroupNorm-prologue form only: the plain form spills with it)
+    const bool tail = tail_env && pre && nch % 2 == 0 && nch >= 4;
+#define WINO_PIPE8(PRE_, TAIL_)                                                                 \
+  hipLaunchKernelGGL((wino_f23_pipe_kernel<1, PRE_, 8, TAIL_>), dim3((unsigned)blocks), dim3(512), \
+                     0, st, x, U, bias, skip, pre2, y, stats2, g, remap, x2)
     if (wg == 8) {
-      if (pre)
-        hipLaunchKernelGGL((wino_f23_pipe_kernel<1, true, 8>), dim3((unsigned)blocks), dim3(512),
-                           0, st, x, U, bias, skip, pre2, y, stats2, g, remap, x2);
-      else
-        hipLaunchKernelGGL((wino_f23_pipe_kernel<1, false, 8>), dim3((unsigned)blocks), dim3(512),
-                           0, st, x, U, bias, skip, pre2, y, stats2, g, remap, x2);
+      if (pre) {
+        if (tail) WINO_PIPE8(true, true); else WINO_PIPE8(true, false);
+      } else {
+        WINO_PIPE8(false, false);
+      }
     } else if (pnb == 2) {
-      if (pre) WINO_PIPE(2, true); else WINO_PIPE(2, false);
+      if (pre) WINO_PIPE(2, true, false); else WINO_PIPE(2, false, false);
+    } else if (tail) {
+      WINO_PIPE(1, true, true);
     } else {
-      if (pre) WINO_PIPE(1, true); else WINO_PIPE(1, false);
+      if (pre) WINO_PIPE(1, true, false); else WINO_PIPE(1, false, false);
     }
+#undef WINO_PIPE8
 #undef WINO_PIPE
     BPK_LAUNCH_CHECK("conv3x3_wino_pipe");
     return BPK_OK;
