@@ -116,7 +116,7 @@ class DDPM(nn.Module):
             elif kind == "h_from_top":
                 h = hs[-1]
             elif kind == "res_cat":
-                h = mods[step[1]](torch.cat([h, hs.pop()], dim=1), temb)
+                h = mods[step[1]].forward_pair(h, hs.pop(), temb)
             elif kind == "up":
                 h = mods[step[1]](h)
             elif kind == "head":

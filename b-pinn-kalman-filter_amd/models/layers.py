@@ -106,6 +106,8 @@ _IN_FUSED = os.environ.get("BPK_IN_FUSED", "1") != "0"
 # GroupNorm partial statistics from the producing conv's epilogue (BPK_GN_STATS=0: off)
 _GN_STATS = os.environ.get("BPK_GN_STATS", "1") != "0"
 _GEMM1X1 = os.environ.get("BPK_GEMM1X1", "1") != "0"  # 1x1 convs on the MFMA GEMM kernels
+# ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs (BPK_DDPM_FUSED=0: off)
+_DDPM_FUSED = os.environ.get("BPK_DDPM_FUSED", "1") != "0"
 
 
 def _is_3x3(x, conv: nn.Conv2d):
@@ -344,6 +346,12 @@ class ResnetBlockDDPM(nn.Module):
 
     def forward(self, x, temb=None):
         assert x.shape[1] == self.in_ch
+        if _DDPM_FUSED and fused_inference_ok(self, x, self.act):
+            # inference (the nc_ddpmpp sampler): GroupNorm_0+SiLU inside Conv_0's input load
+            h = gn_silu_conv(x, self.GroupNorm_0, self.Conv_0)
+            if h is None:
+                h = conv_nobias(gn_act(x, self.GroupNorm_0, self.act), self.Conv_0)
+            return self._fused_tail(h, x, None, temb)
         h = gn_act(x, self.GroupNorm_0, self.act)
         h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
@@ -354,6 +362,49 @@ class ResnetBlockDDPM(nn.Module):
         if self.in_ch != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
         return conv_residual(h, self.Conv_1, self.Conv_1.bias, x, 1.0)
+
+    def forward_pair(self, x1, x2, temb=None):
+        """forward(torch.cat([x1, x2], 1), temb) -- the up path's skip concatenation -- at
+        inference without building it: GroupNorm_0 from both parts' partial statistics,
+        Conv_0 reading both sources, NIN_0 as one two-source MFMA GEMM (as
+        ResnetBlockBigGANpp.forward_pair); the concatenation when a piece does not fit."""
+        N, C1, H, W = x1.shape
+        C = C1 + x2.shape[1]
+        ok = (_DDPM_FUSED and fused_inference_ok(self, x1, self.act)
+              and fused_inference_ok(self, x2, self.act) and C == self.in_ch and C1 % 8 == 0
+              and x1.is_cuda and x1.dtype == torch.float32
+              and bool(conv_op.lib.bpk_conv3x3_wino_supported(N, C, self.out_ch, H, W)))
+        if ok:
+            p1, p2 = conv_op.ensure_gn_partials(x1), conv_op.ensure_gn_partials(x2)
+            ok = p1 is not None and p2 is not None and p1[1:] == p2[1:]
+        if not ok:
+            return self.forward(cat_channels(x1, x2), temb)
+        ss = norm_act_op.group_norm_affine_partials(p1, N, C, self.GroupNorm_0, part2=p2)
+        h = conv_op.conv3x3_pair(x1, x2, self.Conv_0.weight, pre=ss, stats=_GN_STATS)
+        return self._fused_tail(h, x1, x2, temb)
+
+    def _fused_tail(self, h, x, x2, temb):
+        """(shortcut([x, x2]) + Conv_1(SiLU(GroupNorm_1(h + bias_nc))) + biases) at inference:
+        GroupNorm_1+SiLU in Conv_1's input load, the residual in its epilogue, NIN_0's bias
+        folded into Conv_1's."""
+        bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
+        if temb is not None:
+            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+        bias = self.Conv_1.bias
+        if self.in_ch == self.out_ch:
+            skip = x
+        elif not self.conv_shortcut and _GEMM1X1 and conv_op.gemm1x1_supported(
+                x, self.NIN_0.W.t(), x2):
+            skip = conv_op.conv1x1(x, self.NIN_0.W.t(), None, x2)
+            bias = bias + self.NIN_0.b
+        else:
+            xs = x if x2 is None else cat_channels(x, x2)
+            skip = self.Conv_2(xs) if self.conv_shortcut else self.NIN_0(xs)
+        out = gn_silu_conv(h, self.GroupNorm_1, self.Conv_1, bias_nc, bias, skip, 1.0)
+        if out is not None:
+            return out
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        return conv_residual(h, self.Conv_1, bias, skip, 1.0)
 
 
 # ---------------------------------------------------------------- PINN (NCSN-style) blocks

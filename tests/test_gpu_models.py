@@ -64,6 +64,34 @@ def test_ncsnpp_128_full_size_matches_cpu_oracle(hip):
     _close(out, ref, NET_RTOL, "ncsnpp 128 vs oracle")
 
 
+def test_nc_ddpmpp_128_fused_blocks_match_unfused_and_cpu_oracle(hip, monkeypatch):
+    """The literal nc_ddpmpp net (`ddpm`, 128x128x1) at inference: ResnetBlockDDPM on the
+    GroupNorm+SiLU-prologue Winograd convs with the residual tail in Conv_1's epilogue and
+    GroupNorm statistics from the producers' epilogues (models/layers.py) vs the unfused
+    GroupNorm / conv / residual launches (BPK_DDPM_FUSED=0) and vs the oracle on CPU."""
+    import models  # noqa: F401
+    from configs.vp import nc_ddpmpp
+    from models import layers
+    from models import utils as mutils
+    torch.manual_seed(0)
+    c = nc_ddpmpp.get_config()
+    c.device = hip
+    model = mutils.create_model(c, wrap=False).eval()
+    with torch.no_grad():  # non-zero init everywhere (Conv_1 starts at zero)
+        for p in model.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    x = torch.rand(2, 1, 128, 128)
+    t = torch.tensor([3.0, 870.0])
+    with torch.no_grad():
+        fused = model(x.to(hip), t.to(hip)).cpu().numpy()
+        monkeypatch.setattr(layers, "_DDPM_FUSED", False)
+        plain = model(x.to(hip), t.to(hip)).cpu().numpy()
+    _close(fused, plain, NET_RTOL, "nc_ddpmpp 128 fused vs unfused")
+    params = nets_ref.init_params(model.state_dict())
+    ref = nets_ref.forward(params, c, x, t).numpy()
+    _close(fused, ref, NET_RTOL, "nc_ddpmpp 128 vs oracle")
+
+
 @pytest.mark.parametrize("name", ["em_langevin", "rd_ald", "anc_none", "em_none"])
 def test_pc_sampler_matches_reference_with_injected_noise(hip, name):
     """Fused PC engine, fed the reference's own noise draws, reproduces its samples."""
