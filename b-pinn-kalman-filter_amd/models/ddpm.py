@@ -97,6 +97,11 @@ class DDPM(nn.Module):
             temb = mods[1](self.act(temb))
         else:
             temb = None
+        fused = layers._DDPM_FUSED and layers.fused_inference_ok(self, x, self.act)
+        if temb is not None and fused:
+            # every block's Dense_0 projection of act(temb) as one GEMM (layers.TembBank)
+            temb = layers.TembBank(temb, self.act, [m.Dense_0 for m in mods
+                                                    if isinstance(m, layers.ResnetBlockDDPM)])
         h = x if self.centered else 2 * x - 1.
         x_in = h
         hs: list = []
@@ -120,7 +125,11 @@ class DDPM(nn.Module):
             elif kind == "up":
                 h = mods[step[1]](h)
             elif kind == "head":
-                h = mods[step[2]](layers.gn_act(h, mods[step[1]], self.act))
+                y = None
+                if fused:  # GroupNorm+SiLU in the output conv's input load
+                    y = layers.gn_silu_conv(h, mods[step[1]], mods[step[2]],
+                                            conv_bias=mods[step[2]].bias)
+                h = y if y is not None else mods[step[2]](layers.gn_act(h, mods[step[1]], self.act))
         assert not hs
         if self.scale_by_sigma:
             h = h / self.sigmas[labels, None, None, None]

@@ -356,7 +356,7 @@ class ResnetBlockDDPM(nn.Module):
         h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
         if temb is not None:
-            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+            bias_nc = bias_nc + temb_proj(self.Dense_0, self.act, temb)
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
         h = self.Dropout_0(h)
         if self.in_ch != self.out_ch:
@@ -389,7 +389,7 @@ class ResnetBlockDDPM(nn.Module):
         folded into Conv_1's."""
         bias_nc = self.Conv_0.bias[None, :].expand(h.shape[0], -1)
         if temb is not None:
-            bias_nc = bias_nc + self.Dense_0(self.act(temb))
+            bias_nc = bias_nc + temb_proj(self.Dense_0, self.act, temb)
         bias = self.Conv_1.bias
         if self.in_ch == self.out_ch:
             skip = x
