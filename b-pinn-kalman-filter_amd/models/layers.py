@@ -281,6 +281,11 @@ class AttnBlock(nn.Module):
 
     def forward(self, x):
         h = gn_act(x, self.GroupNorm_0, None)
+        if _DDPM_FUSED and not torch.is_grad_enabled():
+            # inference: AttnBlockpp's stacked q/k/v MFMA GEMM (the same NIN_0..3 layout)
+            from .layerspp import _ATTN_QKV, AttnBlockpp
+            if _ATTN_QKV and AttnBlockpp._qkv_ok(self, h):
+                return residual_rescale(x, AttnBlockpp._forward_qkv(self, h), None, 1.0)
         h = self.NIN_3(_attention(h, self.NIN_0, self.NIN_1, self.NIN_2))
         return residual_rescale(x, h, None, 1.0)
 
