@@ -30,16 +30,20 @@ class ExponentialMovingAverage:
             torch._foreach_lerp_(self.shadow_params, params, 1.0 - decay)
 
     def copy_to(self, parameters):
+        # In-place copies under no_grad (not `p.data.copy_`): they bump the parameter's
+        # version counter, which keys the cached Winograd filter transforms (op/conv.py).
         params = [p for p in parameters if p.requires_grad]
-        for s, p in zip(self.shadow_params, params):
-            p.data.copy_(s.data)
+        with torch.no_grad():
+            for s, p in zip(self.shadow_params, params):
+                p.copy_(s)
 
     def store(self, parameters):
-        self.collected_params = [p.clone() for p in parameters]
+        self.collected_params = [p.detach().clone() for p in parameters]
 
     def restore(self, parameters):
-        for c, p in zip(self.collected_params, parameters):
-            p.data.copy_(c.data)
+        with torch.no_grad():
+            for c, p in zip(self.collected_params, parameters):
+                p.copy_(c)
 
     def state_dict(self):
         return dict(decay=self.decay, num_updates=self.num_updates,

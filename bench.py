@@ -19,6 +19,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -65,6 +67,12 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=8,
                     help="CPU-baseline sample: 1 PC step on this many samples (~10 s on 16 cores)")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--sample-sums", action="store_true",
+                    help="add the per-sample sums of x_mean (global sample order) to the line")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="launcher / rendezvous check only (no GPU work): each rank all-reduces "
+                         "its rank id and rank 0 prints the line skeleton")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="1: MIOpen exhaustive find (cudnn.benchmark); immediate mode (0) picks "
                          "the same fp32 Winograd kernels for the forward and avoids minutes of "
@@ -625,10 +633,73 @@ def _heartbeat(period=45.0):
     threading.Thread(target=run, daemon=True).start()
 
 
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` (N > 1) outside torchrun: start N ranks, one per GPU, as
+    `torch.distributed.run` in a child process (this process never touches the GPU), relay
+    rank 0's JSON line to stdout and exit with the launcher's status.  The reference reaches
+    every visible GPU from one command too (nn.DataParallel, models/utils.py:93)."""
+    backend = os.environ.get("BPK_DIST_BACKEND", "nccl")
+    if backend == "nccl" and not args.plumbing:
+        have = torch.cuda.device_count()  # no HIP context is created by this call
+        if have < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but only {have} GPU(s) visible "
+                  "(BPK_DIST_BACKEND=gloo rehearses several ranks on one device)",
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for out in proc.stdout:
+        if out.startswith("{") and '"metric"' in out:
+            line = out.strip()
+        else:
+            sys.stderr.write(out)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc == 0 and line is None:
+        print("[bench] ranks exited 0 but rank 0 printed no result line", file=sys.stderr)
+        rc = 1
+    if line is not None:
+        print(line, flush=True)
+    return rc
+
+
+def _plumbing(args, ctx):
+    """--plumbing: the multi-rank launch path without GPU work (CPU tests, gloo)."""
+    t = torch.tensor([float(ctx.rank + 1)], dtype=torch.float64)
+    if ctx.world_size > 1:
+        torch.distributed.all_reduce(t)
+    if ctx.rank == 0:
+        print(json.dumps({"metric": "plumbing", "value": float(t.item()), "n_gpus": ctx.world_size,
+                          "backend": torch.distributed.get_backend() if ctx.world_size > 1 else None}),
+              flush=True)
+    if ctx.world_size > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
     _heartbeat()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if world_env is not None and int(world_env) != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world_env}: refusing a mismatched "
+              "launch", file=sys.stderr, flush=True)
+        sys.exit(2)
     import dist
+    if args.plumbing:
+        return _plumbing(args, dist.init_from_env(
+            backend=os.environ.get("BPK_DIST_BACKEND", "gloo")))
     import sampling
     import sde_lib
     ctx = dist.init_from_env()
@@ -666,8 +737,12 @@ def main():
     evals_per_s = evals / dt
     ms_per_step = dt / args.steps * 1e3
 
+    sums = None
+    if args.sample_sums:
+        sums = ctx.all_gather_cat(x.double().sum(dim=(1, 2, 3))).cpu().tolist()
+
     roof = None
-    if ctx.rank == 0:
+    if ctx.rank == 0 and not args.no_roofline:
         log("dominant-kernel roofline (right after the sampler: same clock regime)")
         roof = conv_roofline(dev, B)
 
@@ -734,8 +809,10 @@ def main():
 
     result = None
     if ctx.rank == 0:
-        log("upfirdn2d rooflines")
-        up_roof = upfirdn_rooflines(dev, B)
+        up_roof = None
+        if not args.no_roofline:
+            log("upfirdn2d rooflines")
+            up_roof = upfirdn_rooflines(dev, B)
         model_tflops = evals_per_s * NCSNPP_GFLOP_PER_EVAL / 1e3
         result = {
             "metric": "PC-sampler score-net evals/s (NCSN++ 128x128x1, EM + Langevin)",
@@ -747,13 +824,19 @@ def main():
                                    "euler_maruyama + langevin (snr 0.075), batch 64/GPU",
                        "model": "ncsnpp (62.69M params)", "global_batch": B * world,
                        "seq_len": None, "parallelism": f"dp{world} (batch-sharded, RCCL)",
-                       "hip_graph": eng.graph is not None},
+                       "hip_graph": eng.graph is not None,
+                       "dist_backend": torch.distributed.get_backend() if world > 1 else None,
+                       "pc_graph_allreduce": bool(world > 1 and sampling._graph_collective(ctx))},
             "score_net_tflops": round(model_tflops, 2),
-            "score_net_mfma_frac_direct_equivalent": round(model_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+            "score_net_tflops_basis": "direct-conv FLOP count (333.25 GFLOP/eval, SURVEY 8d); "
+                                      "the Winograd convs execute 4/9 of its 3x3 multiplies, so "
+                                      "this rate may exceed the MFMA peak",
             "samples_finite": finite,
             "roofline": roof,
             "roofline_upfirdn2d": up_roof,
         }
+        if sums is not None:
+            result["sample_sums"] = sums
         for part in (train, cifar, pinn, dps, ns, ncd):
             if part:
                 result.update(part)

@@ -223,3 +223,43 @@ def test_train_step_matches_reference(hip, name, monkeypatch):
         _close(grads[k], d["g:" + k], 2e-3)
     for k, p in model.named_parameters():
         _close(p.detach().cpu().numpy(), d["p1:" + k], 1e-4)
+
+
+def test_eval_step_between_train_steps_leaves_training_unchanged(hip):
+    """The eval step swaps the EMA weights in and out (ema.store / copy_to / restore); the
+    Winograd filter transforms cached on each weight (op/conv.py) must not survive the swap.
+    train -> eval -> train must give the parameters of train -> train."""
+    import losses
+    import models  # noqa: F401
+    import sde_lib
+    from configs.vp import cifar10_ncsnpp_continuous
+    from models import utils as mutils
+    from models.ema import ExponentialMovingAverage
+
+    c = cifar10_ncsnpp_continuous.get_config()
+    c.device = hip
+    c.model.dropout = 0.0
+    c.optim.lr = 1e-2          # large steps: EMA and trained weights differ by O(1e-2)
+    sde = sde_lib.VPSDE(c.model.beta_min, c.model.beta_max, c.model.num_scales)
+    batch = torch.rand(4, 3, 32, 32, device=hip, generator=torch.Generator(device=hip).manual_seed(0))
+
+    def run(with_eval):
+        torch.manual_seed(0)
+        model = mutils.create_model(c, wrap=False).train()
+        opt = losses.get_optimizer(c, model.parameters())
+        ema = ExponentialMovingAverage(model.parameters(), decay=c.model.ema_rate)
+        state = dict(optimizer=opt, model=model, ema=ema, step=c.optim.warmup + 1)
+        kw = dict(reduce_mean=True, continuous=True)
+        train = losses.get_step_fn(sde, True, losses.optimization_manager(c), **kw)
+        evals = losses.get_step_fn(sde, False, **kw)
+        for i in range(2):
+            torch.manual_seed(10 + i)
+            train(state, batch)
+            if with_eval and i == 0:
+                torch.manual_seed(99)
+                evals(state, batch)
+        return [p.detach().clone() for p in model.parameters()]
+
+    ref, got = run(False), run(True)
+    worst = max(float((a - b).abs().max() / b.abs().max().clamp_min(1e-12)) for a, b in zip(got, ref))
+    assert worst <= 1e-5, f"eval step leaked into training: rel diff {worst:.3e}"
