@@ -19,6 +19,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from . import flops
 from ._lib import check, lib, require_hip, stream_ptr, mark_inputs, want_grad
 
 
@@ -140,6 +141,7 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=Fa
         None if b is None else b.data_ptr(), None if sk is None else sk.data_ptr(), float(div),
         y.data_ptr(), None if part is None else part.data_ptr(), N, C, Cout, H, W,
         stream_ptr(x.device)), "conv3x3_wino")
+    flops.wino3x3("wino_dgrad" if ft else "wino_fwd", N, C, Cout, H, W)
     if part is not None:
         attach_gn_partials(y, part, R)
     return y
@@ -178,6 +180,7 @@ def conv3x3_wgrad_raw(x, gy, wshape, bias_grad=False):
     check(lib.bpk_conv3x3_wino_wgrad_bias_f32(
         x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None if db is None else db.data_ptr(),
         ws.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)), "conv3x3_wgrad")
+    flops.wino3x3("wino_wgrad", N, C, Cout, H, W)
     return (dw, db) if bias_grad else dw
 
 
@@ -196,6 +199,7 @@ def conv3x3_small_raw(x, weight, bias=None, pre=None):
         x.data_ptr(), None if pr is None else pr.data_ptr(), w.data_ptr(),
         None if b is None else b.data_ptr(), y.data_ptr(), N, C, Cout, H, W,
         stream_ptr(x.device)), "conv3x3_small")
+    flops.add("valu_conv3x3", 18.0 * N * C * Cout * H * W)
     return y
 
 
@@ -245,6 +249,7 @@ def conv2d_igemm_raw(x, w, bias=None, stride=1, padding=0):
                                        None if b is None else b.data_ptr(), y.data_ptr(),
                                        ws.data_ptr(), N, C, H, W, Co, KH, KW, s[0], s[1], p[0],
                                        p[1], Ho, Wo, stream_ptr(x.device)), "conv2d_igemm_fwd")
+    flops.add("igemm_fwd", 2.0 * N * Co * C * KH * KW * Ho * Wo)
     return y
 
 
@@ -263,6 +268,7 @@ def conv2d_input_igemm_raw(xshape, w, gy, stride=1, padding=0):
                                          ws.data_ptr(), N, C, H, W, Co, KH, KW, s[0], s[1],
                                          p[0], p[1], Ho, Wo, stream_ptr(gy.device)),
           "conv2d_igemm_dgrad")
+    flops.add("igemm_dgrad", 2.0 * N * Co * C * KH * KW * Ho * Wo)
     return gx
 
 
@@ -282,6 +288,7 @@ def conv2d_weight_igemm_raw(x, wshape, gy, stride=1, padding=0, bias_grad=False)
                                          None if db is None else db.data_ptr(), ws.data_ptr(),
                                          N, C, H, W, Co, KH, KW, s[0], s[1], p[0], p[1], Ho, Wo,
                                          stream_ptr(x.device)), "conv2d_igemm_wgrad")
+    flops.add("igemm_wgrad", 2.0 * N * Co * C * KH * KW * Ho * Wo)
     return dw, db
 
 
@@ -637,6 +644,7 @@ def conv1x1(x, weight, bias=None, x2=None):
                                 None if x2 is None else x2.data_ptr(), K2,
                                 None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
                                 stream_ptr(x.device)), "conv1x1")
+    flops.add("gemm1x1", 2.0 * N * M * (K1 + K2) * H * W)
     return y
 
 
@@ -666,6 +674,7 @@ def _gemm1x1_raw(x, w2d, bias=None):
     check(lib.bpk_gemm_nchw_f32(w.data_ptr(), K, x.data_ptr(), K, None, 0,
                                 None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
                                 stream_ptr(x.device)), "conv1x1")
+    flops.add("gemm1x1", 2.0 * N * M * K * H * W)
     return y
 
 
@@ -682,6 +691,7 @@ def _wgrad1x1_raw(gy, x, bias_grad):
     check(lib.bpk_gemm_nchw_wgrad_f32(gy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                                       None if db is None else db.data_ptr(), ws.data_ptr(),
                                       N, M, K, H * W, stream_ptr(x.device)), "conv1x1_wgrad")
+    flops.add("gemm1x1_wgrad", 2.0 * N * M * K * H * W)
     return dw, db
 
 

@@ -133,6 +133,53 @@ def _pmc(key):
         return None
 
 
+def step_roofline(tally, steps_per_s, what, unit_of_work="step", survey_direct=None):
+    """Roofline object of a whole step (train / PINN / DPS rows): achieved =
+    executed FLOPs of one counted step (op.flops: every native MFMA launch on its executed
+    basis -- Winograd 4/9 of direct --, aten matmuls / MIOpen convs via FlopCounterMode on
+    the direct basis) x steps/s, against the f32 MFMA peak."""
+    ex, di = tally.total_executed, tally.total_direct
+    ach = ex * steps_per_s / 1e12
+    out = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+           "kernel": what, "flop_basis": "executed (native kernels as issued; aten ops direct)",
+           f"executed_flop_per_{unit_of_work}": ex, f"direct_flop_per_{unit_of_work}": di,
+           "direct_basis_tflops": round(di * steps_per_s / 1e12, 2),
+           "native_flop_by_kind": {k: round(v["executed"] / 1e12, 4)
+                                   for k, v in tally.summary()["native"].items()},
+           "aten_flop": tally.aten}
+    if survey_direct is not None:
+        out["survey_direct_flop_per_" + unit_of_work] = survey_direct
+    return out
+
+
+def counted(fn, dev):
+    """fn() once inside an op.flops counting block (outside any timed region)."""
+    from op import flops
+    with flops.counting() as tally:
+        r = fn()
+    torch.cuda.synchronize(dev)
+    return tally, r
+
+
+def _ns_valu_cycles():
+    """SIMD-cycles of VALU issue per ns_step full step at B=256, 192^2: SQ_ACTIVE_INST_VALU
+    (quad-cycles) x 4 of the velocity launch + the pressure/density launch, from the committed
+    PMC pass (profiles/r0*_pmc_sq.json; the instruction stream does not depend on the data)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r0*_pmc_sq.json")), reverse=True):
+        try:
+            with open(path) as f:
+                runs = json.load(f)["ns_step launches (3 full steps)"]
+        except (OSError, KeyError, ValueError):
+            continue
+        per = {}
+        for r in runs:
+            per.setdefault(r["_grid"], []).append(4.0 * r["SQ_ACTIVE_INST_VALU"])
+        return sum(sum(v) / len(v) for v in per.values()), os.path.basename(path)
+    return None, None
+
+
 def wino_mix_times(dev, batch, reps=10):
     """Per-shape HIP-event launch times (s) of the PRE+stats and PRE+residual forms."""
     from op.conv import conv3x3, filter_transform
@@ -339,6 +386,104 @@ def cpu_train_baselines():
     return out
 
 
+def cpu_pinn_baseline(B=16, steps=3):
+    """The oracle PINN (oracle/pinn_ref.py: FlowNet + PressureNet on aten CPU ops with the
+    restated correlation and grid_sample double backward, pinned against the reference
+    fixtures by tests/test_pinn_ref.py) trained one configs[3] step at a time on the host
+    cores: data losses + pinn_loss_weight x equation_mse, backward, two Adams, EMA.  Bounded
+    sample: B = 16 (instead of 64), 1 warm-up + `steps` timed."""
+    from configs.pinn import pinn_pde
+    from oracle import pinn_ref
+    from pinn_kalman.pinn import PINN
+    cores = _cpu_threads()
+    torch.set_num_threads(cores)
+    c = pinn_pde.get_config()
+    c.device = torch.device("cpu")
+    torch.manual_seed(0)
+    P = pinn_ref.init_params(PINN(c).state_dict())
+    fl = [v for k, v in P.items() if k.startswith("flownet.")]
+    pr = [v for k, v in P.items() if k.startswith("pressurenet.")]
+    opt_f, opt_p = torch.optim.Adam(fl, lr=1e-3), torch.optim.Adam(pr, lr=5e-3)
+    ema = [v.detach().clone() for v in fl + pr]
+    g = torch.Generator().manual_seed(0)
+    n = c.data.image_size
+    lin = torch.linspace(0.05, 1.0, n)
+    f1, f2 = torch.rand(B, 1, n, n, generator=g), torch.rand(B, 1, n, n, generator=g)
+    x = (lin.view(1, 1, 1, n) + 0.01 * torch.rand(B, 1, n, n, generator=g)).requires_grad_()
+    y = (lin.view(1, 1, n, 1) + 0.01 * torch.rand(B, 1, n, n, generator=g)).requires_grad_()
+    t = torch.randint(300, 900, (B,), generator=g).float().requires_grad_()
+    target = torch.randn(B, 3, n, n, generator=g) * 0.5
+    mask = (torch.rand(B, 1, n, n, generator=g) > 0.1).float()
+
+    def step():
+        opt_f.zero_grad()
+        opt_p.zero_grad()
+        noise = (torch.randn(B, 1, n, n), torch.randn(B, 1, n, n))
+        loss, _, _ = pinn_ref.pinn_loss(P, c, (f1, f2, x, y, t, target), mask, noise)
+        loss.backward()
+        opt_f.step()
+        opt_p.step()
+        with torch.no_grad():
+            for e, v in zip(ema, fl + pr):
+                e.mul_(0.9).add_(v.detach(), alpha=0.1)
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(B / dt, 4), "unit": "train samples/s", "steps_per_s": round(1 / dt, 4),
+            "batch": B, "cores": cores, "kind": "port",
+            "sample": f"oracle/pinn_ref PINN step (configs[3] pinn_pde 64x64) at B={B}: 1 warm-up "
+                      f"+ {steps} timed, {dt:.2f}s/step"}
+
+
+def cpu_dps_baseline(nfe=1):
+    """One DPS function evaluation (reference inverse/conditional_sampling.py:100-169: score
+    forward, x0_hat, inpainting residual norm, input gradient through the net, drift) on the
+    oracle ddpm net (oracle/nets_ref.py, the reference's aten op sequence) at 256x256 on the
+    host cores.  Bounded sample: B = 1 (instead of 16), 1 warm-up + `nfe` timed evaluations;
+    unit sample-NFE/s."""
+    from configs.vp import nc_ddpmpp
+    from oracle import nets_ref, score_sde_ref
+    import models  # noqa: F401
+    from models import utils as mutils
+    cores = _cpu_threads()
+    torch.set_num_threads(cores)
+    c = nc_ddpmpp.get_config()
+    c.data.image_size = 256
+    c.device = "cpu"
+    torch.manual_seed(0)
+    params = nets_ref.init_params(mutils.create_model(c, wrap=False).state_dict())
+    sde = score_sde_ref.SDESpec("vp", N=c.model.num_scales, beta_min=c.model.beta_min,
+                                beta_max=c.model.beta_max)
+    score = score_sde_ref.make_score(lambda v, tt: nets_ref.forward(params, c, v, tt), sde, True)
+    g = torch.Generator().manual_seed(0)
+    n = 256
+    mask = (torch.rand(1, 1, n, n, generator=g) > 0.5).float()
+    obs = mask * torch.rand(1, 1, n, n, generator=g)
+    x = torch.randn(1, 1, n, n, generator=g)
+    t = torch.full((1,), 0.5)
+
+    def one():
+        xt = x.detach().requires_grad_()
+        sc = score(xt, t)
+        mean, std = sde.marginal_mean_coef(t), sde.marginal_std(t)
+        x0 = xt / mean[:, None, None, None] + std[:, None, None, None] ** 2 * sc
+        diff = obs - mask * x0
+        norm = torch.linalg.norm(diff)
+        gr = torch.autograd.grad(-norm ** 2 / 0.1, xt)[0] / norm.detach()
+        dc, dif = sde.coefficient(t)
+        return dc[:, None, None, None] * x - dif[:, None, None, None] ** 2 * (sc.detach() + gr) * 0.5
+    one()
+    t0 = time.perf_counter()
+    for _ in range(nfe):
+        one()
+    dt = (time.perf_counter() - t0) / nfe
+    return {"value": round(1 / dt, 4), "unit": "sample-NFE/s", "cores": cores, "kind": "port",
+            "sample": f"oracle nets_ref ddpm 256x256 DPS evaluation (forward + input gradient) "
+                      f"at B=1: 1 warm-up + {nfe} timed, {dt:.2f}s each"}
+
+
 def cpu_ns_baseline():
     """The C restatement of the reference ns_step (oracle/ns_step_ref.c, single thread) on a
     bounded sample: B = 16 replicas of 192x192, 3 full steps (velocity, pressure, density)."""
@@ -406,7 +551,21 @@ def bench_ns_step(args, ctx, dev):
                                  "frac": round(gbs / HBM_PEAK_GBS, 4),
                                  "traffic": _pmc("ns_step full step B256 192^2"),
                                  "kernel": "ns_step fused velocity + pressure/density launches",
-                                 "bytes_per_step": 32.0 * sites}}
+                                 "bytes_per_step": 32.0 * sites},
+            "roofline_ns_step_valu": _ns_valu_roofline(t_step)}
+
+
+def _ns_valu_roofline(t_step):
+    cyc, src = _ns_valu_cycles()
+    if cyc is None:
+        return None
+    peak = 1024 * 2.4e9  # SIMD-cycles/s: 256 CUs x 4 SIMDs at the 2.4 GHz max clock
+    ach = cyc / t_step
+    return {"bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
+            "unit": "T SIMD-issue-cycles/s", "frac": round(ach / peak, 4), "traffic": None,
+            "kernel": "ns_step full step (velocity + pressure/density launches)",
+            "basis": f"VALU-active SIMD-cycles per step {cyc:.4g} (SQ_ACTIVE_INST_VALU x 4, {src}) "
+                     "/ live step time, vs 1024 SIMDs x 2.4 GHz"}
 
 
 def bench_ncddpmpp(args, ctx, dev):
@@ -494,6 +653,7 @@ def bench_cifar_train(args, ctx, dev):
     batch = torch.rand(B, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(ctx.rank))
     for _ in range(2):
         step_fn(state, batch)
+    tally, _ = counted(lambda: step_fn(state, batch), dev)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
@@ -508,7 +668,10 @@ def bench_cifar_train(args, ctx, dev):
             "cifar_train_ms_per_step": round(dt / args.cifar_steps * 1e3, 2),
             "cifar_train_global_batch": B * ctx.world_size,
             "cifar_train_loss": round(float(loss.item()), 5),
-            "cifar_config": "configs[1]: cifar10_ncsnpp_continuous 32x32x3, batch 128/GPU"}
+            "cifar_config": "configs[1]: cifar10_ncsnpp_continuous 32x32x3, batch 128/GPU",
+            "roofline_cifar_train": step_roofline(
+                tally, args.cifar_steps / dt, "configs[1] DSM train step, NCSN++ CIFAR-10 32x32x3 "
+                "B=128/GPU", survey_direct=8.36e12)}
 
 
 def _pinn_run(args, ctx, dev, graph):
@@ -532,6 +695,9 @@ def _pinn_run(args, ctx, dev, graph):
     # graph: two eager steps, then the capture (outside the timed region)
     for _ in range(max(args.pinn_warmup, 3) if graph else args.pinn_warmup):
         step_fn(state, operator, batch)
+    tally = None
+    if not graph:
+        tally, _ = counted(lambda: step_fn(state, operator, batch), dev)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
@@ -542,7 +708,7 @@ def _pinn_run(args, ctx, dev, graph):
     ctx.barrier()
     torch.cuda.synchronize(dev)
     dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
-    return dt, (loss, pinn_loss, data_loss)
+    return dt, (loss, pinn_loss, data_loss), tally
 
 
 def bench_pinn(args, ctx, dev):
@@ -553,8 +719,15 @@ def bench_pinn(args, ctx, dev):
     Eager.  --pinn-graph times the hipGraph-replay form instead (get_pinn_step_fn(graph=True),
     experimental: its replays read stale memory after ~4 replays in this configuration, see
     DESIGN.md section 8; the line then carries its losses so a NaN shows)."""
-    dt, losses_ = _pinn_run(args, ctx, dev, graph=args.pinn_graph)
-    return {"pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
+    dt, losses_, tally = _pinn_run(args, ctx, dev, graph=args.pinn_graph)
+    roof = None
+    if tally is not None:
+        roof = step_roofline(tally, args.pinn_steps / dt, "configs[3] PINN train step (FlowNet + "
+                             "PressureNet fwd, equation_mse 1st/2nd derivatives, backward, 2x Adam, "
+                             "EMA), B=64/GPU 64x64; latency-bound: ~10k launches per step")
+        roof["bound_note"] = ("mfma is the nominal bound; the step is launch/latency-bound (small "
+                              "images, ~10k kernels), so frac is low by construction")
+    return {"roofline_pinn": roof, "pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
             "pinn_ms_per_step": round(dt / args.pinn_steps * 1e3, 2),
             "pinn_mode": "hipGraph replay (experimental)" if args.pinn_graph else "eager",
             "pinn_global_batch": args.batch * ctx.world_size,
@@ -596,6 +769,13 @@ def bench_dps(args, ctx, dev):
     z = torch.randn(B, 1, n, n, device=dev, generator=g)
     c.inverse.max_steps = 1
     sampler(model, z=z)  # warm-up (kernel selection, allocator)
+    from models.utils import input_grad_only
+    f = sampler.make_ode_func(model)
+
+    def one_nfe():
+        with input_grad_only(model):
+            return f(0.5, z.reshape(-1).to(torch.float64))
+    tally, _ = counted(one_nfe, dev)
     c.inverse.max_steps = args.dps_steps
     torch.cuda.synchronize(dev)
     ctx.barrier()
@@ -608,7 +788,11 @@ def bench_dps(args, ctx, dev):
     return {"dps_nfe_per_s": round(nfe / dt, 3), "dps_sample_nfe_per_s": round(nfe * B * ctx.world_size / dt, 2),
             "dps_nfe_timed": nfe, "dps_global_batch": B * ctx.world_size,
             "dps_finite": bool(torch.isfinite(x).all().item()),
-            "dps_config": "configs[4]: nc_ddpmpp_inpaint_dps @256x256 (ddpm net), B=16/GPU, RK45"}
+            "dps_config": "configs[4]: nc_ddpmpp_inpaint_dps @256x256 (ddpm net), B=16/GPU, RK45",
+            "roofline_dps": step_roofline(tally, nfe / dt, "configs[4] DPS function evaluation "
+                                          "(ddpm 256x256 forward + input gradient through the net, "
+                                          "B=16/GPU)", unit_of_work="nfe",
+                                          survey_direct=2 * 1198.88e9 * B)}
 
 
 _PHASE = ["start"]
@@ -766,6 +950,7 @@ def main():
         log(f"sampler {evals_per_s:.1f} evals/s; train warm-up")
         for _ in range(args.train_warmup):
             step_fn(state, batch)
+        tally, _ = counted(lambda: step_fn(state, batch), dev)
         torch.cuda.synchronize(dev)
         ctx.barrier()
         torch.cuda.synchronize(dev)
@@ -779,8 +964,11 @@ def main():
         train = {"train_steps_per_s": round(args.train_steps / tdt, 4),
                  "train_ms_per_step": round(tdt / args.train_steps * 1e3, 2),
                  "train_global_batch": B * world, "train_loss": round(float(loss.item()), 5),
-                 "train_tflops": round(args.train_steps * B * world * NCSNPP_GFLOP_PER_TRAIN_SAMPLE
-                                       / tdt / 1e3, 2)}
+                 "train_tflops_direct_basis": round(args.train_steps * B * world * NCSNPP_GFLOP_PER_TRAIN_SAMPLE
+                                                    / tdt / 1e3, 2),
+                 "roofline_train": step_roofline(
+                     tally, args.train_steps / tdt, "configs[2] DSM train step, NCSN++ 128x128x1 B=64/GPU "
+                     "(fwd + bwd-data + wgrad + clip + Adam + EMA)", survey_direct=63.9e12)}
 
     cifar = None
     if args.cifar_steps > 0 and not args.no_train:
@@ -848,6 +1036,10 @@ def main():
         extra = {"upfirdn2d": cpu_upfirdn_baseline(), "ns_step": cpu_ns_baseline()}
         if not args.no_train:
             extra.update(cpu_train_baselines())
+        if not args.no_pinn:
+            extra["pinn"] = cpu_pinn_baseline()
+        if not args.no_dps:
+            extra["dps"] = cpu_dps_baseline()
         result["cpu_baselines_other"] = extra
     if ctx.rank == 0:
         print(json.dumps(result), flush=True)
