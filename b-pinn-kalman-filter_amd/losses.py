@@ -344,15 +344,18 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                      * config.training.pinn_loss_weight)
         return pinn_loss + data_loss, pinn_loss, data_loss
 
-    # graph=True (training, EXPERIMENTAL -- not used by bench.py by default): in the full
-    # configs[3] setup (B = 64, 64x64) the replayed step turns to garbage / NaN after ~4
-    # replays, while a capture of the model alone replays correctly (tools/diag_pinn_graph*.py,
-    # DESIGN.md section 8); tests/test_gpu_pinn.py covers two replays of the small config.
-    # After two eager steps, the forward, the residual's first and
-    # second derivatives and the backward are captured once in a hipGraph and replayed with
-    # the step's batch / mask copied into static buffers -- the ~17k small kernel launches
-    # of a step are issued by the device instead of the host.  Gradient all-reduce, the NaN
-    # check, the optimizers and the EMA stay eager.
+    # graph=True: after two eager steps, the forward, the residual's first and second
+    # derivatives and the backward are captured once in a hipGraph and replayed with the
+    # step's batch / mask copied into static buffers -- the ~10k small kernel launches of a
+    # step are issued by the device instead of the host.  Gradient all-reduce, the NaN check,
+    # the optimizers and the EMA stay eager.
+    #
+    # Every tensor the graph writes must be owned by the graph's private pool: the gradients
+    # are set to None before the capture, so the captured AccumulateGrad nodes allocate them
+    # there (round 2 zeroed the eager .grad tensors inside the capture instead; the replays
+    # then accumulated into whatever those blocks held once an eager step had re-allocated
+    # them -- garbage / NaN after a few replays).  The pool gradients are re-attached before
+    # every replay, so a zero_grad(set_to_none=True) between steps cannot detach them.
     gstate = {"eager": 0}
 
     def graph_forward_backward(model, operator, batch, opt_flow, opt_pres):
@@ -362,6 +365,7 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
             opt_pres.zero_grad(set_to_none=False)
             return loss_fn(model, operator, batch)
         dev = batch[0].device
+        params = [p for p in model.parameters() if p.requires_grad]
         if "graph" not in gstate:
             sb = []
             for t in batch:
@@ -383,14 +387,14 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
             # drop the warm-up graph: its AccumulateGrad nodes (created on the side stream)
             # would otherwise be reused by the capture, on another stream
             del l3
+            for t in list(params) + list(gstate["batch"]):
+                t.grad = None
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for p in model.parameters():
-                    if p.grad is not None:
-                        p.grad.zero_()
                 out = loss_fn(model, operator, gstate["batch"])
                 out[0].backward()
             operator.mask = real_mask
+            gstate["grads"] = [p.grad for p in params]
             # detached views of the static outputs: replays rewrite them in place, and no
             # autograd graph outlives the capture
             gstate["graph"], gstate["out"] = g, tuple(o.detach() for o in out)
@@ -400,6 +404,9 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                 if s_ is not t:
                     s_.copy_(t)
             gstate["mask"].copy_(operator.mask, non_blocking=True)
+        for p, gr in zip(params, gstate["grads"]):
+            if p.grad is not gr:
+                p.grad = gr
         gstate["graph"].replay()
         return gstate["out"]
 

@@ -3,8 +3,10 @@
 The native MFMA kernels are launched through ctypes, which torch's FlopCounterMode cannot
 see, so every launch site in op/conv.py reports its own count here while a `counting()`
 block is open; the aten ops that remain (MIOpen convolutions the per-call selection keeps,
-rocBLAS bmm of the attention blocks, linear layers) are counted by FlopCounterMode inside
-the same block.  Two bases per launch:
+rocBLAS bmm of the attention blocks, linear layers) are counted inside the same block by a
+TorchDispatchMode over torch.utils.flop_counter's per-op formulas (FlopCounterMode itself
+adds module-tracking autograd hooks that cannot run inside the PINN residual's
+torch.autograd.grad passes).  Two bases per launch:
   executed  the multiplies the kernel actually issues -- Winograd F(2x2,3x3) does 16 per
             2x2 output tile per (cin, cout), i.e. 4/9 of the direct count;
   direct    2 * MACs of the direct convolution / GEMM (SURVEY.md 8(d)'s FlopCounterMode basis).
@@ -58,20 +60,35 @@ def wino3x3(kind, N, C, Cout, H, W):
         add(kind, 32.0 * N * C * Cout * ((H + 1) // 2) * ((W + 1) // 2), 18.0 * N * C * Cout * H * W)
 
 
+def _aten_mode():
+    from torch.utils._python_dispatch import TorchDispatchMode
+    from torch.utils.flop_counter import flop_registry
+
+    class AtenFlops(TorchDispatchMode):
+        total = 0
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            kwargs = kwargs or {}
+            out = func(*args, **kwargs)
+            f = flop_registry.get(func._overloadpacket)
+            if f is not None:
+                self.total += f(*args, **kwargs, out_val=out)
+            return out
+
+    return AtenFlops()
+
+
 @contextlib.contextmanager
 def counting(aten=True):
-    """Tally every native launch (and, with aten=True, every aten matmul / convolution via
-    torch.utils.flop_counter.FlopCounterMode) issued inside the block."""
+    """Tally every native launch (and, with aten=True, every aten matmul / convolution,
+    counted with torch.utils.flop_counter's formulas) issued inside the block."""
     t = Tally()
     _ACTIVE.append(t)
-    mode = contextlib.nullcontext()
-    if aten:
-        from torch.utils.flop_counter import FlopCounterMode
-        mode = FlopCounterMode(display=False)
+    mode = _aten_mode() if aten else contextlib.nullcontext()
     try:
         with mode:
             yield t
     finally:
         _ACTIVE.remove(t)
         if aten:
-            t.aten = float(mode.get_total_flops())
+            t.aten = float(mode.total)

@@ -24,3 +24,5 @@ PY
 rc=$?; cat gpurun_out/ema_old.log | tail -2; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 python bench.py > gpurun_out/bench_b.log 2> gpurun_out/bench_b.err || { tail -20 gpurun_out/bench_b.err; exit 1; }
 cat gpurun_out/bench_b.log
+timeout -k 10 600 python -u tools/diag_pinn_graph4.py > gpurun_out/diag_pinn_graph4.log 2>&1; rc=$?
+tail -14 gpurun_out/diag_pinn_graph4.log; [ $rc -eq 0 ] || exit $rc
