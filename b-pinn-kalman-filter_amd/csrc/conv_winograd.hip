@@ -139,6 +139,11 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 #ifndef WINO_PRIO
 #define WINO_PRIO 0
 #endif
+// 8-wave form (A/B): static s_setprio 1 for the second-dispatched half (waves 4-7) through the
+// chunk loop (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+#ifndef WINO_PRIO8
+#define WINO_PRIO8 0
+#endif
 
 __device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 
@@ -800,6 +805,9 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
 #if WINO_PRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
+#if WINO_PRIO8
+  if (WG == 8 && ph) __builtin_amdgcn_s_setprio(1);
+#endif
   using T0 = std::integral_constant<int, 0>;
   auto run = [&](auto rot_c) __attribute__((always_inline)) {
     step(0, C0{}, std::true_type{}, rot_c, T0{});
@@ -886,6 +894,277 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
             const float d = sm - lm;
             lm = lm + d * kW[st];
             lm2 = (lm2 + sm2) + d * d * (4.f * st * kW[st]);
+          }
+        }
+      }
+    }
+    if (stats) {
+      merge_stats(lm, lm2, __shfl_xor(lm, 16, 64), __shfl_xor(lm2, 16, 64), 32.f);
+      merge_stats(lm, lm2, __shfl_xor(lm, 32, 64), __shfl_xor(lm2, 32, 64), 64.f);
+      if (kq == 0) {
+        const int R = g.regions_x * g.regions_y;
+        const int region = (oy0 / kOutRows) * g.regions_x + ox0 / kOutCols;
+        stats[((int64_t)n * g.CoutS + co) * R + region] = make_float2(lm, lm2);
+      }
+    }
+  }
+  WINO_TS(5);
+}
+
+// 16-cin chunk form of the 8-wave pipelined kernel (one workgroup per CU, 8 waves x 16 couts =
+// 128 couts, 32 tiles).  With 8-cin chunks the 8 waves transform the 256 (cin, tile) records of
+// a chunk twice (waves w and w + 4 write identical V records: a wave-uniform branch around the
+// transform made the compiler spill) and meet at a barrier every 64 MFMAs per wave.  Here a
+// chunk is 16 input channels: the 512 threads own one (cin, tile) record each (no duplicate
+// transform), every thread stages 8 channels of the patch (as the 4-wave form), and each wave
+// issues 128 MFMAs per barrier; the side work of a chunk spreads over 8 MFMA groups.  The B
+// operands (U) keep two k-step slots in registers: the slot a group has just finished is
+// refilled with the k-step two ahead (next chunk's for the last two), one group pair before use.
+// LDS: 2 x 15 KB patches + 2 x 40 KB V + the GroupNorm table (8 KB) = 118 KB.
+template <bool PRE>
+__global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
+    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
+    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
+    float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2) {
+  constexpr int CK = 16;
+  constexpr int kPatch = CK * kPR * kPCp;
+  __shared__ __attribute__((aligned(16))) float s_patch_raw[2][kPatch];
+  constexpr int kVBuf = CK * kM * kVS;
+  __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];
+  __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];
+
+  WINO_TS(0);
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const unsigned nblk = gridDim.x;
+  unsigned b = blockIdx.x;
+  if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
+  unsigned cb, rx, ry;
+  unsigned r = udivmod(b, (unsigned)g.cout_blocks, cb);
+  r = udivmod(r, (unsigned)g.regions_x, rx);
+  const int n = (int)udivmod(r, (unsigned)g.regions_y, ry);
+  const int oy0 = (int)ry * kOutRows, ox0 = (int)rx * kOutCols;
+  const int cout_w = (int)cb * 128 + wave * 16;
+  const int ph = __builtin_amdgcn_readfirstlane(tid >> 8);  // channels 8 ph .. 8 ph + 7
+
+  f4 acc[16][2];
+  const int64_t plane = (int64_t)g.H * g.W;
+  const int C2 = g.Cin - g.C1;
+  const float* xn = x + (int64_t)n * g.C1 * plane;
+  const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
+  const int kq = lane >> 4, jj = lane & 15;
+  const int nch = g.Cin / CK;
+
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xn), 0, (int)(g.C1 * plane * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(C2 > 0 ? x2 + (int64_t)n * C2 * plane : xn), 0,
+      (int)((C2 > 0 ? C2 : g.C1) * plane * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
+
+  constexpr int kPos = kPR * kPC;  // 180 patch positions; threads >= 180 of a half duplicate 0
+  int poff, pdst;
+  bool pin;
+  {
+    const int t8 = tid & 255;
+    const int t = t8 < kPos ? t8 : 0;
+    const int py = t / kPC, px = t - py * kPC;
+    const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+    pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+    const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
+    poff = (cy * g.W + cx) * 4;
+    pdst = py * kPCp + px + ph * 8 * (kPR * kPCp);
+  }
+  float pv[8];
+  auto load_patch_part = [&](float* dst, int k, int c0, int cn) {
+    const int cc = min(k, nch - 1) * CK;
+    const bool second = cc >= g.C1;
+    const int soff = ((second ? cc - g.C1 : cc) + ph * 8) * (int)plane * 4;
+#pragma unroll
+    for (int c = c0; c < c0 + cn; ++c)
+      dst[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          second ? xrs2 : xrs, poff, soff + c * (int)plane * 4, 0));
+  };
+  auto store_patch_part = [&](const float* src, float* sp, int k, int c0, int cn) {
+    const int cb0 = min(k, nch - 1) * CK + ph * 8;
+#pragma unroll
+    for (int c = c0; c < c0 + cn; ++c) {
+      float v = src[c];
+      if (PRE) {
+        const float2 st = s_ss[cb0 + c];
+        v = silu_f(v * st.x + st.y);
+      }
+      sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
+    }
+  };
+  // B operands: uo[ks & 1][q] = U[c0 + 4 ks + kq][cout_w + jj][4q..4q + 3]
+  f4 uo[2][4];
+  const int uoff = ((kq * g.Cout + cout_w + jj) * 16) * 4;
+  auto u_soff = [&](int k, int ks) { return ((min(k, nch - 1) * CK + 4 * ks) * g.Cout) * 64; };
+  auto load_u = [&](int slot, int k, int ks) {
+    const int soff = u_soff(k, ks);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      using u4 = __attribute__((ext_vector_type(4))) unsigned;
+      const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff, 0);
+      uo[slot][q] = __builtin_bit_cast(f4, w);
+    }
+  };
+  // V = B^T d B of one (cin, tile) per thread (512 records = 16 cin x 32 tiles)
+  const int tc = tid >> 5, tm = tid & 31;
+  const int tty = tm / kTC, ttx = tm - tty * kTC;
+  float d[4][4];
+  auto read_d = [&](const float* sp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const float2 v2 =
+            *reinterpret_cast<const float2*>(&sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j]);
+        d[i][j] = v2.x;
+        d[i][j + 1] = v2.y;
+      }
+  };
+  auto write_v = [&](float* sv) {
+    float t[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[0][j] = d[0][j] - d[2][j];
+      t[1][j] = d[1][j] + d[2][j];
+      t[2][j] = d[2][j] - d[1][j];
+      t[3][j] = d[1][j] - d[3][j];
+    }
+    f4* dst = reinterpret_cast<f4*>(&sv[(tc * kM + tm) * kVS]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
+  };
+
+  // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight
+  {
+    float pv0[8], pv1[8];
+    load_patch_part(pv0, 0, 0, 8);
+    load_patch_part(pv1, 1, 0, 8);
+    load_patch_part(pv, 2, 0, 8);
+    load_u(0, 0, 0);
+    load_u(1, 0, 1);
+    if (PRE) {
+      for (int c = tid; c < g.Cin; c += 512) s_ss[c] = pre_n[c];
+      __syncthreads();
+    }
+    WINO_TS(1);
+    store_patch_part(pv0, s_patch_raw[0], 0, 0, 8);
+    store_patch_part(pv1, s_patch_raw[1], 1, 0, 8);
+  }
+  __syncthreads();
+  WINO_TS(2);
+  read_d(s_patch_raw[0]);
+  write_v(s_v[0]);
+  __syncthreads();
+
+  f4 a[4];
+  auto a_src = [&](const float* sv, int grp) {  // grp = 2 ks + mb
+    const int ks = grp >> 1, mb = grp & 1;
+    return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
+  };
+  {
+    const f4* src = a_src(s_v[0], 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = src[q];
+  }
+  auto step = [&](int k, auto sb_c, auto first_c) __attribute__((always_inline)) {
+    constexpr int SB = decltype(sb_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
+    const float* sv = s_v[SB];
+#pragma unroll
+    for (int grp = 0; grp < 8; ++grp) {
+      const int ks = grp >> 1, mb = grp & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                        // patch(k+1)
+      if (grp == 1) write_v(s_v[SB ^ 1]);                               // V(k+1)
+      if (grp == 2) store_patch_part(pv, s_patch_raw[SB], k + 2, 0, 4);  // patch(k+2)
+      if (grp == 3) store_patch_part(pv, s_patch_raw[SB], k + 2, 4, 4);
+      if (grp == 4) load_patch_part(pv, k + 3, 0, 4);
+      if (grp == 5) load_patch_part(pv, k + 3, 4, 4);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp)
+          acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              a[q][pp], uo[ks & 1][q][pp],
+              (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb], 0, 0, 0);
+        if (grp < 7) a[q] = a_src(sv, grp + 1)[q];
+        if (mb == 1) {  // k-step ks + 2 of this chunk, or ks - 2 of the next
+          const int soff = ks < 2 ? u_soff(k, ks + 2) : u_soff(k + 1, ks - 2);
+          using u4 = __attribute__((ext_vector_type(4))) unsigned;
+          const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff, 0);
+          uo[ks & 1][q] = __builtin_bit_cast(f4, w);
+        }
+      }
+    }
+    __syncthreads();
+    const f4* src = a_src(s_v[SB ^ 1], 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = src[q];
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  WINO_TS(3);
+  step(0, C0{}, std::true_type{});
+  int k = 1;
+  for (; k + 1 < nch; k += 2) {
+    step(k, C1{}, std::false_type{});
+    step(k + 1, C0{}, std::false_type{});
+  }
+  if (k < nch) step(k, C1{}, std::false_type{});
+  WINO_TS(4);
+
+  // output transform straight from registers (as wino_f23_pipe_kernel, NB = 1)
+  const float rdiv = 1.f / g.div;
+  if (cout_w < g.CoutS) {
+    const int co = cout_w + jj;
+    const float bv = bias ? bias[co] : 0.f;
+    const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
+    float lm = 0.f, lm2 = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int oy = oy0 + 2 * (2 * mb + (kq >> 1));
+      const int ox = ox0 + 8 * (kq & 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          f4 v;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int rg = 2 * e + u;
+            float t[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              t[j] = h == 0 ? acc[j][mb][rg] + acc[4 + j][mb][rg] + acc[8 + j][mb][rg]
+                            : acc[4 + j][mb][rg] - acc[8 + j][mb][rg] - acc[12 + j][mb][rg];
+            v[2 * u] = t[0] + t[1] + t[2] + bv;
+            v[2 * u + 1] = t[1] - t[2] - t[3] + bv;
+          }
+          const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
+          if (skip) {
+            const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = div_rn(sk[c] + v[c], g.div, rdiv);
+          }
+          *reinterpret_cast<f4*>(&y[o]) = v;
+          if (stats) {
+            const float sm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+            float sm2 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sm2 = fmaf(v[c] - sm, v[c] - sm, sm2);
+            constexpr float kW[8] = {1.f, 1.f / 2, 1.f / 3, 1.f / 4, 1.f / 5, 1.f / 6, 1.f / 7, 1.f / 8};
+            const int st = 4 * mb + 2 * h + e;
+            const float dd = sm - lm;
+            lm = lm + dd * kW[st];
+            lm2 = (lm2 + sm2) + dd * dd * (4.f * st * kW[st]);
           }
         }
       }
@@ -1340,6 +1619,29 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     }();
     const bool w8_case = w8_env == 2 || (w8_env == 1 && pre && !skip) || (w8_env == 3 && !skip);
     const int wg = (w8_case && pnb == 1 && CoutP % 128 == 0) ? 8 : 4;
+    // the 16-cin chunk form of the 8-wave kernel (BPK_WINO_K16: 0 off, 1 = where the 8-wave
+    // form runs, 2 = every launch it supports)
+    static const int k16_env = [] {
+      const char* e = getenv("BPK_WINO_K16");
+      return e ? atoi(e) : 0;
+    }();
+    const bool k16 = k16_env && pnb == 1 && CoutP % 128 == 0 && Cin % 16 == 0 && C1 % 16 == 0 &&
+                     (k16_env == 2 || wg == 8);
+    if (k16) {
+      WinoGeo gk{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / 128, div, C1, Cout};
+      const int64_t kblocks = (int64_t)N * gk.regions_x * gk.regions_y * gk.cout_blocks;
+      BPK_REQUIRE(kblocks < (1LL << 31), "conv3x3_wino: grid too large");
+      const int kremap = (kblocks % 8 == 0) ? 1 : 0;
+      const float2* kpre = reinterpret_cast<const float2*>(pre);
+      if (pre)
+        hipLaunchKernelGGL((wino_f23_k16_kernel<true>), dim3((unsigned)kblocks), dim3(512), 0,
+                           bpk::as_stream(stream), x, U, bias, skip, kpre, y, stats2, gk, kremap, x2);
+      else
+        hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3((unsigned)kblocks), dim3(512), 0,
+                           bpk::as_stream(stream), x, U, bias, skip, kpre, y, stats2, gk, kremap, x2);
+      BPK_LAUNCH_CHECK("conv3x3_wino_k16");
+      return BPK_OK;
+    }
     WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * pnb * wg / 4), div,
               C1, Cout};
     const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
