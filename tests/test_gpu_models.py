@@ -227,9 +227,11 @@ def test_train_step_matches_reference(hip, name, monkeypatch):
 
 def test_eval_step_between_train_steps_leaves_training_unchanged(hip):
     """The eval step swaps the EMA weights in and out (ema.store / copy_to / restore); the
-    Winograd filter transforms cached on each weight (op/conv.py) must not survive the swap
-    (`p.data.copy_` kept the version counter that keys the cache).  A training-mode
-    forward after an eval step must equal the one before it, bit for bit."""
+    Winograd filter transforms cached on each weight by the inference path (op/conv.py, keyed
+    by the weight's version counter) must not survive the swap (`p.data.copy_`
+    kept the version, so an inference forward after an eval step ran on the EMA weights'
+    transforms).  The eval loss must be the EMA-weight model's, and an inference forward of
+    the live weights after the eval step must equal the one before it, bit for bit."""
     import losses
     import models  # noqa: F401
     import sde_lib
@@ -237,15 +239,15 @@ def test_eval_step_between_train_steps_leaves_training_unchanged(hip):
     from models import utils as mutils
     from models.ema import ExponentialMovingAverage
 
-    # the benchmark architecture at nf 32, 64^2: every 3x3 conv on the Winograd kernel with
-    # its cached filter transform (images <= 32^2 may time-select the uncached igemm kernel)
+    # the benchmark architecture at nf 32, 64^2: the inference convs run on the Winograd
+    # kernel with the filter transform cached on the parameter
     c = nc_ncsnpp_128.get_config()
     c.model.nf = 32
     c.data.image_size = 64
     c.device = hip
     c.model.dropout = 0.0
     torch.manual_seed(0)
-    model = mutils.create_model(c, wrap=False).train()
+    model = mutils.create_model(c, wrap=False)
     with torch.no_grad():
         for p in model.parameters():
             p.add_(torch.randn_like(p) * 0.01)
@@ -258,15 +260,20 @@ def test_eval_step_between_train_steps_leaves_training_unchanged(hip):
     g = torch.Generator(device=hip).manual_seed(0)
     x = torch.rand(2, 1, 64, 64, device=hip, generator=g)
     t = torch.rand(2, device=hip, generator=g) * 0.9 + 0.05
-    y0 = model(x, t)
-    y0.sum().backward()        # also populate the backward-data filter cache
+
+    def infer():
+        model.eval()
+        with torch.no_grad():
+            return model(x, t)
+
+    y0 = infer()               # caches the live weights' transforms
     with torch.no_grad():      # an optimizer step: in-place update, version bump
         for p in model.parameters():
             p.add_(0.0)
     torch.manual_seed(99)
     loss_e = evals(dict(model=model, ema=ema, step=0), x)
     # the eval loss is the EMA-weight model's loss ...
-    twin = mutils.create_model(c, wrap=False).train()  # fresh tensors: no cached transforms
+    twin = mutils.create_model(c, wrap=False)  # fresh tensors: no cached transforms
     twin.load_state_dict(model.state_dict())
     with torch.no_grad():
         for p, s_ in zip([p for p in twin.parameters() if p.requires_grad], ema.shadow_params):
@@ -274,6 +281,6 @@ def test_eval_step_between_train_steps_leaves_training_unchanged(hip):
     torch.manual_seed(99)
     loss_t = evals(dict(model=twin, ema=ExponentialMovingAverage(twin.parameters(), 0.9), step=0), x)
     assert abs(loss_e.item() - loss_t.item()) <= 1e-6 * abs(loss_t.item()), (loss_e.item(), loss_t.item())
-    # ... and the next training-mode forward runs on the live weights again
-    y1 = model(x, t)
+    # ... and the next inference forward runs on the live weights again
+    y1 = infer()
     assert torch.equal(y1, y0), float((y1 - y0).abs().max())

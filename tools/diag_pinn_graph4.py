@@ -17,9 +17,10 @@ if os.path.exists(old):
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     mods.append(("r02", m))
+B = int(os.environ.get("B", 2))
 for name, mod in mods:
     for poison in (False, True):
-        l1, l2, g1, g2 = T.pinn_graph_vs_eager(dev, mod, steps=10, poison=poison)
+        l1, l2, g1, g2 = T.pinn_graph_vs_eager(dev, mod, steps=12, poison=poison, batch=B)
         rel = np.abs(np.array(l2) - np.array(l1)) / np.abs(np.array(l1))
         print(name, "poison" if poison else "plain", "max rel loss diff", float(np.nanmax(rel)) if np.isfinite(rel).any() else "nan",
               "grad rel", float((g1 - g2).norm() / g1.norm()), flush=True)
