@@ -230,7 +230,7 @@ def _poison(dev, mb=512):
     del t
 
 
-def pinn_graph_vs_eager(hip, losses_mod=None, steps=10, poison=True, batch=2):
+def pinn_graph_vs_eager(hip, losses_mod=None, steps=10, poison=True, B=2):
     """Losses of `steps` PINN steps (configs[3] pinn_pde as shipped: 64^2, 5 levels; B = 2)
     with get_pinn_step_fn(graph=True) -- 2 eager steps, then capture + replays -- and with the
     eager step function, from the same weights; NaN-filled eager re-allocations between the
@@ -243,7 +243,7 @@ def pinn_graph_vs_eager(hip, losses_mod=None, steps=10, poison=True, batch=2):
     from models.ema import ExponentialMovingAverage
     from pinn_kalman.pinn import PINN
     L = losses_mod or losses_default
-    c = full_pinn_config(pinn_pde.get_config, batch)
+    c = full_pinn_config(pinn_pde.get_config, B)
     m = build_pinn_weights(PINN, c).to(hip)
     c.device = hip
     c.inverse.variance = 0.0
@@ -251,7 +251,7 @@ def pinn_graph_vs_eager(hip, losses_mod=None, steps=10, poison=True, batch=2):
     f1, f2, x, y, t, target = (v.to(hip) for v in make_pinn_inputs(c, 3))
     batch = (f1, f2, x.requires_grad_(), y.requires_grad_(), t.requires_grad_(), target)
     g = torch.Generator().manual_seed(5)
-    masks = [(torch.rand(batch, 1, 64, 64, generator=g) > 0.1).float() for _ in range(3)]
+    masks = [(torch.rand(B, 1, 64, 64, generator=g) > 0.1).float() for _ in range(3)]
     runs = []
     for model, graph in ((m, False), (m2, True)):
         em = ExponentialMovingAverage(model.parameters(), decay=c.model.ema_rate)

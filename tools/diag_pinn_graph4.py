@@ -20,7 +20,7 @@ if os.path.exists(old):
 B = int(os.environ.get("B", 2))
 for name, mod in mods:
     for poison in (False, True):
-        l1, l2, g1, g2 = T.pinn_graph_vs_eager(dev, mod, steps=12, poison=poison, batch=B)
+        l1, l2, g1, g2 = T.pinn_graph_vs_eager(dev, mod, steps=12, poison=poison, B=B)
         rel = np.abs(np.array(l2) - np.array(l1)) / np.abs(np.array(l1))
         print(name, "poison" if poison else "plain", "max rel loss diff", float(np.nanmax(rel)) if np.isfinite(rel).any() else "nan",
               "grad rel", float((g1 - g2).norm() / g1.norm()), flush=True)
