@@ -1620,10 +1620,11 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     const bool w8_case = w8_env == 2 || (w8_env == 1 && pre && !skip) || (w8_env == 3 && !skip);
     const int wg = (w8_case && pnb == 1 && CoutP % 128 == 0) ? 8 : 4;
     // the 16-cin chunk form of the 8-wave kernel (BPK_WINO_K16: 0 off, 1 = where the 8-wave
-    // form runs, 2 = every launch it supports)
+    // form runs, 2 = every launch it supports, the default: the weighted NCSN++ PRE-conv mix
+    // 0.705 (8-cin forms) -> 0.716 (K16=1) -> 0.720 (K16=2) of the f32 MFMA peak, one box)
     static const int k16_env = [] {
       const char* e = getenv("BPK_WINO_K16");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 2;
     }();
     const bool k16 = k16_env && pnb == 1 && CoutP % 128 == 0 && Cin % 16 == 0 && C1 % 16 == 0 &&
                      (k16_env == 2 || wg == 8);

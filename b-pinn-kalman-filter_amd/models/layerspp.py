@@ -25,6 +25,9 @@ from . import layers, up_or_down_sampling
 
 # attention at inference: q, k, v as one GEMM over the stacked NIN weights (BPK_ATTN_QKV=0: off)
 _ATTN_QKV = os.environ.get("BPK_ATTN_QKV", "1") != "0"
+# ... and softmax(q^T k) v as one fused kernel (csrc/attention.hip; BPK_ATTN_FUSED=0: bmm +
+# softmax + bmm)
+_ATTN_FUSED = os.environ.get("BPK_ATTN_FUSED", "1") != "0"
 
 conv1x1 = layers.ddpm_conv1x1
 conv3x3 = layers.ddpm_conv3x3
@@ -103,6 +106,10 @@ class AttnBlockpp(nn.Module):
         wqkv = torch.cat([self.NIN_0.W.t() * sq, self.NIN_1.W.t(), self.NIN_2.W.t()], 0)
         bqkv = torch.cat([self.NIN_0.b * sq, self.NIN_1.b, self.NIN_2.b], 0)
         qkv = conv_op.conv1x1(h, wqkv, bqkv).reshape(B, 3, C, H * W)
+        from op import attention as attn_op
+        if _ATTN_FUSED and attn_op.supported(qkv):
+            out = attn_op.attention(qkv, 1.0 if fold else s).reshape(B, C, H, W)
+            return conv_op.conv1x1(out, self.NIN_3.W.t(), self.NIN_3.b)
         q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
         w = torch.bmm(q.transpose(1, 2), k)
         if not fold:

@@ -419,6 +419,15 @@ int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2);
 int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K1, const float* X2, int K2,
                       const float* bias, float* Y, int N, int M, int P, void* stream);
 
+/* Channel self-attention of the score networks' attention blocks at inference, one kernel:
+ *   out[b, c, i] = sum_j V[b, c, j] softmax_j(scale * sum_c' Q[b, c', i] K[b, c', j])
+ * qkv [B, 3, C, P] (Q, K, V = the three channel blocks of the stacked NIN_0/1/2 projection),
+ * out [B, C, P], P = H*W.  Replaces the einsum / bmm + softmax + bmm of AttnBlockpp
+ * (models/layerspp.py:75-91) and AttnBlock (models/layers.py:549-573).
+ * supported(): C % 32 == 0, P in {64, 128, 256}. */
+int bpk_attention_supported(int B, int C, int P);
+int bpk_attention_f32(const float* qkv, float* out, int B, int C, int P, float scale, void* stream);
+
 /* Weight / bias gradient of that 1x1 conv (replaces the conv2d backward-weights MIOpen
  * runs for the reference's nn.Conv2d 1x1 layers -- ddpm_conv1x1 (models/layers.py:96), the
  * BigGAN blocks' Conv_2 skip projection (models/layerspp.py:235) -- under loss.backward(),

@@ -1135,3 +1135,44 @@ def test_instance_norm_elu_residual_block_matches_aten(hip, monkeypatch):
         floor, tol = (1e-3 * gmax, 1e-3) if i >= 2 else (1e-6, 1e-4)
         err = (a - b).abs().max().item() / max(b.abs().max().item(), floor)
         assert err < tol, (i, err)
+
+
+@pytest.mark.parametrize("B,C,P,scale", [(3, 256, 256, 1.0), (2, 64, 256, 0.125), (2, 32, 128, 0.3),
+                                         (5, 96, 64, 1.0 / 96 ** 0.5)])
+def test_fused_attention_matches_fp32_reference(hip, B, C, P, scale):
+    """csrc/attention.hip (q^T k logits, row softmax and the PV product in one kernel) vs the
+    reference's bmm + softmax + bmm in float64 (1e-5 relative to max|ref|)."""
+    from op.attention import attention
+    g = torch.Generator().manual_seed(B * C + P)
+    qkv = torch.randn(B, 3, C, P, generator=g) * 0.5
+    q, k, v = qkv[:, 0].double(), qkv[:, 1].double(), qkv[:, 2].double()
+    w = torch.softmax(torch.bmm(q.transpose(1, 2), k) * scale, dim=-1)
+    ref = torch.bmm(v, w.transpose(1, 2))
+    out = attention(qkv.to(hip), scale).double().cpu()
+    assert out.shape == (B, C, P)
+    assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_attention_block_fused_equals_bmm_path(hip, monkeypatch):
+    """AttnBlockpp at inference with the fused attention kernel vs the same block on the
+    bmm + softmax + bmm path (1e-5 relative)."""
+    import models.layerspp as lpp
+    g = torch.Generator().manual_seed(5)
+    blk = lpp.AttnBlockpp(256, skip_rescale=True, init_scale=0.1).to(hip).eval()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn(p.shape, generator=g).to(hip) * 0.05)
+    x = torch.randn(4, 256, 16, 16, generator=g).to(hip)
+    with torch.no_grad():
+        fused = blk(x)
+        monkeypatch.setattr(lpp, "_ATTN_FUSED", False)
+        ref = blk(x)
+    assert (fused - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_fused_attention_rejects_bad_shapes(hip):
+    from op.attention import attention
+    with pytest.raises(RuntimeError, match="unsupported"):
+        attention(torch.zeros(1, 3, 48, 100, device=hip), 1.0)
+    with pytest.raises(RuntimeError, match="HIP"):
+        attention(torch.zeros(1, 3, 32, 64), 1.0)
