@@ -1176,3 +1176,42 @@ def test_fused_attention_rejects_bad_shapes(hip):
         attention(torch.zeros(1, 3, 48, 100, device=hip), 1.0)
     with pytest.raises(RuntimeError, match="HIP"):
         attention(torch.zeros(1, 3, 32, 64), 1.0)
+
+
+@pytest.mark.parametrize("mode", ["pre_stats", "pre_skip", "plain", "two_sources"])
+def test_conv3x3_winograd_multi_item_workgroups(hip, mode):
+    """A launch large enough for the multi-item 16-cin kernel (wino_f23_k16p_kernel: >= 2
+    items per workgroup with one workgroup per CU; 4 x 128 -> 128 @ 128^2 = 512 items) vs
+    F.conv2d in fp32 (1e-5 relative), incl. the GroupNorm+SiLU prologue with bias and partial
+    statistics, the residual tail, the plain form and two input sources."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3, conv3x3_fwd_raw, gn_partials
+    g = torch.Generator().manual_seed(17)
+    N, cin, cout, hw = 4, 128, 128, 128
+    x = (torch.randn(N, cin, hw, hw, generator=g) * 1.5).to(hip)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(hip)
+    b = torch.randn(cout, generator=g).to(hip)
+    st = torch.stack([torch.rand(N, cin, generator=g) + 0.5, torch.randn(N, cin, generator=g) * 0.3], -1).to(hip)
+    skip = torch.randn(N, cout, hw, hw, generator=g).to(hip)
+    with torch.no_grad():
+        if mode == "plain":
+            a = x
+            out = conv3x3_fwd_raw(x, w, b)
+        else:
+            a = F.silu(x * st[..., 0, None, None] + st[..., 1, None, None])
+            if mode == "pre_stats":
+                out = conv3x3(x, w, b, pre=st, stats=True)
+            elif mode == "pre_skip":
+                out = conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=st, stats=True)
+            else:
+                out = conv3x3_fwd_raw(x[:, :48].contiguous(), w, b, pre=st, stats=True,
+                                      x2=x[:, 48:].contiguous())
+        ref = F.conv2d(a, w, b, padding=1)
+        if mode == "pre_skip":
+            ref = (skip + ref) / 2 ** 0.5
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() <= 1e-5 * scale
+    if mode != "plain":
+        part, R, cnt = gn_partials(out)
+        m = out.reshape(N, cout, hw // 8, 8, hw // 16, 16).mean((3, 5)).reshape(N, cout, R)
+        assert (part[..., 0] - m).abs().max().item() <= 1e-5 * scale

@@ -54,6 +54,14 @@ def run(lib, B, cin, cout, hw, dev):
     nblk = B * (hw // 16) * (hw // 8) * ((cout + 63) // 64)
     if os.environ.get("BPK_WINO_W8", "1") != "0" and cout % 128 == 0:
         nblk //= 2  # 8-wave form: 128 couts per workgroup
+        # multi-item 16-cin form (conv_winograd.hip, BPK_WINO_K16_IPW): items per workgroup
+        ipw_env = int(os.environ.get("BPK_WINO_K16_IPW", "0"))
+        ipi = (hw // 16) * (hw // 8) * (cout // 128)
+        if ipw_env != 1 and cin % 32 == 0 and cin >= 64:
+            for c in range(ipi if ipw_env <= 1 else min(ipw_env, ipi), 1, -1):
+                if ipi % c == 0 and nblk // c >= (1 if ipw_env > 1 else 256):
+                    nblk //= c
+                    break
     ts6 = np.zeros((nblk, 8), dtype=np.int64)
     cu = np.zeros(nblk, dtype=np.uint32)
     n = lib.bpk_wino_timing_read(ts6.ctypes.data_as(P), cu.ctypes.data_as(P), nblk)
