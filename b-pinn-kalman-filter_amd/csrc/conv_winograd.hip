@@ -1249,36 +1249,42 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
 
   constexpr int kPos = kPR * kPC;  // 180 patch positions; threads >= 180 of a half duplicate 0
-  int pdst, ppy, ppx;
-  {
-    const int t8 = tid & 255;
+  // a lane's patch position (py, px) and LDS slot, recomputed from an opaque copy of the
+  // thread id where used: kept live through the chunk loop they were spilled, and a spill
+  // reload there waits (vmcnt is in order) for every patch / filter load in flight
+  struct PPos {
+    int py, px, dst;
+  };
+  auto ppos = [&]() {
+    int t8 = tid & 255;
+    asm volatile("" : "+v"(t8));
     const int t = t8 < kPos ? t8 : 0;
-    ppy = t / kPC;
-    ppx = t - ppy * kPC;
-    pdst = ppy * kPCp + ppx + ph * 8 * (kPR * kPCp);
-  }
+    const int py = t / kPC, px = t - (t / kPC) * kPC;
+    return PPos{py, px, py * kPCp + px + ph * 8 * (kPR * kPCp)};
+  };
   float pv[8];
   // a chunk of the stream: the item's geometry and the chunk index within the item
   struct Chunk {
     Geo q;
     int k;
   };
-  auto load_patch_part = [&](float* dst, Chunk ch, int c0, int cn) {
+  auto load_patch_part = [&](float* dst, Chunk ch, int c0, int cn, const PPos& pp) {
     const int cc = ch.k * CK;
     const bool second = cc >= g.C1;
     const int soff = ((second ? cc - g.C1 : cc) + ph * 8) * (int)plane * 4;
     // clamped to the plane (padding positions load an edge value, zeroed at the store): every
     // address stays inside the tensor
-    const int iy = min(max(ch.q.oy0 - 1 + ppy, 0), g.H - 1);
-    const int ix = min(max(ch.q.ox0 - 1 + ppx, 0), g.W - 1);
+    const int iy = min(max(ch.q.oy0 - 1 + pp.py, 0), g.H - 1);
+    const int ix = min(max(ch.q.ox0 - 1 + pp.px, 0), g.W - 1);
     const int voff = (iy * g.W + ix) * 4;
 #pragma unroll
     for (int c = c0; c < c0 + cn; ++c)
       dst[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
           second ? xrs2 : xrs, voff, soff + c * (int)plane * 4, 0));
   };
-  auto store_patch_part = [&](const float* src, float* sp, Chunk ch, int c0, int cn) {
-    const int iy = ch.q.oy0 - 1 + ppy, ix = ch.q.ox0 - 1 + ppx;
+  auto store_patch_part = [&](const float* src, float* sp, Chunk ch, int c0, int cn,
+                              const PPos& pp) {
+    const int iy = ch.q.oy0 - 1 + pp.py, ix = ch.q.ox0 - 1 + pp.px;
     const bool pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
     const int cb0 = ch.k * CK + ph * 8;
 #pragma unroll
@@ -1288,7 +1294,7 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
         const float2 st = s_ss[cb0 + c];
         v = silu_f(v * st.x + st.y);
       }
-      sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
+      sp[pp.dst + c * (kPR * kPCp)] = pin ? v : 0.f;
     }
   };
   // B operands: uo[ks & 1][q] = U[c0 + 4 ks + kq][cb * 128 + 16 wave + jj][4q..4q + 3]
@@ -1348,9 +1354,10 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
   // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight
   {
     float pv0[8], pv1[8];
-    load_patch_part(pv0, Chunk{cur, 0}, 0, 8);
-    load_patch_part(pv1, Chunk{cur, 1}, 0, 8);
-    load_patch_part(pv, Chunk{cur, 2}, 0, 8);
+    const PPos pp = ppos();
+    load_patch_part(pv0, Chunk{cur, 0}, 0, 8, pp);
+    load_patch_part(pv1, Chunk{cur, 1}, 0, 8, pp);
+    load_patch_part(pv, Chunk{cur, 2}, 0, 8, pp);
     load_u(0, Chunk{cur, 0}, 0);
     load_u(1, Chunk{cur, 0}, 1);
     if (PRE) {
@@ -1358,8 +1365,8 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       __syncthreads();
     }
     WINO_TS(1);
-    store_patch_part(pv0, s_patch_raw[0], Chunk{cur, 0}, 0, 8);
-    store_patch_part(pv1, s_patch_raw[1], Chunk{cur, 1}, 0, 8);
+    store_patch_part(pv0, s_patch_raw[0], Chunk{cur, 0}, 0, 8, pp);
+    store_patch_part(pv1, s_patch_raw[1], Chunk{cur, 1}, 0, 8, pp);
   }
   __syncthreads();
   WINO_TS(2);
@@ -1367,16 +1374,14 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
   write_v(s_v[0]);
   __syncthreads();
 
-  f4 a[4];
+  // A operands one q ahead (2 buffers): a[q & 1] holds V[pos 4q..4q+3] of this lane's
+  // (cin, tile) row while the next q's is in flight
+  f4 a[2];
   auto a_src = [&](const float* sv, int grp) {  // grp = 2 ks + mb
     const int ks = grp >> 1, mb = grp & 1;
     return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
   };
-  {
-    const f4* src = a_src(s_v[0], 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a[q] = src[q];
-  }
+  a[0] = a_src(s_v[0], 0)[0];
   // chunk k of the current item on V buffer SB
   auto step = [&](int k, auto sb_c, auto first_c, auto tm_c) __attribute__((always_inline)) {
     constexpr int SB = decltype(sb_c)::value;
@@ -1395,20 +1400,28 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       __builtin_amdgcn_sched_barrier(0);
       if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                    // patch(k+1)
       if (grp == 1) write_v(s_v[SB ^ 1]);                           // V(k+1)
-      if (grp == 2) store_patch_part(pv, s_patch_raw[SB], c2, 0, 4);  // patch(k+2)
-      if (grp == 3) store_patch_part(pv, s_patch_raw[SB], c2, 4, 4);
-      if (grp == 4) load_patch_part(pv, c3, 0, 4);
-      if (grp == 5) load_patch_part(pv, c3, 4, 4);
+      if (grp == 2) {  // patch(k+2)
+        const PPos pp = ppos();
+        store_patch_part(pv, s_patch_raw[SB], c2, 0, 4, pp);
+        store_patch_part(pv, s_patch_raw[SB], c2, 4, 4, pp);
+      }
+      if (grp == 4) {  // patch(k+3)
+        const PPos pp = ppos();
+        load_patch_part(pv, c3, 0, 8, pp);
+      }
       __builtin_amdgcn_sched_barrier(0);
       const int soff_next = mb == 1 ? (ks < 2 ? u_soff(c0, ks + 2) : u_soff(c1, ks - 2)) : 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        // prefetch the next q's A (the next group's q = 0 after the last q; the next chunk's
+        // comes after the barrier)
+        if (q < 3) a[(q + 1) & 1] = a_src(sv, grp)[q + 1];
+        else if (grp < 7) a[0] = a_src(sv, grp + 1)[0];
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp)
           acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[q][pp], uo[ks & 1][q][pp],
+              a[q & 1][pp], uo[ks & 1][q][pp],
               (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb], 0, 0, 0);
-        if (grp < 7) a[q] = a_src(sv, grp + 1)[q];
         if (mb == 1) {  // k-step ks + 2 of this chunk, or ks - 2 of the next
           using u4 = __attribute__((ext_vector_type(4))) unsigned;
           const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff_next, 0);
@@ -1417,11 +1430,8 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       }
     }
     __syncthreads();
-    if constexpr (decltype(tm_c)::value < 3) {  // (the item's last chunk: after the epilogue)
-      const f4* src = a_src(s_v[SB ^ 1], 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = src[q];
-    }
+    if constexpr (decltype(tm_c)::value < 3)  // (the item's last chunk: after the epilogue)
+      a[0] = a_src(s_v[SB ^ 1], 0)[0];
   };
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
@@ -1439,14 +1449,34 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
     step(nch - 2, C0{}, F{}, std::integral_constant<int, 2>{});
     step(nch - 1, C1{}, F{}, std::integral_constant<int, 3>{});
 
-    // output transform straight from registers (as wino_f23_pipe_kernel, NB = 1)
+    // output transform: the 32 outputs of a lane first (acc is dead after this block), then
+    // the residual tail, the stores and the GroupNorm partial statistics
     const Geo q = cur;
     cur = nxt;
     nxt = geo((unsigned)min(it + 2, ipw - 1));
     const int cout_w = q.cb * 128 + wave * 16;
+    const int co = cout_w + jj;
+    const float bv = (bias && cout_w < g.CoutS) ? bias[co] : 0.f;
+    f4 ov[2][2][2];  // [mb][h][e]
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int rg = 2 * e + u;
+            float t[4];
+#pragma unroll
+            for (int jx = 0; jx < 4; ++jx)
+              t[jx] = h == 0 ? acc[jx][mb][rg] + acc[4 + jx][mb][rg] + acc[8 + jx][mb][rg]
+                             : acc[4 + jx][mb][rg] - acc[8 + jx][mb][rg] - acc[12 + jx][mb][rg];
+            ov[mb][h][e][2 * u] = t[0] + t[1] + t[2] + bv;
+            ov[mb][h][e][2 * u + 1] = t[1] - t[2] - t[3] + bv;
+          }
+    __builtin_amdgcn_sched_barrier(0);
     if (cout_w < g.CoutS) {
-      const int co = cout_w + jj;
-      const float bv = bias ? bias[co] : 0.f;
       const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
       float lm = 0.f, lm2 = 0.f;
 #pragma unroll
@@ -1457,18 +1487,7 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
         for (int h = 0; h < 2; ++h) {
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            f4 v;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int rg = 2 * e + u;
-              float t[4];
-#pragma unroll
-              for (int jx = 0; jx < 4; ++jx)
-                t[jx] = h == 0 ? acc[jx][mb][rg] + acc[4 + jx][mb][rg] + acc[8 + jx][mb][rg]
-                               : acc[4 + jx][mb][rg] - acc[8 + jx][mb][rg] - acc[12 + jx][mb][rg];
-              v[2 * u] = t[0] + t[1] + t[2] + bv;
-              v[2 * u + 1] = t[1] - t[2] - t[3] + bv;
-            }
+            f4 v = ov[mb][h][e];
             const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
             if (skip) {
               const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
@@ -1500,11 +1519,8 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
         }
       }
     }
-    {  // the next item's first A operands (V(0) is in s_v[0] since the last chunk's barrier)
-      const f4* src = a_src(s_v[0], 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = src[q];
-    }
+    // the next item's first A operands (V(0) is in s_v[0] since the last chunk's barrier)
+    a[0] = a_src(s_v[0], 0)[0];
   }
   WINO_TS(5);
 }
