@@ -1374,14 +1374,19 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
   write_v(s_v[0]);
   __syncthreads();
 
-  // A operands one q ahead (2 buffers): a[q & 1] holds V[pos 4q..4q+3] of this lane's
-  // (cin, tile) row while the next q's is in flight
-  f4 a[2];
+  // A operands, a ring of kAR (q-distance of the prefetch = kAR - 1): a[q % kAR] holds
+  // V[pos 4q..4q+3] of this lane's (cin, tile) row
+#ifndef WINO_K16P_AR
+#define WINO_K16P_AR 3
+#endif
+  constexpr int kAR = WINO_K16P_AR;
+  f4 a[kAR];
   auto a_src = [&](const float* sv, int grp) {  // grp = 2 ks + mb
     const int ks = grp >> 1, mb = grp & 1;
     return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
   };
-  a[0] = a_src(s_v[0], 0)[0];
+#pragma unroll
+  for (int q = 0; q < kAR - 1; ++q) a[q] = a_src(s_v[0], 0)[q];
   // chunk k of the current item on V buffer SB
   auto step = [&](int k, auto sb_c, auto first_c, auto tm_c) __attribute__((always_inline)) {
     constexpr int SB = decltype(sb_c)::value;
@@ -1413,14 +1418,17 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       const int soff_next = mb == 1 ? (ks < 2 ? u_soff(c0, ks + 2) : u_soff(c1, ks - 2)) : 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        // prefetch the next q's A (the next group's q = 0 after the last q; the next chunk's
-        // comes after the barrier)
-        if (q < 3) a[(q + 1) & 1] = a_src(sv, grp)[q + 1];
-        else if (grp < 7) a[0] = a_src(sv, grp + 1)[0];
+        // prefetch the A of kAR - 1 q's ahead (into the next group; the next chunk's first
+        // ones come after the barrier)
+        {
+          const int qa = q + kAR - 1;  // q index counted from this group's q = 0
+          if (qa < 4) a[qa % kAR] = a_src(sv, grp)[qa];
+          else if (grp < 7) a[qa % kAR] = a_src(sv, grp + 1)[qa - 4];
+        }
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp)
           acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[q & 1][pp], uo[ks & 1][q][pp],
+              a[q % kAR][pp], uo[ks & 1][q][pp],
               (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb], 0, 0, 0);
         if (mb == 1) {  // k-step ks + 2 of this chunk, or ks - 2 of the next
           using u4 = __attribute__((ext_vector_type(4))) unsigned;
@@ -1430,8 +1438,10 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       }
     }
     __syncthreads();
-    if constexpr (decltype(tm_c)::value < 3)  // (the item's last chunk: after the epilogue)
-      a[0] = a_src(s_v[SB ^ 1], 0)[0];
+    if constexpr (decltype(tm_c)::value < 3) {  // (the item's last chunk: after the epilogue)
+#pragma unroll
+      for (int q = 0; q < kAR - 1; ++q) a[q] = a_src(s_v[SB ^ 1], 0)[q];
+    }
   };
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
@@ -1520,7 +1530,8 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
       }
     }
     // the next item's first A operands (V(0) is in s_v[0] since the last chunk's barrier)
-    a[0] = a_src(s_v[0], 0)[0];
+#pragma unroll
+    for (int q = 0; q < kAR - 1; ++q) a[q] = a_src(s_v[0], 0)[q];
   }
   WINO_TS(5);
 }
