@@ -1212,24 +1212,25 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
   const unsigned nblk = gridDim.x;
   unsigned b = blockIdx.x;
   if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
-  // item = ((n * regions_y + ry) * regions_x + rx) * cout_blocks + cb; this workgroup's items
-  // [b * ipw, (b + 1) * ipw) lie in one image (host check)
-  const unsigned item0 = b * (unsigned)ipw;
-  const unsigned ipi = (unsigned)(g.regions_x * g.regions_y * g.cout_blocks);
-  unsigned r0;
-  const int n = (int)udivmod(item0, ipi, r0);
+  // workgroup b owns cout block cb = b % cout_blocks of the ipw consecutive regions starting
+  // at region (b / cout_blocks) * ipw (one image; host check): the workgroups of the other
+  // cout blocks of those regions are its logical neighbours -- the same XCD, in step -- so a
+  // region's input patch is fetched from HBM once and read again from L2
   const int ph = __builtin_amdgcn_readfirstlane(tid >> 8);  // channels 8 ph .. 8 ph + 7
   struct Geo {
     int oy0, ox0, cb;
   };
-  // regions_x and cout_blocks are powers of two (host check): the item decode is shifts
+  // regions_x and cout_blocks are powers of two (host check): the decode is shifts
   const unsigned sh_cb = __builtin_ctz((unsigned)g.cout_blocks);
   const unsigned sh_rx = __builtin_ctz((unsigned)g.regions_x);
+  const unsigned rpi = (unsigned)(g.regions_x * g.regions_y);
+  const int cbw = (int)(b & ((unsigned)g.cout_blocks - 1u));
+  unsigned r0;
+  const int n = (int)udivmod((b >> sh_cb) * (unsigned)ipw, rpi, r0);
   auto geo = [&](unsigned it) {  // item it (< ipw) of this workgroup
     const unsigned r = r0 + it;
-    const unsigned rr = r >> sh_cb;
-    return Geo{(int)(rr >> sh_rx) * kOutRows, (int)(rr & ((unsigned)g.regions_x - 1u)) * kOutCols,
-               (int)(r & ((unsigned)g.cout_blocks - 1u))};
+    return Geo{(int)(r >> sh_rx) * kOutRows, (int)(r & ((unsigned)g.regions_x - 1u)) * kOutCols,
+               cbw};
   };
 
   f4 acc[16][2];
@@ -2002,15 +2003,15 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (cus <= 0) cus = 256;
       }
-      const int ipi = gk.regions_x * gk.regions_y * gk.cout_blocks;
+      const int rpi = gk.regions_x * gk.regions_y;  // items per workgroup divide an image's regions
       const int nch16 = Cin / 16;
       int ipw = 1;
       const bool pow2 = (gk.regions_x & (gk.regions_x - 1)) == 0 &&
                         (gk.cout_blocks & (gk.cout_blocks - 1)) == 0;
       if (ipw_env != 1 && pow2 && nch16 % 2 == 0 && nch16 >= 4) {
-        const int cap = ipw_env > 1 ? std::min(ipw_env, ipi) : ipi;
+        const int cap = ipw_env > 1 ? std::min(ipw_env, rpi) : rpi;
         for (int c = cap; c > 1; --c)
-          if (ipi % c == 0 && items / c >= (ipw_env > 1 ? 1 : cus)) {
+          if (rpi % c == 0 && items / c >= (ipw_env > 1 ? 1 : cus)) {
             ipw = c;
             break;
           }

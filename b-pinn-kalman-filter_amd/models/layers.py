@@ -397,7 +397,7 @@ class ResnetBlockDDPM(nn.Module):
             bias_nc = bias_nc + temb_proj(self.Dense_0, self.act, temb)
         bias = self.Conv_1.bias
         if self.in_ch == self.out_ch:
-            skip = x
+            skip = x if x2 is None else cat_channels(x, x2)  # identity of [x, x2]
         elif not self.conv_shortcut and _GEMM1X1 and conv_op.gemm1x1_supported(
                 x, self.NIN_0.W.t(), x2):
             skip = conv_op.conv1x1(x, self.NIN_0.W.t(), None, x2)

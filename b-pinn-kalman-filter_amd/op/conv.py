@@ -14,6 +14,7 @@ its weights transforms each filter once.
 """
 from __future__ import annotations
 
+import functools
 import os
 
 import torch
@@ -218,11 +219,26 @@ def igemm_supported(x, w, stride=1, padding=0, dilation=1, groups=1):
     wshape = tuple(w) if isinstance(w, (tuple, list, torch.Size)) else tuple(w.shape)
     if isinstance(w, torch.Tensor) and w.dtype != torch.float32:
         return False
-    return (_IGEMM and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+    if not (_IGEMM and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
             and len(wshape) == 4 and int(groups) == 1
             and _pair(dilation) == (1, 1) and wshape[1] == x.shape[1]
             and x.shape[2] + 2 * _pair(padding)[0] >= wshape[2]
-            and x.shape[3] + 2 * _pair(padding)[1] >= wshape[3])
+            and x.shape[3] + 2 * _pair(padding)[1] >= wshape[3]):
+        return False
+    return _igemm_shape_ok(tuple(x.shape), tuple(int(v) for v in wshape), _pair(stride),
+                           _pair(padding))
+
+
+@functools.lru_cache(maxsize=4096)
+def _igemm_shape_ok(xshape, wshape, s, p):
+    """The kernels' own limits (32-bit index ranges, tile counts): the workspace query of the
+    forward, its adjoint and the weight gradient answers -1 for a shape they cannot run, and
+    such a conv stays on MIOpen instead of raising."""
+    N, C, H, W = xshape
+    Co, _, KH, KW = wshape
+    Ho, Wo = (H + 2 * p[0] - KH) // s[0] + 1, (W + 2 * p[1] - KW) // s[1] + 1
+    return all(lib.bpk_conv2d_igemm_workspace_bytes(m, N, C, H, W, Co, KH, KW, s[0], s[1], p[0],
+                                                    p[1], Ho, Wo, 1) >= 0 for m in (0, 1, 2))
 
 
 def _igemm_ws(mode, N, C, H, W, Co, KH, KW, s, p, Ho, Wo, bias_grad, device):
@@ -430,7 +446,7 @@ def _wgrad_impl(x, gy, wshape, want_b):
             dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
             return dw, (db if want_b else None)
         dw = conv3x3_wgrad_raw(x, gy, wshape)
-    elif _IGEMM and x.is_cuda and x.dtype == torch.float32:
+    elif igemm_supported(x, tuple(wshape), 1, 1):
         return conv2d_weight_select(x, tuple(wshape), gy, 1, 1, want_b)
     else:
         with torch.no_grad():
@@ -445,12 +461,14 @@ def _fwd_ft_impl(x, w):
     N, C, H, W = x.shape
     if (C == w.shape[0] and x.is_cuda and x.dtype == torch.float32
             and bool(lib.bpk_conv3x3_wino_supported(N, C, w.shape[1], H, W))):
-        if _small_img(x) and _IGEMM and w.dtype == torch.float32:  # (igemm: any 3x3 / pad 1)
+        if (_small_img(x) and _IGEMM and w.dtype == torch.float32
+                and _igemm_shape_ok((N, w.shape[1], H, W), tuple(w.shape), (1, 1), (1, 1))):
             key = ("d3", tuple(x.shape), tuple(w.shape))
             return _pick_any(key, [lambda: conv3x3_fwd_raw(x.detach(), w, ft=True),
                                    lambda: conv2d_input_igemm_raw((N, w.shape[1], H, W), w, x, 1, 1)])
         return conv3x3_fwd_raw(x.detach(), w, ft=True)
-    if _IGEMM and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32:
+    if (_IGEMM and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32
+            and _igemm_shape_ok((N, w.shape[1], H, W), tuple(w.shape), (1, 1), (1, 1))):
         # conv3x3(x, flip_t(w)) is the adjoint of conv3x3(., w): the dgrad kernel, no flip
         return conv2d_input_select((N, w.shape[1], H, W), w, x, 1, 1)
     return _fwd_impl(x, _flip_t(w))
@@ -837,7 +855,9 @@ class _ConvTG(torch.autograd.Function):
             ctx.save_for_backward(u, w)
             ctx.cfg = cfg
         if (_IGEMM and u.is_cuda and u.dtype == torch.float32 and w.dtype == torch.float32
-                and int(cfg[3]) == 1 and _pair(cfg[2]) == (1, 1)):
+                and int(cfg[3]) == 1 and _pair(cfg[2]) == (1, 1)
+                and _igemm_shape_ok(tuple(int(v) for v in xshape), tuple(w.shape),
+                                    _pair(cfg[0]), _pair(cfg[1]))):
             return conv2d_input_select(xshape, w, u, cfg[0], cfg[1])
         with torch.no_grad():
             return torch.nn.grad.conv2d_input(xshape, w.detach(), u.detach(), **_cfg(cfg))

@@ -10,8 +10,3 @@ for r in 1 2; do for v in 1 0; do
   echo "IPW=$v $(tail -1 gpurun_out/mix_ipw_$v.txt)"
 done; done
 cat gpurun_out/mix_ipw_0.txt
-for v in 1 0; do
-  echo "### timeline IPW=$v"
-  BPK_WINO_K16_IPW=$v WINO_TIMING_LIB=b-pinn-kalman-filter_amd/lib/libbpk_wino_timing_k16p.so timeout -k 10 120 python tools/wino_timing.py 128 128 128 256 256 64 512 256 64 > gpurun_out/tl_ipw_$v.txt 2>&1 || { tail -5 gpurun_out/tl_ipw_$v.txt; exit 1; }
-  grep "==\|  loop\|  prologue \|  epilogue" gpurun_out/tl_ipw_$v.txt
-done
