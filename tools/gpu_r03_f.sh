@@ -10,3 +10,12 @@ for r in 1 2; do for v in 1 0; do
   echo "IPW=$v $(tail -1 gpurun_out/mix_ipw_$v.txt)"
 done; done
 cat gpurun_out/mix_ipw_0.txt
+cat > /tmp/upf_ab.py <<'PY'
+import sys, json, os
+sys.path[:0] = ["b-pinn-kalman-filter_amd", "."]
+import torch, bench
+dev = torch.device("cuda:0")
+r = bench.upfirdn_rooflines(dev, 64)
+print(os.environ.get("BPK_UPFIRDN_R2", "4"), json.dumps([(x["kernel"][:28], x["frac"]) for x in r]))
+PY
+for r2 in 4 8 16 4 8 16; do BPK_UPFIRDN_R2=$r2 timeout -k 10 120 python /tmp/upf_ab.py || exit 1; done
