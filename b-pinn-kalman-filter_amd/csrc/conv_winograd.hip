@@ -1420,16 +1420,17 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         // prefetch the A of kAR - 1 q's ahead (into the next group; the next chunk's first
-        // ones come after the barrier)
+        // ones come after the barrier).  Ring slots follow the q count from the chunk's start
+        // (idx = 4 grp + q), which restarts after every barrier.
+        const int idx = 4 * grp + q;
         {
-          const int qa = q + kAR - 1;  // q index counted from this group's q = 0
-          if (qa < 4) a[qa % kAR] = a_src(sv, grp)[qa];
-          else if (grp < 7) a[qa % kAR] = a_src(sv, grp + 1)[qa - 4];
+          const int ia = idx + kAR - 1;
+          if (ia < 32) a[ia % kAR] = a_src(sv, ia >> 2)[ia & 3];
         }
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp)
           acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[q % kAR][pp], uo[ks & 1][q][pp],
+              a[idx % kAR][pp], uo[ks & 1][q][pp],
               (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb], 0, 0, 0);
         if (mb == 1) {  // k-step ks + 2 of this chunk, or ks - 2 of the next
           using u4 = __attribute__((ext_vector_type(4))) unsigned;
