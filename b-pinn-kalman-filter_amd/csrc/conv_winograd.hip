@@ -1182,362 +1182,6 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   WINO_TS(5);
 }
 
-// Multi-item form of the 16-cin chunk kernel (wino_f23_k16_kernel).  A workgroup runs `ipw`
-// consecutive work items (an item = one 8 x 16 pixel region x 128 output channels; items of
-// one image only, the cout blocks of a region adjacent) as ONE chunk stream: the patch loads /
-// stores, the V transform and the U loads of an item's first chunks run inside the previous
-// item's last three chunks exactly as between the chunks of one item, so the prologue (one
-// memory latency + the first transform: ~4 us, 10-16 % of a 128-channel item) is paid once
-// per workgroup; the output transform of each item runs between its last chunk and the next
-// item's first.  The last three chunks of an item are peeled (TM = 1, 2, 3) so that which
-// side work refers to the next item is known at compile time (the last item's "next" is
-// itself: those loads are redundant and unused).  Needs nch = Cin / 16 even and >= 4, and
-// power-of-two region / cout-block counts.  A lane's patch address and padding mask follow
-// from its patch position and the region's origin at each load / store.
-template <bool PRE>
-__global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
-    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
-    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2, int ipw) {
-  constexpr int CK = 16;
-  constexpr int kPatch = CK * kPR * kPCp;
-  __shared__ __attribute__((aligned(16))) float s_patch_raw[2][kPatch];
-  constexpr int kVBuf = CK * kM * kVS;
-  __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];
-  __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];
-
-  WINO_TS(0);
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
-  const unsigned nblk = gridDim.x;
-  unsigned b = blockIdx.x;
-  if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
-  // workgroup b owns cout block cb = b % cout_blocks of the ipw consecutive regions starting
-  // at region (b / cout_blocks) * ipw (one image; host check): the workgroups of the other
-  // cout blocks of those regions are its logical neighbours -- the same XCD, in step -- so a
-  // region's input patch is fetched from HBM once and read again from L2
-  const int ph = __builtin_amdgcn_readfirstlane(tid >> 8);  // channels 8 ph .. 8 ph + 7
-  struct Geo {
-    int oy0, ox0, cb;
-  };
-  // regions_x and cout_blocks are powers of two (host check): the decode is shifts
-  const unsigned sh_cb = __builtin_ctz((unsigned)g.cout_blocks);
-  const unsigned sh_rx = __builtin_ctz((unsigned)g.regions_x);
-  const unsigned rpi = (unsigned)(g.regions_x * g.regions_y);
-  const int cbw = (int)(b & ((unsigned)g.cout_blocks - 1u));
-  unsigned r0;
-  const int n = (int)udivmod((b >> sh_cb) * (unsigned)ipw, rpi, r0);
-  auto geo = [&](unsigned it) {  // item it (< ipw) of this workgroup
-    const unsigned r = r0 + it;
-    return Geo{(int)(r >> sh_rx) * kOutRows, (int)(r & ((unsigned)g.regions_x - 1u)) * kOutCols,
-               cbw};
-  };
-
-  f4 acc[16][2];
-  const int64_t plane = (int64_t)g.H * g.W;
-  const int C2 = g.Cin - g.C1;
-  const float* xn = x + (int64_t)n * g.C1 * plane;
-  const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
-  const int kq = lane >> 4, jj = lane & 15;
-  const int nch = g.Cin / CK;
-
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xn), 0, (int)(g.C1 * plane * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t xrs2 = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(C2 > 0 ? x2 + (int64_t)n * C2 * plane : xn), 0,
-      (int)((C2 > 0 ? C2 : g.C1) * plane * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
-
-  constexpr int kPos = kPR * kPC;  // 180 patch positions; threads >= 180 of a half duplicate 0
-  // a lane's patch position (py, px) and LDS slot, recomputed from an opaque copy of the
-  // thread id where used: kept live through the chunk loop they were spilled, and a spill
-  // reload there waits (vmcnt is in order) for every patch / filter load in flight
-  struct PPos {
-    int py, px, dst;
-  };
-  auto ppos = [&]() {
-    int t8 = tid & 255;
-    asm volatile("" : "+v"(t8));
-    const int t = t8 < kPos ? t8 : 0;
-    const int py = t / kPC, px = t - (t / kPC) * kPC;
-    return PPos{py, px, py * kPCp + px + ph * 8 * (kPR * kPCp)};
-  };
-  float pv[8];
-  // a chunk of the stream: the item's geometry and the chunk index within the item
-  struct Chunk {
-    Geo q;
-    int k;
-  };
-  auto load_patch_part = [&](float* dst, Chunk ch, int c0, int cn, const PPos& pp) {
-    const int cc = ch.k * CK;
-    const bool second = cc >= g.C1;
-    const int soff = ((second ? cc - g.C1 : cc) + ph * 8) * (int)plane * 4;
-    // clamped to the plane (padding positions load an edge value, zeroed at the store): every
-    // address stays inside the tensor
-    const int iy = min(max(ch.q.oy0 - 1 + pp.py, 0), g.H - 1);
-    const int ix = min(max(ch.q.ox0 - 1 + pp.px, 0), g.W - 1);
-    const int voff = (iy * g.W + ix) * 4;
-#pragma unroll
-    for (int c = c0; c < c0 + cn; ++c)
-      dst[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-          second ? xrs2 : xrs, voff, soff + c * (int)plane * 4, 0));
-  };
-  auto store_patch_part = [&](const float* src, float* sp, Chunk ch, int c0, int cn,
-                              const PPos& pp) {
-    const int iy = ch.q.oy0 - 1 + pp.py, ix = ch.q.ox0 - 1 + pp.px;
-    const bool pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-    const int cb0 = ch.k * CK + ph * 8;
-#pragma unroll
-    for (int c = c0; c < c0 + cn; ++c) {
-      float v = src[c];
-      if (PRE) {
-        const float2 st = s_ss[cb0 + c];
-        v = silu_f(v * st.x + st.y);
-      }
-      sp[pp.dst + c * (kPR * kPCp)] = pin ? v : 0.f;
-    }
-  };
-  // B operands: uo[ks & 1][q] = U[c0 + 4 ks + kq][cb * 128 + 16 wave + jj][4q..4q + 3]
-  f4 uo[2][4];
-  const int uoff = ((kq * g.Cout + wave * 16 + jj) * 16) * 4;
-  auto u_soff = [&](Chunk ch, int ks) { return ((ch.k * CK + 4 * ks) * g.Cout + ch.q.cb * 128) * 64; };
-  auto load_u = [&](int slot, Chunk ch, int ks) {
-    const int soff = u_soff(ch, ks);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      using u4 = __attribute__((ext_vector_type(4))) unsigned;
-      const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff, 0);
-      uo[slot][q] = __builtin_bit_cast(f4, w);
-    }
-  };
-  // V = B^T d B of one (cin, tile) per thread (512 records = 16 cin x 32 tiles)
-  const int tc = tid >> 5, tm = tid & 31;
-  const int tty = tm / kTC, ttx = tm - tty * kTC;
-  float d[4][4];
-  auto read_d = [&](const float* sp) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jx = 0; jx < 4; jx += 2) {
-        const float2 v2 =
-            *reinterpret_cast<const float2*>(&sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + jx]);
-        d[i][jx] = v2.x;
-        d[i][jx + 1] = v2.y;
-      }
-  };
-  auto write_v = [&](float* sv) {
-    float t[4][4];
-#pragma unroll
-    for (int jx = 0; jx < 4; ++jx) {
-      t[0][jx] = d[0][jx] - d[2][jx];
-      t[1][jx] = d[1][jx] + d[2][jx];
-      t[2][jx] = d[2][jx] - d[1][jx];
-      t[3][jx] = d[1][jx] - d[3][jx];
-    }
-    f4* dst = reinterpret_cast<f4*>(&sv[(tc * kM + tm) * kVS]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
-  };
-
-  Geo cur = geo(0u);
-  Geo nxt = geo(ipw > 1 ? 1u : 0u);
-  // the chunk d (1..3) ahead of chunk k; TM = 0: k <= nch - 4 (inside the item), TM = 1..3:
-  // k = nch - 4 + TM (the next item's first chunks come into view)
-  auto ahead = [&](auto tm_c, int k, int d) {
-    constexpr int TM = decltype(tm_c)::value;
-    if (TM == 0 || d < 4 - TM) return Chunk{cur, k + d};
-    return Chunk{nxt, d - (4 - TM)};
-  };
-  using T0 = std::integral_constant<int, 0>;
-
-  // prologue: V(0) in s_v[0], patch(1) in s_patch[1], patch(2) and U(0) in flight
-  {
-    float pv0[8], pv1[8];
-    const PPos pp = ppos();
-    load_patch_part(pv0, Chunk{cur, 0}, 0, 8, pp);
-    load_patch_part(pv1, Chunk{cur, 1}, 0, 8, pp);
-    load_patch_part(pv, Chunk{cur, 2}, 0, 8, pp);
-    load_u(0, Chunk{cur, 0}, 0);
-    load_u(1, Chunk{cur, 0}, 1);
-    if (PRE) {
-      for (int c = tid; c < g.Cin; c += 512) s_ss[c] = pre_n[c];
-      __syncthreads();
-    }
-    WINO_TS(1);
-    store_patch_part(pv0, s_patch_raw[0], Chunk{cur, 0}, 0, 8, pp);
-    store_patch_part(pv1, s_patch_raw[1], Chunk{cur, 1}, 0, 8, pp);
-  }
-  __syncthreads();
-  WINO_TS(2);
-  read_d(s_patch_raw[0]);
-  write_v(s_v[0]);
-  __syncthreads();
-
-  // A operands, a ring of kAR (q-distance of the prefetch = kAR - 1): a[q % kAR] holds
-  // V[pos 4q..4q+3] of this lane's (cin, tile) row
-#ifndef WINO_K16P_AR
-#define WINO_K16P_AR 3
-#endif
-  constexpr int kAR = WINO_K16P_AR;
-  f4 a[kAR];
-  auto a_src = [&](const float* sv, int grp) {  // grp = 2 ks + mb
-    const int ks = grp >> 1, mb = grp & 1;
-    return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
-  };
-#pragma unroll
-  for (int q = 0; q < kAR - 1; ++q) a[q] = a_src(s_v[0], 0)[q];
-  // chunk k of the current item on V buffer SB
-  auto step = [&](int k, auto sb_c, auto first_c, auto tm_c) __attribute__((always_inline)) {
-    constexpr int SB = decltype(sb_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value;
-    const float* sv = s_v[SB];
-    // opaque copies: the chunk's offsets are computed here, not hoisted out of the item loop
-    // (hoisted, the three peeled chunks' offsets stayed live through it and spilled SGPRs)
-    asm volatile("" : "+s"(k));
-    const Chunk c1 = ahead(tm_c, k, 1);
-    const Chunk c2 = ahead(tm_c, k, 2);
-    const Chunk c3 = ahead(tm_c, k, 3);
-    const Chunk c0{cur, k};
-#pragma unroll
-    for (int grp = 0; grp < 8; ++grp) {
-      const int ks = grp >> 1, mb = grp & 1;
-      __builtin_amdgcn_sched_barrier(0);
-      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                    // patch(k+1)
-      if (grp == 1) write_v(s_v[SB ^ 1]);                           // V(k+1)
-      if (grp == 2) {  // patch(k+2)
-        const PPos pp = ppos();
-        store_patch_part(pv, s_patch_raw[SB], c2, 0, 4, pp);
-        store_patch_part(pv, s_patch_raw[SB], c2, 4, 4, pp);
-      }
-      if (grp == 4) {  // patch(k+3)
-        const PPos pp = ppos();
-        load_patch_part(pv, c3, 0, 8, pp);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const int soff_next = mb == 1 ? (ks < 2 ? u_soff(c0, ks + 2) : u_soff(c1, ks - 2)) : 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        // prefetch the A of kAR - 1 q's ahead (into the next group; the next chunk's first
-        // ones come after the barrier).  Ring slots follow the q count from the chunk's start
-        // (idx = 4 grp + q), which restarts after every barrier.
-        const int idx = 4 * grp + q;
-        {
-          const int ia = idx + kAR - 1;
-          if (ia < 32) a[ia % kAR] = a_src(sv, ia >> 2)[ia & 3];
-        }
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp)
-          acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[idx % kAR][pp], uo[ks & 1][q][pp],
-              (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb], 0, 0, 0);
-        if (mb == 1) {  // k-step ks + 2 of this chunk, or ks - 2 of the next
-          using u4 = __attribute__((ext_vector_type(4))) unsigned;
-          const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff_next, 0);
-          uo[ks & 1][q] = __builtin_bit_cast(f4, w);
-        }
-      }
-    }
-    __syncthreads();
-    if constexpr (decltype(tm_c)::value < 3) {  // (the item's last chunk: after the epilogue)
-#pragma unroll
-      for (int q = 0; q < kAR - 1; ++q) a[q] = a_src(s_v[SB ^ 1], 0)[q];
-    }
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  WINO_TS(3);
-  const float rdiv = 1.f / g.div;
-  // nch even: every item starts on V buffer 0
-  using F = std::false_type;
-  for (int it = 0; it < ipw; ++it) {
-    step(0, C0{}, std::true_type{}, T0{});
-    for (int k = 1; k + 1 <= nch - 4; k += 2) {
-      step(k, C1{}, F{}, T0{});
-      step(k + 1, C0{}, F{}, T0{});
-    }
-    step(nch - 3, C1{}, F{}, std::integral_constant<int, 1>{});
-    step(nch - 2, C0{}, F{}, std::integral_constant<int, 2>{});
-    step(nch - 1, C1{}, F{}, std::integral_constant<int, 3>{});
-
-    // output transform: the 32 outputs of a lane first (acc is dead after this block), then
-    // the residual tail, the stores and the GroupNorm partial statistics
-    const Geo q = cur;
-    cur = nxt;
-    nxt = geo((unsigned)min(it + 2, ipw - 1));
-    const int cout_w = q.cb * 128 + wave * 16;
-    const int co = cout_w + jj;
-    const float bv = (bias && cout_w < g.CoutS) ? bias[co] : 0.f;
-    f4 ov[2][2][2];  // [mb][h][e]
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int rg = 2 * e + u;
-            float t[4];
-#pragma unroll
-            for (int jx = 0; jx < 4; ++jx)
-              t[jx] = h == 0 ? acc[jx][mb][rg] + acc[4 + jx][mb][rg] + acc[8 + jx][mb][rg]
-                             : acc[4 + jx][mb][rg] - acc[8 + jx][mb][rg] - acc[12 + jx][mb][rg];
-            ov[mb][h][e][2 * u] = t[0] + t[1] + t[2] + bv;
-            ov[mb][h][e][2 * u + 1] = t[1] - t[2] - t[3] + bv;
-          }
-    __builtin_amdgcn_sched_barrier(0);
-    if (cout_w < g.CoutS) {
-      const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
-      float lm = 0.f, lm2 = 0.f;
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb) {
-        const int oy = q.oy0 + 2 * (2 * mb + (kq >> 1));
-        const int ox = q.ox0 + 8 * (kq & 1);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            f4 v = ov[mb][h][e];
-            const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
-            if (skip) {
-              const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
-#pragma unroll
-              for (int c = 0; c < 4; ++c) v[c] = div_rn(sk[c] + v[c], g.div, rdiv);
-            }
-            *reinterpret_cast<f4*>(&y[o]) = v;
-            if (stats) {
-              const float sm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
-              float sm2 = 0.f;
-#pragma unroll
-              for (int c = 0; c < 4; ++c) sm2 = fmaf(v[c] - sm, v[c] - sm, sm2);
-              constexpr float kW[8] = {1.f, 1.f / 2, 1.f / 3, 1.f / 4, 1.f / 5, 1.f / 6, 1.f / 7, 1.f / 8};
-              const int st = 4 * mb + 2 * h + e;
-              const float dd = sm - lm;
-              lm = lm + dd * kW[st];
-              lm2 = (lm2 + sm2) + dd * dd * (4.f * st * kW[st]);
-            }
-          }
-        }
-      }
-      if (stats) {
-        merge_stats(lm, lm2, __shfl_xor(lm, 16, 64), __shfl_xor(lm2, 16, 64), 32.f);
-        merge_stats(lm, lm2, __shfl_xor(lm, 32, 64), __shfl_xor(lm2, 32, 64), 64.f);
-        if (kq == 0) {
-          const int R = g.regions_x * g.regions_y;
-          const int region = (q.oy0 / kOutRows) * g.regions_x + q.ox0 / kOutCols;
-          stats[((int64_t)n * g.CoutS + co) * R + region] = make_float2(lm, lm2);
-        }
-      }
-    }
-    // the next item's first A operands (V(0) is in s_v[0] since the last chunk's barrier)
-#pragma unroll
-    for (int q = 0; q < kAR - 1; ++q) a[q] = a_src(s_v[0], 0)[q];
-  }
-  WINO_TS(5);
-}
-
 // Persistent form of the pipelined kernel (NB = 1: 4 waves x 16 couts = 64 couts, 32
 // tiles, two workgroups per CU).  The grid holds at most as many workgroups as fit on the
 // chip at once; workgroup l processes `ipw` consecutive work items of ONE image (an item =
@@ -1990,45 +1634,6 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
       BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino: grid too large");
       const float2* kpre = reinterpret_cast<const float2*>(pre);
       hipStream_t kst = bpk::as_stream(stream);
-      // multi-item form (BPK_WINO_K16_IPW: 0 (default) = the largest items-per-workgroup that
-      // keeps >= one workgroup per CU and each workgroup's run in one image; 1 = one item per
-      // workgroup; n > 1: at most n)
-      static const int ipw_env = [] {
-        const char* e = getenv("BPK_WINO_K16_IPW");
-        return e ? atoi(e) : 0;
-      }();
-      static int cus = 0;
-      if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-      }
-      const int rpi = gk.regions_x * gk.regions_y;  // items per workgroup divide an image's regions
-      const int nch16 = Cin / 16;
-      int ipw = 1;
-      const bool pow2 = (gk.regions_x & (gk.regions_x - 1)) == 0 &&
-                        (gk.cout_blocks & (gk.cout_blocks - 1)) == 0;
-      if (ipw_env != 1 && pow2 && nch16 % 2 == 0 && nch16 >= 4) {
-        const int cap = ipw_env > 1 ? std::min(ipw_env, rpi) : rpi;
-        for (int c = cap; c > 1; --c)
-          if (rpi % c == 0 && items / c >= (ipw_env > 1 ? 1 : cus)) {
-            ipw = c;
-            break;
-          }
-      }
-      if (ipw > 1) {
-        const int64_t kblocks = items / ipw;
-        const int kremap = (kblocks % 8 == 0) ? 1 : 0;
-        if (pre)
-          hipLaunchKernelGGL((wino_f23_k16p_kernel<true>), dim3((unsigned)kblocks), dim3(512), 0, kst,
-                             x, U, bias, skip, kpre, y, stats2, gk, kremap, x2, ipw);
-        else
-          hipLaunchKernelGGL((wino_f23_k16p_kernel<false>), dim3((unsigned)kblocks), dim3(512), 0, kst,
-                             x, U, bias, skip, kpre, y, stats2, gk, kremap, x2, ipw);
-        BPK_LAUNCH_CHECK("conv3x3_wino_k16p");
-        return BPK_OK;
-      }
       const int64_t kblocks = items;
       const int kremap = (kblocks % 8 == 0) ? 1 : 0;
       if (pre)

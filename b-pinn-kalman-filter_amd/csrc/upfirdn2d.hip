@@ -436,10 +436,6 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
         if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 8, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
         if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 8, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
       }
-      if (r2 == 16) {
-        if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 16, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
-        if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 16, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
-      }
       if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
       if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
     }

@@ -1179,11 +1179,11 @@ def test_fused_attention_rejects_bad_shapes(hip):
 
 
 @pytest.mark.parametrize("mode", ["pre_stats", "pre_skip", "plain", "two_sources"])
-def test_conv3x3_winograd_multi_item_workgroups(hip, mode):
-    """A launch large enough for the multi-item 16-cin kernel (wino_f23_k16p_kernel: >= 2
-    items per workgroup with one workgroup per CU; 4 x 128 -> 128 @ 128^2 = 512 items) vs
-    F.conv2d in fp32 (1e-5 relative), incl. the GroupNorm+SiLU prologue with bias and partial
-    statistics, the residual tail, the plain form and two input sources."""
+def test_conv3x3_winograd_large_launch(hip, mode):
+    """A launch with more workgroups than CUs on the 16-cin 8-wave kernel
+    (wino_f23_k16_kernel; 4 x 128 -> 128 @ 128^2 = 512 workgroups) vs F.conv2d in fp32 (1e-5
+    relative), incl. the GroupNorm+SiLU prologue with bias and partial statistics, the
+    residual tail, the plain form and two input sources."""
     import torch.nn.functional as F
     from op.conv import conv3x3, conv3x3_fwd_raw, gn_partials
     g = torch.Generator().manual_seed(17)
