@@ -1,4 +1,4 @@
-"""The bench's PINN step (bench._pinn_run setup: pinn_pde B=64, bench.pinn_batch, the 1600
+"""(DIAG5 toggles) The bench's PINN step (bench._pinn_run setup: pinn_pde B=64, bench.pinn_batch, the 1600
 random inpainting masks, observation noise) eager vs get_pinn_step_fn(graph=True), losses of
 every step, with toggles (env DIAG): var0 = observation variance 0, mask1 = one fixed mask,
 block = blocking mask copy."""
@@ -16,7 +16,7 @@ from inverse.operators import InpaintOperator, get_operator  # noqa: E402
 from models.ema import ExponentialMovingAverage  # noqa: E402
 from pinn_kalman.pinn import PINN  # noqa: E402
 
-T = set(os.environ.get("DIAG", "").split(","))
+T = set(os.environ.get("DIAG5", "").split(","))
 dev = torch.device("cuda:0")
 
 
