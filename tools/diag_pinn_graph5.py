@@ -20,7 +20,7 @@ T = set(os.environ.get("DIAG5", "").split(","))
 dev = torch.device("cuda:0")
 
 
-def run(graph, steps=12):
+def run(graph, steps=int(os.environ.get("DIAG_STEPS", 12))):
     c = pinn_pde.get_config()
     c.device = dev
     if "var0" in T:
