@@ -31,8 +31,16 @@ def run(graph, steps=int(os.environ.get("DIAG_STEPS", 12))):
     opt_f = losses.get_optimizer(c, model.flownet.parameters())
     opt_p = losses.get_optimizer(c, model.pressurenet.parameters(), 0.005)
     state = dict(optimizer=(opt_f, opt_p), model=model, ema=ema, step=c.training.n_iters)
-    step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
-                                      graph=graph)
+    opt_fn = losses.optimization_manager(c)
+    if "noopt" in T:  # parameters fixed: every step the same forward / backward
+        opt_fn = lambda *a, **k: None  # noqa: E731
+    if "sync" in T:
+        real = opt_fn
+
+        def opt_fn(*a, _r=real, **k):
+            torch.cuda.synchronize()
+            return _r(*a, **k)
+    step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=opt_fn, graph=graph)
     if "mask1" in T:
         g = torch.Generator().manual_seed(3)
         operator = InpaintOperator(mask=[(torch.rand(64, 1, 64, 64, generator=g) > 0.1).float()])
