@@ -330,6 +330,13 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
     step starts with zero_grad).  Under batch sharding the averaged gradient carries any
     rank's NaN, so every rank takes the same decision."""
 
+    if graph:
+        # round 2-3: the captured step's replays stopped matching the eager step after
+        # optimizer steps / eager allocations between replays, root cause not isolated
+        # (DESIGN.md section 8); the product path is the eager step
+        raise NotImplementedError("get_pinn_step_fn(graph=True): hipGraph replay of the PINN "
+                                  "step is not supported (DESIGN.md section 8)")
+
     def loss_fn(model, operator, batch):
         f1, f2, x, y, t, target = batch
         f1 = _observe(config, operator, f1)
@@ -344,72 +351,6 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                      * config.training.pinn_loss_weight)
         return pinn_loss + data_loss, pinn_loss, data_loss
 
-    # graph=True: after two eager steps, the forward, the residual's first and second
-    # derivatives and the backward are captured once in a hipGraph and replayed with the
-    # step's batch / mask copied into static buffers -- the ~10k small kernel launches of a
-    # step are issued by the device instead of the host.  Gradient all-reduce, the NaN check,
-    # the optimizers and the EMA stay eager.
-    #
-    # Every tensor the graph writes must be owned by the graph's private pool: the gradients
-    # are set to None before the capture, so the captured AccumulateGrad nodes allocate them
-    # there (round 2 zeroed the eager .grad tensors inside the capture instead; the replays
-    # then accumulated into whatever those blocks held once an eager step had re-allocated
-    # them -- garbage / NaN after a few replays).  The pool gradients are re-attached before
-    # every replay, so a zero_grad(set_to_none=True) between steps cannot detach them.
-    gstate = {"eager": 0}
-
-    def graph_forward_backward(model, operator, batch, opt_flow, opt_pres):
-        if gstate["eager"] < 2:
-            gstate["eager"] += 1
-            opt_flow.zero_grad(set_to_none=False)
-            opt_pres.zero_grad(set_to_none=False)
-            return loss_fn(model, operator, batch)
-        dev = batch[0].device
-        params = [p for p in model.parameters() if p.requires_grad]
-        if "graph" not in gstate:
-            sb = []
-            for t in batch:
-                c = t.detach().clone()
-                sb.append(c.requires_grad_(t.requires_grad))
-            gstate["batch"] = tuple(sb)
-            gstate["mask"] = operator.mask.to(dev).clone()
-            cur = torch.cuda.current_stream(dev)
-            side = torch.cuda.Stream(dev)
-            side.wait_stream(cur)
-            real_mask = operator.mask
-            operator.mask = gstate["mask"]
-            with torch.cuda.stream(side):  # warm-up on the capture stream
-                opt_flow.zero_grad(set_to_none=False)
-                opt_pres.zero_grad(set_to_none=False)
-                l3 = loss_fn(model, operator, gstate["batch"])
-                l3[0].backward()
-            cur.wait_stream(side)
-            # drop the warm-up graph: its AccumulateGrad nodes (created on the side stream)
-            # would otherwise be reused by the capture, on another stream
-            del l3
-            for t in list(params) + list(gstate["batch"]):
-                t.grad = None
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                out = loss_fn(model, operator, gstate["batch"])
-                out[0].backward()
-            operator.mask = real_mask
-            gstate["grads"] = [p.grad for p in params]
-            # detached views of the static outputs: replays rewrite them in place, and no
-            # autograd graph outlives the capture
-            gstate["graph"], gstate["out"] = g, tuple(o.detach() for o in out)
-            del out
-        with torch.no_grad():
-            for s_, t in zip(gstate["batch"], batch):
-                if s_ is not t:
-                    s_.copy_(t)
-            gstate["mask"].copy_(operator.mask, non_blocking=True)
-        for p, gr in zip(params, gstate["grads"]):
-            if p.grad is not gr:
-                p.grad = gr
-        gstate["graph"].replay()
-        return gstate["out"]
-
     bucketer = [None]  # eager + sharded: gradient buckets all-reduced during backward
 
     def step_fn(state, operator, batch):
@@ -418,21 +359,12 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
         if train:
             opt_flow, opt_pres = state["optimizer"]
             model.train()
-            if not graph and ctx is not None and ctx.enabled and bucketer[0] is None:
+            if ctx is not None and ctx.enabled and bucketer[0] is None:
                 bucketer[0] = GradBucketer(model.parameters(), ctx)
-            if graph:
-                loss, pinn_loss, data_loss = graph_forward_backward(model, operator, batch,
-                                                                    opt_flow, opt_pres)
-                if gstate["eager"] <= 2 and "graph" not in gstate:
-                    loss.backward()
-                # no graph kept alive by the caller's reference to the losses (AccumulateGrad
-                # nodes of an eager step must not survive into the capture)
-                loss, pinn_loss, data_loss = loss.detach(), pinn_loss.detach(), data_loss.detach()
-            else:
-                opt_flow.zero_grad()
-                opt_pres.zero_grad()
-                loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
-                loss.backward()
+            opt_flow.zero_grad()
+            opt_pres.zero_grad()
+            loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
+            loss.backward()
             if bucketer[0] is not None:
                 bucketer[0].finish()  # buckets all-reduced while backward ran
             else:

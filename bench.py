@@ -55,8 +55,6 @@ def parse():
                     help="configs[1] train steps (NCSN++ CIFAR-10 32x32x3, batch 128/GPU); 0: skip")
     ap.add_argument("--pinn-steps", type=int, default=10)
     ap.add_argument("--pinn-warmup", type=int, default=2)
-    ap.add_argument("--pinn-graph", action="store_true",
-                    help="time the PINN step as a hipGraph replay (experimental, DESIGN.md 8)")
     ap.add_argument("--no-pinn", action="store_true")
     ap.add_argument("--dps-steps", type=int, default=2, help="accepted RK45 steps timed")
     ap.add_argument("--no-dps", action="store_true")
@@ -124,13 +122,18 @@ WINO_MIX = [  # (cin, cout, hw, PRE+stats convs per forward, PRE+residual+stats 
 
 
 def _pmc(key):
-    """HBM bytes of a roofline kernel from the committed PMC passes (FETCH_SIZE x 2 +
-    WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction; profiles/r02_pmc_traffic.json)."""
-    try:
-        with open(os.path.join(REPO, "profiles", "r02_pmc_traffic.json")) as f:
-            return json.load(f)[key]["traffic_bytes"]
-    except (OSError, KeyError, ValueError):
-        return None
+    """HBM bytes of a roofline kernel from the newest committed PMC passes that measured it
+    (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction;
+    profiles/r0*_pmc_traffic.json, tools/pmc_summary.py)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r0*_pmc_traffic.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                return json.load(f)[key]["traffic_bytes"]
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def step_roofline(tally, steps_per_s, what, unit_of_work="step", survey_direct=None):
@@ -674,7 +677,7 @@ def bench_cifar_train(args, ctx, dev):
                 "B=128/GPU", survey_direct=8.36e12)}
 
 
-def _pinn_run(args, ctx, dev, graph):
+def _pinn_run(args, ctx, dev):
     import losses
     from configs.pinn import pinn_pde
     from inverse.operators import get_operator
@@ -689,15 +692,12 @@ def _pinn_run(args, ctx, dev, graph):
     opt_p = losses.get_optimizer(c, model.pressurenet.parameters(), 0.005)
     state = dict(optimizer=(opt_f, opt_p), model=model, ema=ema, step=c.training.n_iters)
     step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
-                                      ctx=ctx, graph=graph)
+                                      ctx=ctx)
     operator = get_operator(c)
     batch = pinn_batch(c, args.batch, dev, seed=ctx.rank)
-    # graph: two eager steps, then the capture (outside the timed region)
-    for _ in range(max(args.pinn_warmup, 3) if graph else args.pinn_warmup):
+    for _ in range(args.pinn_warmup):
         step_fn(state, operator, batch)
-    tally = None
-    if not graph:
-        tally, _ = counted(lambda: step_fn(state, operator, batch), dev)
+    tally, _ = counted(lambda: step_fn(state, operator, batch), dev)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
@@ -716,10 +716,8 @@ def bench_pinn(args, ctx, dev):
     equation_mse with create_graph first derivatives and second derivatives -- correlation,
     grid_sample grad2 and the InstanceNorm+ELU double backward on HIP --, backward, two
     Adams, EMA) at pinn_pde, batch 64/GPU, 64x64; gradients averaged over ranks with RCCL.
-    Eager.  --pinn-graph times the hipGraph-replay form instead (get_pinn_step_fn(graph=True),
-    experimental: its replays read stale memory after ~4 replays in this configuration, see
-    DESIGN.md section 8; the line then carries its losses so a NaN shows)."""
-    dt, losses_, tally = _pinn_run(args, ctx, dev, graph=args.pinn_graph)
+    Eager (the hipGraph replay of this step was withdrawn)."""
+    dt, losses_, tally = _pinn_run(args, ctx, dev)
     roof = None
     if tally is not None:
         roof = step_roofline(tally, args.pinn_steps / dt, "configs[3] PINN train step (FlowNet + "
@@ -729,7 +727,7 @@ def bench_pinn(args, ctx, dev):
                               "images, ~10k kernels), so frac is low by construction")
     return {"roofline_pinn": roof, "pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
             "pinn_ms_per_step": round(dt / args.pinn_steps * 1e3, 2),
-            "pinn_mode": "hipGraph replay (experimental)" if args.pinn_graph else "eager",
+            "pinn_mode": "eager",
             "pinn_global_batch": args.batch * ctx.world_size,
             "pinn_losses": [round(float(v.item()), 6) for v in losses_],
             "pinn_config": "configs[3]: pinn_pde (FlowNet 2.49M + PressureNet 7.54M), 64x64"}

@@ -223,70 +223,6 @@ def test_pinn_stencil_residual_step_runs(hip):
     assert torch.isfinite(loss) and float(pinn_loss) > 0 and state["step"] == 51
 
 
-def _poison(dev, mb=512):
-    """Re-allocate freed eager memory and fill it with NaN (a graph that still reads or
-    writes eager blocks it does not own turns NaN / garbage right away)."""
-    t = torch.full((mb * 262144,), float("nan"), device=dev)
-    del t
-
-
-def pinn_graph_vs_eager(hip, losses_mod=None, steps=10, poison=True, B=2):
-    """Losses of `steps` PINN steps (configs[3] pinn_pde as shipped: 64^2, 5 levels; B = 2)
-    with get_pinn_step_fn(graph=True) -- 2 eager steps, then capture + replays -- and with the
-    eager step function, from the same weights; NaN-filled eager re-allocations between the
-    graph run's steps.  Returns (eager losses, graph losses, eager grads, graph grads)."""
-    import copy
-    import losses as losses_default
-    from configs.pinn import pinn_pde
-    from conftest import full_pinn_config, make_pinn_inputs
-    from inverse.operators import InpaintOperator
-    from models.ema import ExponentialMovingAverage
-    from pinn_kalman.pinn import PINN
-    L = losses_mod or losses_default
-    c = full_pinn_config(pinn_pde.get_config, B)
-    m = build_pinn_weights(PINN, c).to(hip)
-    c.device = hip
-    c.inverse.variance = 0.0
-    m2 = copy.deepcopy(m)
-    f1, f2, x, y, t, target = (v.to(hip) for v in make_pinn_inputs(c, 3))
-    batch = (f1, f2, x.requires_grad_(), y.requires_grad_(), t.requires_grad_(), target)
-    g = torch.Generator().manual_seed(5)
-    masks = [(torch.rand(B, 1, 64, 64, generator=g) > 0.1).float() for _ in range(3)]
-    runs = []
-    for model, graph in ((m, False), (m2, True)):
-        em = ExponentialMovingAverage(model.parameters(), decay=c.model.ema_rate)
-        state = dict(optimizer=(L.get_optimizer(c, model.flownet.parameters()),
-                                L.get_optimizer(c, model.pressurenet.parameters(), 0.001)),
-                     model=model, ema=em, step=50)
-        step_fn = L.get_pinn_step_fn(c, train=True, optimize_fn=L.optimization_manager(c),
-                                     graph=graph)
-        op = InpaintOperator(mask=masks)
-        out = []
-        for _ in range(steps):
-            out.append(float(step_fn(state, op, batch)[0]))
-            if graph and poison:
-                _poison(hip)
-        runs.append((out, torch.cat([p.grad.reshape(-1) for p in model.parameters()
-                                     if p.grad is not None])))
-    (l1, g1), (l2, g2) = runs
-    return l1, l2, g1, g2
-
-
-def test_pinn_step_graph_replay_matches_eager(hip):
-    """get_pinn_step_fn(graph=True) at configs[3]'s real architecture: 8 replays after the two
-    eager steps, with NaN-filled eager allocations between steps, give the eager step
-    function's losses (2e-5 relative; noise variance 0 so both see the same measurements)
-    and gradients of the same size.  Trajectories are compared loosely: the grid_sample
-    backward accumulates with atomics, and Adam turns last-bit differences of near-zero
-    gradients into +-lr steps, so two EAGER runs differ by ~5e-6 in the loss and ~2 % in
-    the last step's gradient (measured, tools/diag_pinn_graph4.py)."""
-    l1, l2, g1, g2 = pinn_graph_vs_eager(hip)
-    assert all(np.isfinite(l2)), l2
-    np.testing.assert_allclose(l2, l1, rtol=2e-5)
-    assert torch.isfinite(g2).all()
-    assert ((g1 - g2).norm() / g1.norm()).item() <= 0.1
-
-
 def test_ns_dynamics_bit_exact_vs_oracle(hip):
     """UKF NSDynamics.forward (reference ukf_utils.py:95-119) on the fused ns_step == the
     oracle's unpatch -> three C ns_step ops (compat quirk on) -> patch, bit for bit; the

@@ -1,5 +1,6 @@
-"""Summarise the round-2 PMC passes (tools/gpu_pmc_r02.sh -> gpurun_out/pmc2) into
-profiles/r02_pmc_traffic.json (bench.py reads `traffic_bytes`) and profiles/r02_pmc_sq.json.
+"""Summarise a round's PMC passes (tools/gpu_pmc_rNN.sh -> gpurun_out/pmcN) into
+profiles/<tag>_pmc_traffic.json (bench.py reads `traffic_bytes` from the newest one) and
+profiles/<tag>_pmc_sq.json.  Usage: pmc_summary.py SRC_DIR TAG (default gpurun_out/pmc2 r02).
 FETCH_SIZE / WRITE_SIZE are in KB; FETCH_SIZE is doubled (MI355X_MICROARCH.md: on gfx950 it
 reports half of a wide streaming read)."""
 import collections
@@ -12,6 +13,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO]
 SRC = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc2")
+TAG = sys.argv[2] if len(sys.argv) > 2 else "r02"
 
 
 def load(pattern, keep):
@@ -28,7 +30,6 @@ def load(pattern, keep):
 def main():
     import bench
     wino = lambda k: "wino_f23" in k
-    fetch = load("*_mix", wino) if False else None  # placeholder for readability
     mix_f = [d["FETCH_SIZE"] for d in load("p3_mix", wino)]
     mix_w = [d["WRITE_SIZE"] for d in load("p4_mix", wino)]
     n = sum(r[3] + r[4] for r in bench.WINO_MIX)
@@ -53,9 +54,9 @@ def main():
     out["ns_step full step B256 192^2"] = {"traffic_bytes": 1024.0 * (2 * f + w),
                                             "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w,
                                             "note": "both fused launches of one full step"}
-    out["_note"] = ("rocprofv3 --pmc passes (tools/gpu_pmc_r02.sh over tools/prof_r02.py); "
+    out["_note"] = (f"rocprofv3 --pmc passes (tools/gpu_pmc_{TAG}.sh over tools/prof_r02.py); "
                     "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB -> bytes")
-    json.dump(out, open(os.path.join(REPO, "profiles", "r02_pmc_traffic.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(REPO, "profiles", f"{TAG}_pmc_traffic.json"), "w"), indent=1)
     sq = {}
     one = [d for d in load("p1_wino_one", wino)]
     one2 = [d for d in load("p2_wino_one", wino)]
@@ -74,7 +75,7 @@ def main():
     sq["_note"] = ("SQ_* wave counters in quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES (cycles, = 32 per "
                    "v_mfma_f32_16x16x4_f32); GRBM_GUI_ACTIVE summed over the 8 XCDs; MFMA busy "
                    "fraction = MFMA busy cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)")
-    json.dump(sq, open(os.path.join(REPO, "profiles", "r02_pmc_sq.json"), "w"), indent=1)
+    json.dump(sq, open(os.path.join(REPO, "profiles", f"{TAG}_pmc_sq.json"), "w"), indent=1)
     print(json.dumps({k: v.get("traffic_bytes") for k, v in out.items() if isinstance(v, dict)}, indent=1))
     print(json.dumps(last["derived"], indent=1))
 
