@@ -136,15 +136,19 @@ def _pmc(key):
     return None
 
 
-def step_roofline(tally, steps_per_s, what, unit_of_work="step", survey_direct=None):
+def step_roofline(tally, steps_per_s, what, unit_of_work="step", survey_direct=None,
+                  traffic_key=None):
     """Roofline object of a whole step (train / PINN / DPS rows): achieved =
     executed FLOPs of one counted step (op.flops: every native MFMA launch on its executed
     basis -- Winograd 4/9 of direct --, aten matmuls / MIOpen convs via FlopCounterMode on
     the direct basis) x steps/s, against the f32 MFMA peak."""
     ex, di = tally.total_executed, tally.total_direct
     ach = ex * steps_per_s / 1e12
+    # traffic: HBM bytes of every kernel of one counted step / nfe (rocprofv3 FETCH_SIZE x 2 +
+    # WRITE_SIZE between marker dispatches, tools/prof_steps.py + tools/pmc_summary.py)
     out = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-           "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+           "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+           "traffic": _pmc(traffic_key) if traffic_key else None,
            "kernel": what, "flop_basis": "executed (native kernels as issued; aten ops direct)",
            f"executed_flop_per_{unit_of_work}": ex, f"direct_flop_per_{unit_of_work}": di,
            "direct_basis_tflops": round(di * steps_per_s / 1e12, 2),
@@ -674,7 +678,7 @@ def bench_cifar_train(args, ctx, dev):
             "cifar_config": "configs[1]: cifar10_ncsnpp_continuous 32x32x3, batch 128/GPU",
             "roofline_cifar_train": step_roofline(
                 tally, args.cifar_steps / dt, "configs[1] DSM train step, NCSN++ CIFAR-10 32x32x3 "
-                "B=128/GPU", survey_direct=8.36e12)}
+                "B=128/GPU", survey_direct=8.36e12, traffic_key="step cifar")}
 
 
 def _pinn_run(args, ctx, dev):
@@ -722,7 +726,8 @@ def bench_pinn(args, ctx, dev):
     if tally is not None:
         roof = step_roofline(tally, args.pinn_steps / dt, "configs[3] PINN train step (FlowNet + "
                              "PressureNet fwd, equation_mse 1st/2nd derivatives, backward, 2x Adam, "
-                             "EMA), B=64/GPU 64x64; latency-bound: ~10k launches per step")
+                             "EMA), B=64/GPU 64x64; latency-bound: ~10k launches per step",
+                             traffic_key="step pinn")
         roof["bound_note"] = ("mfma is the nominal bound; the step is launch/latency-bound (small "
                               "images, ~10k kernels), so frac is low by construction")
     return {"roofline_pinn": roof, "pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
@@ -790,7 +795,8 @@ def bench_dps(args, ctx, dev):
             "roofline_dps": step_roofline(tally, nfe / dt, "configs[4] DPS function evaluation "
                                           "(ddpm 256x256 forward + input gradient through the net, "
                                           "B=16/GPU)", unit_of_work="nfe",
-                                          survey_direct=2 * 1198.88e9 * B)}
+                                          survey_direct=2 * 1198.88e9 * B,
+                                          traffic_key="step dps")}
 
 
 _PHASE = ["start"]
@@ -966,7 +972,8 @@ def main():
                                                     / tdt / 1e3, 2),
                  "roofline_train": step_roofline(
                      tally, args.train_steps / tdt, "configs[2] DSM train step, NCSN++ 128x128x1 B=64/GPU "
-                     "(fwd + bwd-data + wgrad + clip + Adam + EMA)", survey_direct=63.9e12)}
+                     "(fwd + bwd-data + wgrad + clip + Adam + EMA)", survey_direct=63.9e12,
+                     traffic_key="step train")}
 
     cifar = None
     if args.cifar_steps > 0 and not args.no_train:

@@ -1,18 +1,29 @@
 #!/bin/bash
-# Round-3 PMC passes: one counter group per rocprofv3 run, each under its own limit.
+# Round-3 PMC passes: one counter group per rocprofv3 run, each under its own limit; output
+# directories are named <mode>_<group> (tools/pmc_summary.py gpurun_out/pmc3 r03).
+# $1 = kernels (single-kernel passes) | steps (whole-step traffic; $2 = modes)
 mkdir -p gpurun_out/pmc3; export TMPDIR=/tmp
-i=0
-run() {  # mode counters...
-  i=$((i+1)); local mode=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pmc3/p${i}_$mode -o pmc --output-format csv -- python tools/prof_r02.py $mode > gpurun_out/pmc3/p${i}_$mode.log 2>&1 || { echo "pass $i ($mode $*) failed"; tail -5 gpurun_out/pmc3/p${i}_$mode.log; exit 1; }
-  echo "pass $i $mode ok"
+run() {  # script mode group counters...
+  local script=$1 mode=$2 grp=$3; shift 3
+  timeout -s KILL ${PMC_LIMIT:-240} rocprofv3 --pmc "$@" -d gpurun_out/pmc3/${mode}_$grp -o pmc --output-format csv -- python $script $mode > gpurun_out/pmc3/${mode}_$grp.log 2>&1 || { echo "pass $mode $grp failed"; grep -v "^[WE]2026\|^    @" gpurun_out/pmc3/${mode}_$grp.log | tail -12; exit 1; }
+  echo "pass $mode $grp ok"
 }
-run wino_one SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
-run wino_one SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
-run mix FETCH_SIZE
-run mix WRITE_SIZE
-run ns FETCH_SIZE
-run ns WRITE_SIZE
-run ns SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
-run upfirdn FETCH_SIZE
-run upfirdn WRITE_SIZE
+if [ "${1:-kernels}" = kernels ]; then
+run tools/prof_r02.py wino_one sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
+run tools/prof_r02.py wino_one sq2 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
+run tools/prof_r02.py mix fetch FETCH_SIZE
+run tools/prof_r02.py mix write WRITE_SIZE
+run tools/prof_r02.py upfirdn fetch FETCH_SIZE
+run tools/prof_r02.py upfirdn write WRITE_SIZE
+run tools/prof_r02.py ns fetch FETCH_SIZE
+run tools/prof_r02.py ns write WRITE_SIZE
+run tools/prof_r02.py ns sq SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
+else
+for m in ${2:-train cifar pinn dps}; do
+  run tools/prof_steps.py $m fetch FETCH_SIZE
+  python tools/pmc_summary.py gpurun_out/pmc3 r03 reduce-step $m FETCH_SIZE && rm -rf gpurun_out/pmc3/${m}_fetch
+  run tools/prof_steps.py $m write WRITE_SIZE
+  python tools/pmc_summary.py gpurun_out/pmc3 r03 reduce-step $m WRITE_SIZE && rm -rf gpurun_out/pmc3/${m}_write
+done
+fi
+echo PMC_DONE
