@@ -19,6 +19,7 @@
 //    direct kernel; L1/L2 absorb the tap overlap.
 #include "bpk_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -224,8 +225,11 @@ int launch_tiled_w(const T* x, const T* k, T* out, int major, int in_h, int in_w
 // of conv_downsample_2d, 64 -> 65): the segment's last lane also produces the plane's last
 // column from the values it already holds, so a 65-wide row takes a 32-lane segment
 // instead of a half-idle 64-lane one.
+#ifndef UPFIRDN_WPE
+#define UPFIRDN_WPE 1
+#endif
 template <int UP, int DOWN, int P0, int R, int SEGW, int NOCD = 0, bool TAIL = false>
-__global__ __launch_bounds__(256) void upfirdn2d_stream(const float* __restrict__ x,
+__global__ __launch_bounds__(256, UPFIRDN_WPE) void upfirdn2d_stream(const float* __restrict__ x,
                                                          const float* __restrict__ kern,
                                                          float* __restrict__ out, int in_h,
                                                          int in_w, int kh, int kw, int out_h,
@@ -410,6 +414,369 @@ int launch_stream(const float* x, const float* k, float* out, int major, int in_
   return launch_stream_seg<UP, DOWN, P0, R, 64, NOCD>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st);
 }
 
+// Row-rolling kernel for the UP = 1 modes (down2 and the 1:1 FIR), taps <= 4x4: a lane segment
+// owns a column strip of SEGW*NOC output columns (as upfirdn2d_stream) but walks DOWN the plane
+// over `rows` output rows, one input row at a time, keeping only the output rows in flight
+// (2 accumulators for DOWN = 2, 4 for DOWN = 1) instead of the whole strip -- so strips can be
+// tall (the vertical halo is re-read once per strip: (rows*DOWN + 3) / (rows*DOWN) instead of
+// 10 / 8 rows for the 4-row strips) at ~half the registers.  The next input row's loads are
+// issued before the current row's arithmetic (one row of prefetch).
+//   out row oy reads input rows oy*DOWN - P0 + i, i < 4: input row t feeds tap i = t - oy*DOWN + P0.
+template <int DOWN, int P0, int SEGW, int NOC, bool TAIL, bool ALIGN = false>
+__global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ x,
+                                                       const float* __restrict__ kern,
+                                                       float* __restrict__ out, int in_h,
+                                                       int in_w, int kh, int kw, int out_h,
+                                                       int out_w, int rows, int strips_x,
+                                                       int strips_y, int64_t n_strips) {
+  static_assert(DOWN == 1 || DOWN == 2, "upfirdn2d_roll: down 1 or 2");
+  constexpr int LV = NOC * DOWN;                 // input columns loaded per lane
+  constexpr int NOCT = NOC + (TAIL ? 1 : 0);     // columns computed (tail on the last lane)
+  constexpr int NA = 4 / DOWN;                   // output rows in flight
+  constexpr int SEGS = 64 / SEGW;
+  const int lane = threadIdx.x & 63;
+  const int sl = lane % SEGW;
+  const int64_t strip = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * SEGS + lane / SEGW;
+  const bool active = strip < n_strips;
+  const int64_t sidx = active ? strip : 0;
+  const int sxi = (int)(sidx % strips_x);
+  const int syi = (int)((sidx / strips_x) % strips_y);
+  const int64_t plane = sidx / ((int64_t)strips_x * strips_y);
+  const int ox0 = sxi * SEGW * NOC;
+  const int oyb = syi * rows;
+  const int oye = min(oyb + rows, out_h);
+  const int mycol = ox0 * DOWN + LV * sl;
+
+  float w[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[i][j] = (i < kh && j < kw) ? kern[(kh - 1 - i) * kw + (kw - 1 - j)] : 0.f;
+
+  const float* xp = x + plane * in_h * in_w;
+  // one input row: own LV columns (vector load), the neighbours' by segment shuffles, the
+  // segment edges' by direct loads (zero outside the plane)
+  auto load_row = [&](int iy, float (&own)[LV]) {
+    const bool row_ok = active && iy >= 0 && iy < in_h;
+    const float* row = xp + (int64_t)(row_ok ? iy : 0) * in_w;
+    if constexpr (LV == 4) {
+      if (row_ok && mycol + 3 < in_w) {
+        const float4 v = *reinterpret_cast<const float4*>(row + mycol);
+        own[0] = v.x; own[1] = v.y; own[2] = v.z; own[3] = v.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) own[c] = (row_ok && mycol + c < in_w) ? row[mycol + c] : 0.f;
+      }
+    } else if constexpr (LV == 2) {
+      if (row_ok && mycol + 1 < in_w) {
+        const float2 v = *reinterpret_cast<const float2*>(row + mycol);
+        own[0] = v.x; own[1] = v.y;
+      } else {
+        own[0] = (row_ok && mycol < in_w) ? row[mycol] : 0.f;
+        own[1] = (row_ok && mycol + 1 < in_w) ? row[mycol + 1] : 0.f;
+      }
+    } else {
+      own[0] = (row_ok && mycol < in_w) ? row[mycol] : 0.f;
+    }
+  };
+  auto edges = [&](int iy, const float (&own)[LV], float (&left)[LV], float (&right)[LV]) {
+#pragma unroll
+    for (int c = 0; c < LV; ++c) {
+      left[c] = __shfl_up(own[c], 1, SEGW);
+      right[c] = __shfl_down(own[c], 1, SEGW);
+    }
+    const bool row_ok = active && iy >= 0 && iy < in_h;
+    const float* row = xp + (int64_t)(row_ok ? iy : 0) * in_w;
+    if (sl == 0) {
+#pragma unroll
+      for (int c = 0; c < LV; ++c) {
+        const int col = mycol - LV + c;
+        left[c] = (row_ok && col >= 0 && col < in_w) ? row[col] : 0.f;
+      }
+    }
+    if (sl == SEGW - 1) {
+#pragma unroll
+      for (int c = 0; c < LV; ++c) {
+        const int col = mycol + LV + c;
+        right[c] = (row_ok && col < in_w) ? row[col] : 0.f;
+      }
+    }
+  };
+  // acc[oc] += (horizontal taps of row `i` applied to this input row)
+  auto hsum = [&](int i, const float (&own)[LV], const float (&left)[LV],
+                  const float (&right)[LV], float (&acc)[NOCT]) {
+#pragma unroll
+    for (int oc = 0; oc < NOCT; ++oc)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = oc * DOWN + j - P0;
+        const int lo = bpk::floordiv(q, LV);
+        const int comp = bpk::floormod(q, LV);
+        const float v = lo < 0 ? left[comp] : (lo == 0 ? own[comp] : right[comp]);
+        acc[oc] = fmaf(v, w[i][j], acc[oc]);
+      }
+  };
+  const int oxl = ox0 + NOC * sl;
+  float* op = out + plane * out_h * out_w;
+  auto store = [&](int oy, const float (&acc)[NOCT]) {
+    if constexpr (ALIGN) {
+      static_assert(NOC == 4 && TAIL, "aligned stores: the 4-column tail path");
+      // odd row pitch: re-cut the row into 16-byte aligned quads.  Column s is the first at an
+      // aligned address; lane l stores columns 4 l + s .. 4 l + s + 3 (its own s..3 and the
+      // next lane's 0..s-1), lane 0 the s leading columns, the last lane what is left of the
+      // row (the tail column included).  Shuffles run on every lane (inactive ones too).
+      const bool ok = active && oy >= oyb && oy < oye;
+      const int64_t rb = (plane * out_h + oy) * (int64_t)out_w;
+      const int sh = (int)((4 - (rb & 3)) & 3);
+      float nx[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) nx[c] = __shfl_down(acc[c], 1, SEGW);
+      if (!ok) return;
+      float* orow = op + (int64_t)oy * out_w;
+      const bool last = sl == SEGW - 1;
+      if (last) nx[0] = acc[NOC];  // column 4 SEGW = the tail
+      float q[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int a = c + sh;  // 0..6: own[a] for a < 4, else nx[a - 4]
+        float v = acc[0];
+        v = a == 1 ? acc[1] : v;
+        v = a == 2 ? acc[2] : v;
+        v = a == 3 ? acc[3] : v;
+        v = a == 4 ? nx[0] : v;
+        v = a == 5 ? nx[1] : v;
+        v = a == 6 ? nx[2] : v;
+        q[c] = v;
+      }
+      const int c0 = NOC * sl + sh;  // first column of this lane's quad
+      if (!last || c0 + 3 <= out_w - 1) {
+        *reinterpret_cast<float4*>(orow + c0) = make_float4(q[0], q[1], q[2], q[3]);
+        if (last && c0 + 3 < out_w - 1) orow[out_w - 1] = acc[NOC];  // sh = 0: the tail alone
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c0 + c <= out_w - 1) orow[c0 + c] = q[c];
+      }
+      if (sl == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          if (c < sh) orow[c] = acc[c];
+      }
+      return;
+    }
+    if (!active || oy < oyb || oy >= oye) return;
+    float* orow = op + (int64_t)oy * out_w;
+    if constexpr (NOC == 4 && TAIL) {  // odd row pitch: the widest store the address allows
+      const int64_t e0 = (plane * out_h + oy) * (int64_t)out_w + oxl;
+      if ((e0 & 3) == 0) {
+        *reinterpret_cast<float4*>(orow + oxl) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      } else if ((e0 & 1) == 0) {
+        *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[0], acc[1]);
+        *reinterpret_cast<float2*>(orow + oxl + 2) = make_float2(acc[2], acc[3]);
+      } else {  // odd: one float, an aligned pair, one float
+        orow[oxl] = acc[0];
+        *reinterpret_cast<float2*>(orow + oxl + 1) = make_float2(acc[1], acc[2]);
+        orow[oxl + 3] = acc[3];
+      }
+    } else if constexpr (NOC == 2 && TAIL) {
+      const int64_t e0 = (plane * out_h + oy) * (int64_t)out_w + oxl;
+      if ((e0 & 1) == 0) {
+        *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[0], acc[1]);
+      } else {
+        orow[oxl] = acc[0];
+        orow[oxl + 1] = acc[1];
+      }
+    } else if constexpr (NOC == 4) {
+      if (oxl + 3 < out_w) {
+        *reinterpret_cast<float4*>(orow + oxl) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      } else {
+#pragma unroll
+        for (int oc = 0; oc < 4; ++oc)
+          if (oxl + oc < out_w) orow[oxl + oc] = acc[oc];
+      }
+    } else if constexpr (NOC == 2) {
+      if (oxl + 1 < out_w && (((int64_t)oy * out_w + oxl) & 1) == 0 && (out_h * out_w) % 2 == 0) {
+        *reinterpret_cast<float2*>(orow + oxl) = make_float2(acc[0], acc[1]);
+      } else {
+        if (oxl < out_w) orow[oxl] = acc[0];
+        if (oxl + 1 < out_w) orow[oxl + 1] = acc[1];
+      }
+    } else {
+      if (oxl < out_w) orow[oxl] = acc[0];
+    }
+    if constexpr (TAIL) {
+      if (sl == SEGW - 1) orow[out_w - 1] = acc[NOC];
+    }
+  };
+
+  float acc[NA][NOCT];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int oc = 0; oc < NOCT; ++oc) acc[a][oc] = 0.f;
+  // input rows t0 .. t1 feed output rows oyb .. oye - 1
+  const int t0 = oyb * DOWN - P0;
+  const int t1 = (oye - 1) * DOWN - P0 + 3;
+  float cur[LV], nxt[LV], left[LV], right[LV];
+  load_row(t0, cur);
+  if constexpr (DOWN == 1) {
+    // acc[k] = output row t + P0 - 3 + k (tap 3 - k of input row t); after row t, acc[0] is
+    // complete
+    for (int t = t0; t <= t1; ++t) {
+      if (t < t1) load_row(t + 1, nxt);
+      edges(t, cur, left, right);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hsum(3 - k, cur, left, right, acc[k]);
+      store(t + P0 - 3, acc[0]);
+#pragma unroll
+      for (int oc = 0; oc < NOCT; ++oc) {
+        acc[0][oc] = acc[1][oc];
+        acc[1][oc] = acc[2][oc];
+        acc[2][oc] = acc[3][oc];
+        acc[3][oc] = 0.f;
+      }
+#pragma unroll
+      for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+    }
+  } else {
+    // rows in pairs: row t = oy*2 - P0 + 2 (taps 2 of oy, 0 of oy + 1) and t + 1 (taps 3, 1);
+    // acc[0] = output oy, acc[1] = oy + 1.  Prologue: rows t0, t0 + 1 (taps 0, 1 of oyb).
+    load_row(t0 + 1, nxt);
+    edges(t0, cur, left, right);
+    hsum(0, cur, left, right, acc[0]);
+#pragma unroll
+    for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+    int t = t0 + 1;
+    if (t + 1 <= t1) load_row(t + 1, nxt);
+    edges(t, cur, left, right);
+    hsum(1, cur, left, right, acc[0]);
+#pragma unroll
+    for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+    for (int oy = oyb; oy < oye; ++oy) {
+      t = oy * 2 - P0 + 2;  // cur holds row t
+      load_row(t + 1, nxt);
+      edges(t, cur, left, right);
+      hsum(2, cur, left, right, acc[0]);
+      hsum(0, cur, left, right, acc[1]);
+#pragma unroll
+      for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+      if (oy + 1 < oye) load_row(t + 2, nxt);
+      edges(t + 1, cur, left, right);
+      hsum(3, cur, left, right, acc[0]);
+      hsum(1, cur, left, right, acc[1]);
+      store(oy, acc[0]);
+#pragma unroll
+      for (int oc = 0; oc < NOCT; ++oc) {
+        acc[0][oc] = acc[1][oc];
+        acc[1][oc] = 0.f;
+      }
+#pragma unroll
+      for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+    }
+  }
+}
+
+template <int DOWN, int P0, int SEGW, int NOC, bool TAIL = false, bool ALIGN = false>
+int launch_roll(const float* x, const float* k, float* out, int major, int in_h, int in_w, int kh,
+                int kw, int out_h, int out_w, int rows, hipStream_t st) {
+  const int strips_x = TAIL ? 1 : (int)bpk::ceil_div(out_w, SEGW * NOC);
+  const int strips_y = (int)bpk::ceil_div(out_h, rows);
+  const int64_t n = (int64_t)major * strips_x * strips_y;
+  if (n <= 0) return BPK_OK;
+  const int64_t blocks = bpk::ceil_div(n, 4 * (64 / SEGW));
+  BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
+  hipLaunchKernelGGL((upfirdn2d_roll<DOWN, P0, SEGW, NOC, TAIL, ALIGN>), dim3((unsigned)blocks), dim3(256),
+                     0, st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, rows, strips_x, strips_y, n);
+  BPK_LAUNCH_CHECK("upfirdn2d_roll");
+  return BPK_OK;
+}
+
+// Strip height of the rolling kernel.  BPK_UPFIRDN_ROLL: 0 = off (the 4-row upfirdn2d_stream
+// strips), N > 0 = N rows everywhere; unset = automatic: down2 -> about 32 k waves
+// (tools/gpu_upfirdn_roll.sh on MI355X: [64,128,128,128] best at 8 rows, [64,256,64,64] at 4,
+// i.e. 32 k waves both), the odd-width 1:1 FIR -> the divisor of the height in 5..8 (65 = 13 x 5;
+// 5 and 6 rows: 0.59 of HBM vs 0.45 for the 4-row stream strips).
+int roll_env() {
+  static const int r = [] {
+    const char* e = getenv("BPK_UPFIRDN_ROLL");
+    return e ? atoi(e) : -1;
+  }();
+  return r;
+}
+
+int roll_rows_down2(int major, int out_h, int strips_x, int segs) {
+  const int r = roll_env();
+  if (r >= 0) return r;
+  const double per = (double)major * out_h * strips_x / (32768.0 * segs);
+  return std::max(3, std::min(64, (int)(per + 0.5)));
+}
+
+int roll_rows_fir(int out_h) {
+  const int r = roll_env();
+  if (r >= 0) return r;
+  for (int c = 5; c <= 8; ++c)
+    if (out_h % c == 0) return c;
+  return 6;
+}
+
+bool try_roll(const float* x, const float* k, float* out, int major, int in_h, int in_w, int kh,
+              int kw, int down, int p0, int out_h, int out_w, hipStream_t st, int* rc) {
+  if (roll_env() == 0) return false;
+  const bool a16 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && in_w % 4 == 0;
+  if (down == 2 && a16 && (p0 == 1 || p0 == 2)) {
+    const int lanes = (int)bpk::ceil_div(out_w, 2);  // two output columns per lane
+    const int sw = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
+    const int rows = roll_rows_down2(major, out_h, (int)bpk::ceil_div(out_w, 2 * sw), 64 / sw);
+#define BPK_ROLL2(P, SW) \
+  return (*rc = launch_roll<2, P, SW, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+    if (p0 == 1) {
+      if (sw == 8) BPK_ROLL2(1, 8);
+      if (sw == 16) BPK_ROLL2(1, 16);
+      if (sw == 32) BPK_ROLL2(1, 32);
+      BPK_ROLL2(1, 64);
+    }
+    if (sw == 8) BPK_ROLL2(2, 8);
+    if (sw == 16) BPK_ROLL2(2, 16);
+    if (sw == 32) BPK_ROLL2(2, 32);
+    BPK_ROLL2(2, 64);
+#undef BPK_ROLL2
+  }
+  if (down == 1 && p0 == 2 && (out_w & 1) && kw == 4 && a16) {
+    const int rows = roll_rows_fir(out_h);
+    static const bool noc2 = getenv("BPK_UPFIRDN_FIR_NOC2") != nullptr;
+    if (noc2) {  // two columns per lane + the tail (8-byte loads / stores)
+      const int lanes2 = (out_w - 1) / 2;
+#define BPK_ROLLT2(SW) \
+  return (*rc = launch_roll<1, 2, SW, 2, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+      if (lanes2 == 64) BPK_ROLLT2(64);
+      if (lanes2 == 32) BPK_ROLLT2(32);
+      if (lanes2 == 16) BPK_ROLLT2(16);
+      if (lanes2 == 8) BPK_ROLLT2(8);
+#undef BPK_ROLLT2
+    }
+    const int lanes4 = (out_w - 1) / 4;  // 2^k + 1 wide: four columns per lane + the tail
+    static const bool align = getenv("BPK_UPFIRDN_FIR_ALIGN") != nullptr;
+    if (align) {
+#define BPK_ROLLTA(SW) \
+  return (*rc = launch_roll<1, 2, SW, 4, true, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+      if (lanes4 == 64) BPK_ROLLTA(64);
+      if (lanes4 == 32) BPK_ROLLTA(32);
+      if (lanes4 == 16) BPK_ROLLTA(16);
+      if (lanes4 == 8) BPK_ROLLTA(8);
+#undef BPK_ROLLTA
+    }
+#define BPK_ROLLT(SW) \
+  return (*rc = launch_roll<1, 2, SW, 4, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+    if (lanes4 == 64) BPK_ROLLT(64);
+    if (lanes4 == 32) BPK_ROLLT(32);
+    if (lanes4 == 16) BPK_ROLLT(16);
+    if (lanes4 == 8) BPK_ROLLT(8);
+#undef BPK_ROLLT
+  }
+  return false;
+}
+
 // returns true (and sets *rc) when a streaming specialisation applies
 bool try_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                 int kh, int kw, int up, int down, int p0, int out_h, int out_w, hipStream_t st,
@@ -423,6 +790,8 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
   (*rc = launch_stream<U, D, P, RR>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true)
   // strip heights measured on MI355X (tools/ab_upfirdn.sh): R = 4 (down2), 16 (up2), 8 (1x1)
   if (in_w % 2 != 0) return false;  // 8-byte row loads need an even row pitch
+  if (up == 1 && try_roll(x, k, out, major, in_h, in_w, kh, kw, down, p0, out_h, out_w, st, rc))
+    return true;
   if (up == 1 && down == 2) {
     // two output columns per lane (16-byte input loads) where rows allow it; BPK_UPFIRDN_NOC1=1
     // keeps one column per lane (8-byte loads) everywhere
