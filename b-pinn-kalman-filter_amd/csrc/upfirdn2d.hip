@@ -422,7 +422,7 @@ int launch_stream(const float* x, const float* k, float* out, int major, int in_
 // 10 / 8 rows for the 4-row strips) at ~half the registers.  The next input row's loads are
 // issued before the current row's arithmetic (one row of prefetch).
 //   out row oy reads input rows oy*DOWN - P0 + i, i < 4: input row t feeds tap i = t - oy*DOWN + P0.
-template <int DOWN, int P0, int SEGW, int NOC, bool TAIL, bool ALIGN = false>
+template <int DOWN, int P0, int SEGW, int NOC, bool TAIL>
 __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ x,
                                                        const float* __restrict__ kern,
                                                        float* __restrict__ out, int in_h,
@@ -520,51 +520,6 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
   const int oxl = ox0 + NOC * sl;
   float* op = out + plane * out_h * out_w;
   auto store = [&](int oy, const float (&acc)[NOCT]) {
-    if constexpr (ALIGN) {
-      static_assert(NOC == 4 && TAIL, "aligned stores: the 4-column tail path");
-      // odd row pitch: re-cut the row into 16-byte aligned quads.  Column s is the first at an
-      // aligned address; lane l stores columns 4 l + s .. 4 l + s + 3 (its own s..3 and the
-      // next lane's 0..s-1), lane 0 the s leading columns, the last lane what is left of the
-      // row (the tail column included).  Shuffles run on every lane (inactive ones too).
-      const bool ok = active && oy >= oyb && oy < oye;
-      const int64_t rb = (plane * out_h + oy) * (int64_t)out_w;
-      const int sh = (int)((4 - (rb & 3)) & 3);
-      float nx[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) nx[c] = __shfl_down(acc[c], 1, SEGW);
-      if (!ok) return;
-      float* orow = op + (int64_t)oy * out_w;
-      const bool last = sl == SEGW - 1;
-      if (last) nx[0] = acc[NOC];  // column 4 SEGW = the tail
-      float q[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int a = c + sh;  // 0..6: own[a] for a < 4, else nx[a - 4]
-        float v = acc[0];
-        v = a == 1 ? acc[1] : v;
-        v = a == 2 ? acc[2] : v;
-        v = a == 3 ? acc[3] : v;
-        v = a == 4 ? nx[0] : v;
-        v = a == 5 ? nx[1] : v;
-        v = a == 6 ? nx[2] : v;
-        q[c] = v;
-      }
-      const int c0 = NOC * sl + sh;  // first column of this lane's quad
-      if (!last || c0 + 3 <= out_w - 1) {
-        *reinterpret_cast<float4*>(orow + c0) = make_float4(q[0], q[1], q[2], q[3]);
-        if (last && c0 + 3 < out_w - 1) orow[out_w - 1] = acc[NOC];  // sh = 0: the tail alone
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c0 + c <= out_w - 1) orow[c0 + c] = q[c];
-      }
-      if (sl == 0) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          if (c < sh) orow[c] = acc[c];
-      }
-      return;
-    }
     if (!active || oy < oyb || oy >= oye) return;
     float* orow = op + (int64_t)oy * out_w;
     if constexpr (NOC == 4 && TAIL) {  // odd row pitch: the widest store the address allows
@@ -677,7 +632,7 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
   }
 }
 
-template <int DOWN, int P0, int SEGW, int NOC, bool TAIL = false, bool ALIGN = false>
+template <int DOWN, int P0, int SEGW, int NOC, bool TAIL = false>
 int launch_roll(const float* x, const float* k, float* out, int major, int in_h, int in_w, int kh,
                 int kw, int out_h, int out_w, int rows, hipStream_t st) {
   const int strips_x = TAIL ? 1 : (int)bpk::ceil_div(out_w, SEGW * NOC);
@@ -686,7 +641,7 @@ int launch_roll(const float* x, const float* k, float* out, int major, int in_h,
   if (n <= 0) return BPK_OK;
   const int64_t blocks = bpk::ceil_div(n, 4 * (64 / SEGW));
   BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
-  hipLaunchKernelGGL((upfirdn2d_roll<DOWN, P0, SEGW, NOC, TAIL, ALIGN>), dim3((unsigned)blocks), dim3(256),
+  hipLaunchKernelGGL((upfirdn2d_roll<DOWN, P0, SEGW, NOC, TAIL>), dim3((unsigned)blocks), dim3(256),
                      0, st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, rows, strips_x, strips_y, n);
   BPK_LAUNCH_CHECK("upfirdn2d_roll");
   return BPK_OK;
@@ -756,16 +711,6 @@ bool try_roll(const float* x, const float* k, float* out, int major, int in_h, i
 #undef BPK_ROLLT2
     }
     const int lanes4 = (out_w - 1) / 4;  // 2^k + 1 wide: four columns per lane + the tail
-    static const bool align = getenv("BPK_UPFIRDN_FIR_ALIGN") != nullptr;
-    if (align) {
-#define BPK_ROLLTA(SW) \
-  return (*rc = launch_roll<1, 2, SW, 4, true, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
-      if (lanes4 == 64) BPK_ROLLTA(64);
-      if (lanes4 == 32) BPK_ROLLTA(32);
-      if (lanes4 == 16) BPK_ROLLTA(16);
-      if (lanes4 == 8) BPK_ROLLTA(8);
-#undef BPK_ROLLTA
-    }
 #define BPK_ROLLT(SW) \
   return (*rc = launch_roll<1, 2, SW, 4, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
     if (lanes4 == 64) BPK_ROLLT(64);

@@ -14,6 +14,7 @@ its weights transforms each filter once.
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 import os
 
@@ -49,16 +50,58 @@ def supported(x, weight):
     return small_supported(x, weight) or wino_supported(x, weight)
 
 
+_STATIC_FILTERS = None  # the registry of a capture in `static_filters` (else None)
+
+
+@contextlib.contextmanager
+def static_filters(registry: list):
+    """Inside this block, a hipGraph capture reads the eagerly cached Winograd filter
+    transforms instead of recording the transform kernels: each (weight, U) it uses is
+    appended to `registry`, and the capturing code calls refresh_filters(registry) before
+    replaying, which rewrites a U in place when its weight's version counter has moved (EMA
+    copy_to, load_state_dict, an optimizer step).  The PC sampler's step graph uses this:
+    its weights do not change between replays, so ~185 filter transforms per step go."""
+    global _STATIC_FILTERS
+    prev, _STATIC_FILTERS = _STATIC_FILTERS, registry
+    try:
+        yield registry
+    finally:
+        _STATIC_FILTERS = prev
+
+
+def _transform_into(weight, U, ft):
+    w = weight.detach().contiguous()
+    Cout, Cin = (w.shape[1], w.shape[0]) if ft else (w.shape[0], w.shape[1])
+    fn = lib.bpk_conv3x3_wino_filter_ft_f32 if ft else lib.bpk_conv3x3_wino_filter_f32
+    check(fn(w.data_ptr(), U.data_ptr(), Cin, Cout, stream_ptr(w.device)), "conv3x3 filter")
+
+
+def refresh_filters(registry: list):
+    """Recompute, in place, the registered transforms whose weight changed since capture."""
+    for i, (weight, U, ft, ver) in enumerate(registry):
+        if weight._version != ver:
+            _transform_into(weight, U, ft)
+            registry[i] = (weight, U, ft, weight._version)
+
+
 def filter_transform(weight, ft=False):
     """U [Cin, CoutP, 16] (CoutP = Cout rounded up to 64), cached on `weight` while its
     version counter is unchanged.  ft=True: the transform of _flip_t(weight) (the filter of
     the backward-data conv, Cin = weight.shape[0]), read from `weight` in place."""
     attr = "_bpk_wino_u_ft" if ft else "_bpk_wino_u"
-    # under hipGraph capture the transform is always recorded (and the cache left alone):
-    # replays run after optimizer steps have rewritten the weight in place, so a cached U
-    # baked into the graph would be stale from the second replay on
+    # under hipGraph capture the transform is recorded (and the cache left alone): replays
+    # run after optimizer steps have rewritten the weight in place, so a cached U baked into
+    # the graph would be stale from the second replay on -- unless the capture registers it
+    # for refresh_filters (static_filters)
     capturing = torch.cuda.is_current_stream_capturing()
-    cached = None if capturing else getattr(weight, attr, None)
+    cached = getattr(weight, attr, None)
+    if capturing and _STATIC_FILTERS is not None and cached is not None \
+            and cached[0] == weight._version:
+        if not any(e[1] is cached[1] for e in _STATIC_FILTERS):
+            _STATIC_FILTERS.append((weight, cached[1], ft, weight._version))
+        return cached[1]
+    if capturing:
+        cached = None
     if cached is not None and cached[0] == weight._version:
         return cached[1]
     w = weight.detach().contiguous()

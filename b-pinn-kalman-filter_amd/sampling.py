@@ -439,6 +439,7 @@ class PCEngine:
         self.sample_offset = self.rank * self.B
         self.seed = seed
         self.graph = None
+        self._filters = []  # Winograd filter transforms the step graph reads (conv.static_filters)
         self._graph_key = None
         self.pred_kind = self._pred_kind()
         self.corr_mode = {LangevinCorrector: 0, AnnealedLangevinDynamics: 1}.get(corrector, None)
@@ -555,6 +556,11 @@ class PCEngine:
         """Run n more PC steps on the current state (no host sync)."""
         if self._done + n > self.sde.N:
             raise ValueError(f"only {self.sde.N - self._done} steps left on the time grid")
+        if self.use_graph and self._filters:
+            # the step graph reads the cached Winograd filter transforms (conv.static_filters):
+            # rewrite those whose weights changed since the capture (EMA copy_to, a load)
+            from op import conv as conv_op
+            conv_op.refresh_filters(self._filters)
         for k in range(n):
             if self.use_graph:
                 for gi, g in enumerate(self.graph):
@@ -577,6 +583,12 @@ class PCEngine:
         return x.clone(), xm.clone()
 
     def _capture(self, model, x, x_mean):
+        from op import conv as conv_op
+        self._filters = []
+        with conv_op.static_filters(self._filters):
+            self._capture_graphs(model, x, x_mean)
+
+    def _capture_graphs(self, model, x, x_mean):
         # static buffers owned by the graph
         self._gx = x.clone()
         self._gxm = x_mean.clone()

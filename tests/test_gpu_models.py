@@ -136,6 +136,18 @@ def test_pc_engine_graph_replay_equals_eager_and_is_shard_invariant(hip):
     xg, _ = graph.run(model, prior)
     assert graph.graph is not None, getattr(graph, "capture_error", "")
     assert torch.equal(xe, xg)
+    # the step graph reads the cached Winograd filter transforms (op.conv.static_filters);
+    # rewriting the weights in place after the capture (as EMA copy_to does) must reach the
+    # replays through refresh_filters
+    assert graph._filters, "no Winograd filter registered by the capture"
+    with torch.no_grad():
+        for p in model.parameters():
+            if p.dim() == 4:
+                p.mul_(1.05)
+    xe2, _ = eager.run(model, prior)
+    xg2, _ = graph.run(model, prior)
+    assert not torch.equal(xe2, xe)
+    assert torch.equal(xe2, xg2)
 
 
 def test_fused_update_kernels_bit_exact_vs_cpu_formula(hip):
