@@ -106,8 +106,31 @@ def time_kernel(fn, stream, reps=10):
     return s.elapsed_time(e) / 1e3 / reps
 
 
+def time_kernel_graph(fn, stream, reps=20):
+    """Average duration (s) of fn() with `reps` launches captured in one hipGraph and timed
+    with HIP events around its replays: short kernels (tens of us) are not stretched by the
+    host's per-call overhead between eager launches."""
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            fn()
+    stream.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        for _ in range(reps):
+            fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        g.replay()
+        s.record(stream)
+        for _ in range(3):
+            g.replay()
+        e.record(stream)
+    e.synchronize()
+    return s.elapsed_time(e) / 1e3 / (3 * reps)
+
+
 # The sampler's dominant kernel: the Winograd conv with the GroupNorm+SiLU prologue
-# (csrc/conv_winograd.hip wino_f23_pipe_kernel<1, true, 8 | 4>), ~75 % of a PC step.  Its roofline
+# (csrc/conv_winograd.hip wino_f23_k16_kernel<true>), ~77 % of a PC step.  Its roofline
 # is taken over the NCSN++ 128x128 shape mix it runs in the sampler: per (cin, cout, hw) the
 # PRE form with bias + GroupNorm partial statistics (Conv_0 of a BigGAN block) and with the
 # residual tail (Conv_1), weighted by their counts per forward (SURVEY.md 8(a) a11): the
@@ -228,10 +251,10 @@ def conv_roofline(dev, batch):
             "traffic_unit": "HBM bytes per forward mix (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
             "algorithmic_bytes": sum((r["n_pre"] + r["n_res"]) * 4.0 * batch * (r["cin"] + r["cout"]) * r["hw"] ** 2
                                      + r["n_res"] * 4.0 * batch * r["cout"] * r["hw"] ** 2 for r in rows),
-            "kernel": "wino_f23_pipe_kernel<1,true,WG> (GroupNorm+SiLU prologue): the NCSN++ "
-                      "128x128 forward's PRE-conv mix -- bias + GN partial statistics on the 8-wave "
-                      "128-cout workgroup form (WG=8), residual tail on the 4-wave 64-cout form "
-                      f"(WG=4); {n_launch} launches, B={batch}",
+            "kernel": "wino_f23_k16_kernel<true> (GroupNorm+SiLU prologue; 8 waves x 16 couts, "
+                      "16-input-channel chunks): the NCSN++ 128x128 forward's PRE-conv mix -- bias + "
+                      "GN partial statistics, and the residual tail + statistics; "
+                      f"{n_launch} launches, B={batch}",
             "flop_basis": "executed (Winograd, 4/9 of direct)",
             "ms_per_mix": round(t * 1e3, 3), "flop_per_mix": fl,
             "direct_equivalent_tflops": round(fl * 9 / 4 / t / 1e12, 2),
@@ -255,7 +278,8 @@ def _upfirdn_out(hw, kw):
 
 
 def upfirdn_rooflines(dev, batch):
-    """HBM roofline of upfirdn2d on the four 8(d) shapes: bytes = 4 (in + out) per launch."""
+    """HBM roofline of upfirdn2d on the four 8(d) shapes: bytes = 4 (in + out) per launch;
+    duration = HIP events around graph replays of 20 launches (time_kernel_graph)."""
     from op import upfirdn2d
     k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32, device=dev)
     st = torch.cuda.Stream(dev)
@@ -263,8 +287,7 @@ def upfirdn_rooflines(dev, batch):
     for name, (c, hw), kw, gain in UPFIRDN_SHAPES:
         x = torch.randn(batch, c, hw, hw, device=dev)
         kg = (k * gain).contiguous()  # the scaled taps outside the timed launches
-        with torch.cuda.stream(st):
-            t = time_kernel(lambda: upfirdn2d(x, kg, **kw), st)
+        t = time_kernel_graph(lambda: upfirdn2d(x, kg, **kw), st)
         ho = _upfirdn_out(hw, kw)
         nbytes = 4.0 * (x.numel() + batch * c * ho * ho)
         ach = nbytes / t / 1e9

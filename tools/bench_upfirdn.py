@@ -1,5 +1,5 @@
-"""upfirdn2d on the four SURVEY 8(d) shapes (B = 64): HIP-event time per launch over 50
-launches (the scaled FIR kernel prepared outside the timed region) and the fraction of the
+"""upfirdn2d on the four SURVEY 8(d) shapes (B = 64): HIP-event time per launch over graph
+replays of 20 launches (bench.time_kernel_graph; the scaled FIR taps prepared outside) and the fraction of the
 8 TB/s HBM peak on the algorithmic bytes 4 (in + out).  Env switches of csrc/upfirdn2d.hip
 select variants for A/B runs."""
 import os
@@ -20,8 +20,7 @@ tag = os.environ.get("TAG", "")
 for name, (c, hw), kw, gain in bench.UPFIRDN_SHAPES:
     x = torch.randn(64, c, hw, hw, device=dev)
     kg = (k * gain).contiguous()
-    with torch.cuda.stream(st):
-        t = bench.time_kernel(lambda: upfirdn2d(x, kg, **kw), st, reps=50)
+    t = bench.time_kernel_graph(lambda: upfirdn2d(x, kg, **kw), st, reps=20)
     ho = bench._upfirdn_out(hw, kw)
     nbytes = 4.0 * (x.numel() + 64 * c * ho * ho)
     print(f"{tag} {name}: {t * 1e6:7.1f} us  {nbytes / t / 1e9:7.0f} GB/s  frac {nbytes / t / 8e12:.3f}",
