@@ -384,32 +384,89 @@ def _small_img(x):
     return _SEL3 and _IG_MODE != "0" and x.shape[2] * x.shape[3] <= _SEL3_MAX_HW
 
 
+# Reproducibility of the per-call choice (the timing is noisy, so two runs -- or two ranks --
+# could take different kernels for the same call and differ in the last bits):
+#  * BPK_CONV_PICK=first: no timing, always the first candidate (igemm / Winograd);
+#  * BPK_CONV_TABLE=path.json: choices are read from the file at import and every new
+#    choice is written back (a run can replay another run's table exactly);
+#  * under torch.distributed with world size > 1 the choice of rank 0 is broadcast, so
+#    every rank runs the same kernels (the calls are SPMD: every rank reaches each new key
+#    in the same order).
+_PICK_FIRST = os.environ.get("BPK_CONV_PICK", "") == "first"
+_TABLE_PATH = os.environ.get("BPK_CONV_TABLE")
+
+
+def _key_str(key):
+    return repr(key)
+
+
+def _load_table():
+    if not _TABLE_PATH or not os.path.exists(_TABLE_PATH):
+        return {}
+    import json
+    with open(_TABLE_PATH) as f:
+        return {k: int(v) for k, v in json.load(f).items()}
+
+
+_TABLE = _load_table()
+
+
+def _save_table():
+    import json
+    tmp = _TABLE_PATH + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(_TABLE, f, indent=0, sort_keys=True)
+    os.replace(tmp, _TABLE_PATH)
+
+
+def _agree(c: int) -> int:
+    """Rank 0's choice on every rank (identity when not distributed)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return c
+    dev = "cpu" if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([c], dtype=torch.int64, device=dev)
+    dist.broadcast(t, 0)
+    return int(t.item())
+
+
+def _decide(key, timers):
+    """Index of the candidate to run for `key`: cached, from the table, or timed once
+    (None under graph capture for a key never decided eagerly)."""
+    c = _CHOICE.get(key)
+    if c is not None:
+        return c
+    ks = _key_str(key)
+    if ks in _TABLE:
+        c = _TABLE[ks]
+    elif _PICK_FIRST:
+        c = 0
+    elif torch.cuda.is_current_stream_capturing():
+        return None
+    else:
+        with torch.no_grad():
+            ts = [_time_us(f) for f in timers]
+        c = _agree(min(range(len(timers)), key=ts.__getitem__))
+        if _TABLE_PATH:
+            _TABLE[ks] = c
+            _save_table()
+    _CHOICE[key] = c
+    return c
+
+
 def _pick_any(key, cands):
     """cands[i]() for the candidate the cached per-key timing says is fastest (the first
     one under graph capture for a key never timed eagerly)."""
-    c = _CHOICE.get(key)
-    if c is None:
-        if torch.cuda.is_current_stream_capturing():
-            return cands[0]()
-        with torch.no_grad():
-            ts = [_time_us(f) for f in cands]
-        c = min(range(len(cands)), key=ts.__getitem__)
-        _CHOICE[key] = c
-    return cands[c]()
+    c = _decide(key, cands)
+    return cands[0 if c is None else c]()
 
 
 def _pick(key, run_ig, run_mi):
-    """run_ig() or run_mi(), whichever the cached per-key timing says is faster."""
+    """run_ig() or run_mi(), whichever the cached per-key timing says is faster (ties: igemm)."""
     if _IG_MODE == "2":
         return run_ig()
-    c = _CHOICE.get(key)
-    if c is None:
-        if torch.cuda.is_current_stream_capturing():
-            return run_ig()
-        with torch.no_grad():
-            c = _time_us(run_ig) <= _time_us(run_mi)
-        _CHOICE[key] = c
-    return run_ig() if c else run_mi()
+    c = _decide(key, [run_ig, run_mi])
+    return run_mi() if c == 1 else run_ig()
 
 
 def conv2d_select(x, w, bias, stride, padding):

@@ -1,0 +1,85 @@
+"""Host logic of the per-call conv kernel choice (op/conv.py `_decide`): a table file is
+replayed exactly and new choices are written back, BPK_CONV_PICK=first skips the timing, and
+under torch.distributed every rank takes rank 0's choice (gloo, world size 2) -- so runs and
+ranks do not differ by a noisy timing."""
+import json
+import os
+import sys
+
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _never():
+    raise AssertionError("timed a candidate that the table / policy already decides")
+
+
+def test_table_replay_and_pick_first(tmp_path, monkeypatch):
+    from op import conv
+    key = ("fwd", (2, 8, 16, 16), (8, 8, 3, 3), (2, 2), (1, 1), True)
+    path = tmp_path / "t.json"
+    path.write_text(json.dumps({conv._key_str(key): 1}))
+    monkeypatch.setattr(conv, "_TABLE_PATH", str(path))
+    monkeypatch.setattr(conv, "_TABLE", conv._load_table())
+    monkeypatch.setattr(conv, "_CHOICE", {})
+    assert conv._decide(key, [_never, _never]) == 1
+    assert conv._CHOICE[key] == 1
+    # policy "first": no timing, candidate 0, and nothing invented for the table
+    key2 = ("dgrad", (2, 8, 16, 16), (8, 8, 3, 3), (1, 1), (1, 1))
+    monkeypatch.setattr(conv, "_PICK_FIRST", True)
+    assert conv._decide(key2, [_never, _never]) == 0
+    assert conv._pick(key2, lambda: "ig", lambda: "mi") == "ig"
+    assert conv._pick(key, lambda: "ig", lambda: "mi") == "mi"
+
+
+def test_new_choice_written_back(tmp_path, monkeypatch):
+    from op import conv
+    path = tmp_path / "t.json"
+    monkeypatch.setattr(conv, "_TABLE_PATH", str(path))
+    monkeypatch.setattr(conv, "_TABLE", {})
+    monkeypatch.setattr(conv, "_CHOICE", {})
+    monkeypatch.setattr(conv, "_PICK_FIRST", False)
+    monkeypatch.setattr(conv.torch.cuda, "is_current_stream_capturing", lambda: False)
+    times = iter([5.0, 2.0, 9.0])
+    monkeypatch.setattr(conv, "_time_us", lambda f: next(times))
+    key = ("wgrad", (4, 3, 8, 8), (6, 3, 3, 3), (1, 1), (1, 1), False)
+    assert conv._decide(key, [None, None, None]) == 1
+    assert json.loads(path.read_text()) == {conv._key_str(key): 1}
+
+
+def _worker(rank, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE="2", LOCAL_RANK=str(rank))
+        sys.path[:0] = [os.path.join(HERE, "..", "b-pinn-kalman-filter_amd"), os.path.join(HERE, "..")]
+        import torch.distributed as dist
+        from op import conv
+        dist.init_process_group("gloo")
+        conv._TABLE_PATH = None
+        conv._PICK_FIRST = False
+        conv.torch.cuda.is_current_stream_capturing = lambda: False
+        # rank 0 times candidate 1 faster, rank 1 candidate 0
+        times = iter([3.0, 1.0] if rank == 0 else [1.0, 3.0])
+        conv._time_us = lambda f: next(times)
+        c = conv._decide(("fwd", rank), [None, None])  # keys may differ: only the order matters
+        q.put((rank, c, None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_ranks_take_rank0_choice():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33000 + os.getpid() % 2000
+    ps = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[2] is None, r[2]
+    assert [r[1] for r in res] == [1, 1]
