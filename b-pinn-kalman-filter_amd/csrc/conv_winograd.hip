@@ -95,6 +95,8 @@ struct WinoGeo {
   float div;  // fused residual: y = (skip + (conv + bias)) / div when skip != nullptr
   int C1;     // input channels [0, C1) from x, [C1, Cin) from x2 (pipelined kernel only)
   int CoutS;  // couts stored (y, skip, stats channel count); Cout = CoutS rounded up to 64
+  int up;     // 16-cin kernel only: 1 = x is [N, Cin, H/2, W/2], convolved as its nearest x2
+              // upsample (the ddpm net's Upsample + Conv_0, reference layers.py:576-590)
 };
 
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
@@ -949,14 +951,16 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
 
   f4 acc[16][2];
   const int64_t plane = (int64_t)g.H * g.W;
+  const int up = g.up;  // nearest x2 input: the patch reads x[iy >> 1][ix >> 1] of an H/2 x W/2 plane
+  const int64_t xplane = plane >> (2 * up);
   const int C2 = g.Cin - g.C1;
-  const float* xn = x + (int64_t)n * g.C1 * plane;
+  const float* xn = x + (int64_t)n * g.C1 * xplane;
   const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
   const int kq = lane >> 4, jj = lane & 15;
   const int nch = g.Cin / CK;
 
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xn), 0, (int)(g.C1 * plane * 4), 0x00020000);
+      const_cast<float*>(xn), 0, (int)(g.C1 * xplane * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t xrs2 = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(C2 > 0 ? x2 + (int64_t)n * C2 * plane : xn), 0,
       (int)((C2 > 0 ? C2 : g.C1) * plane * 4), 0x00020000);
@@ -973,18 +977,18 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
     const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
     pin = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
     const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
-    poff = (cy * g.W + cx) * 4;
+    poff = ((cy >> up) * (g.W >> up) + (cx >> up)) * 4;
     pdst = py * kPCp + px + ph * 8 * (kPR * kPCp);
   }
   float pv[8];
   auto load_patch_part = [&](float* dst, int k, int c0, int cn) {
     const int cc = min(k, nch - 1) * CK;
     const bool second = cc >= g.C1;
-    const int soff = ((second ? cc - g.C1 : cc) + ph * 8) * (int)plane * 4;
+    const int soff = ((second ? cc - g.C1 : cc) + ph * 8) * (int)xplane * 4;
 #pragma unroll
     for (int c = c0; c < c0 + cn; ++c)
       dst[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-          second ? xrs2 : xrs, poff, soff + c * (int)plane * 4, 0));
+          second ? xrs2 : xrs, poff, soff + c * (int)xplane * 4, 0));
   };
   auto store_patch_part = [&](const float* src, float* sp, int k, int c0, int cn) {
     const int cb0 = min(k, nch - 1) * CK + ph * 8;
@@ -1701,6 +1705,31 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
   }
 #undef WINO_LAUNCH
   BPK_LAUNCH_CHECK("conv3x3_wino");
+  return BPK_OK;
+}
+
+extern "C" int bpk_conv3x3_wino_up2_supported(int N, int Cin, int Cout, int H, int W) {
+  return bpk_conv3x3_wino_supported(N, Cin, Cout, H, W) && wino_pipe_env() != 0 &&
+         Cin % 16 == 0 && cout_padded(Cout) % 128 == 0;
+}
+
+// y = conv3x3(nearest_x2(x)) + bias for x [N, Cin, H/2, W/2], y [N, Cout, H, W]: the 16-cin
+// kernel reads the half-resolution input inside its patch load, so the upsampled tensor is
+// never written (reference layers.py:576-590, Upsample(with_conv=True)).
+extern "C" int bpk_conv3x3_wino_up2_f32(const float* x, const float* U, const float* bias,
+                                        float* y, int N, int Cin, int Cout, int H, int W,
+                                        void* stream) {
+  BPK_REQUIRE(bpk_conv3x3_wino_up2_supported(N, Cin, Cout, H, W),
+              "conv3x3_wino_up2: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 16, "
+              "Cout %% 128, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
+  const int CoutP = cout_padded(Cout);
+  WinoGeo gk{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / 128, 1.0f, Cin, Cout, 1};
+  const int64_t items = (int64_t)N * gk.regions_x * gk.regions_y * gk.cout_blocks;
+  BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino_up2: grid too large");
+  hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3((unsigned)items), dim3(512), 0,
+                     bpk::as_stream(stream), x, U, bias, nullptr, nullptr, y, nullptr, gk,
+                     (items % 8 == 0) ? 1 : 0, nullptr);
+  BPK_LAUNCH_CHECK("conv3x3_wino_up2");
   return BPK_OK;
 }
 

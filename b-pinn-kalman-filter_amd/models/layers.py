@@ -301,6 +301,10 @@ class Upsample(nn.Module):
 
     def forward(self, x):
         B, C, H, W = x.shape
+        if (self.with_conv and _WINO_ENABLED and x.is_cuda
+                and conv_op.up2_supported(x, self.Conv_0.weight)):
+            # the upsample read inside the Winograd conv's patch load (BPK_WINO_UP2=0: off)
+            return conv_op.conv3x3_up2(x, self.Conv_0.weight, self.Conv_0.bias)
         h = F.interpolate(x, (H * 2, W * 2), mode="nearest")
         return self.Conv_0(h) if self.with_conv else h
 

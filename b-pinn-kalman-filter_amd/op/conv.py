@@ -730,6 +730,81 @@ def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
     return _Conv3x3.apply(x, weight, bias, skip, div)
 
 
+def up2_supported(x, weight):
+    """conv3x3(nearest_x2(x)) on the fused kernel (bpk_conv3x3_wino_up2_f32) for these operands"""
+    if not (_WINO_UP2 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and weight.dtype == torch.float32 and tuple(weight.shape[1:]) == (x.shape[1], 3, 3)):
+        return False
+    N, C, H, W = x.shape
+    return bool(lib.bpk_conv3x3_wino_up2_supported(N, C, weight.shape[0], 2 * H, 2 * W))
+
+
+_WINO_UP2 = os.environ.get("BPK_WINO_UP2", "1") != "0"
+
+
+def _up2_raw(x, weight, bias):
+    x = x.detach().contiguous()
+    N, C, H, W = x.shape
+    Cout = weight.shape[0]
+    U = filter_transform(weight, False)
+    y = torch.empty((N, Cout, 2 * H, 2 * W), dtype=x.dtype, device=x.device)
+    b = None if bias is None else bias.detach().contiguous()
+    check(lib.bpk_conv3x3_wino_up2_f32(x.data_ptr(), U.data_ptr(),
+                                       None if b is None else b.data_ptr(), y.data_ptr(),
+                                       N, C, Cout, 2 * H, 2 * W, stream_ptr(x.device)),
+          "conv3x3_wino_up2")
+    flops.wino3x3("wino_fwd", N, C, Cout, 2 * H, 2 * W)
+    return y
+
+
+def _sum2x2(g):
+    """adjoint of the nearest x2 upsample: the sum of each 2 x 2 block"""
+    N, C, H2, W2 = g.shape
+    return g.reshape(N, C, H2 // 2, 2, W2 // 2, 2).sum((3, 5))
+
+
+class _ConvUp2(torch.autograd.Function):
+    """y = conv3x3(nearest_x2(x), w) + b in one launch.  Backward: d/dx = the 2 x 2 block sums
+    of the backward-data conv, d/dw = the weight gradient against the upsampled input
+    (recomputed), d/db = the sum of gy -- all recorded ops, so higher orders work too."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        mark_inputs(ctx, x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return _up2_raw(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gw = gb = None
+        if want_grad(ctx, 0):
+            gx = _sum2x2(_conv_ft_any(gy, w))
+        want_b = ctx.has_bias and want_grad(ctx, 2)
+        if want_grad(ctx, 1) or want_b:
+            xu = F.interpolate(x, scale_factor=2, mode="nearest")
+            if torch.is_grad_enabled():
+                gw = _Wgrad3x3.apply(xu, gy, tuple(w.shape)) if want_grad(ctx, 1) else None
+                gb = gy.sum((0, 2, 3)) if want_b else None
+            else:
+                dw, gb = _wgrad_impl(xu, gy, tuple(w.shape), want_b)
+                gw = dw if want_grad(ctx, 1) else None
+        return gx, gw, gb
+
+
+def conv3x3_up2(x, weight, bias=None):
+    """F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest'), weight, bias, padding=1)
+    without materialising the upsampled input (ddpm Upsample, reference layers.py:576-590);
+    differentiable.  Raises when up2_supported(x, weight) is False."""
+    require_hip(x, weight, bias, what="conv3x3_up2")
+    if not up2_supported(x, weight):
+        raise RuntimeError(f"conv3x3_up2: unsupported operands {tuple(x.shape)} x {tuple(weight.shape)}")
+    if _needs_grad(x, weight, bias):
+        return _ConvUp2.apply(x, weight, bias)
+    return _up2_raw(x, weight, bias)
+
+
 def gemm1x1_supported(x, weight, x2=None):
     """The MFMA 1x1-conv GEMM (csrc/gemm_nchw.hip) runs conv1x1([x, x2], weight)."""
     if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4 or not x.is_cuda:

@@ -379,6 +379,15 @@ int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, const float
                             const float* U, const float* bias, const float* skip, float div,
                             float* y, float* stats, int N, int Cin, int Cout, int H, int W,
                             void* stream);
+/* y = conv3x3(nearest_x2(x)) + bias (bias may be NULL) for x [N, Cin, H/2, W/2] and y
+ * [N, Cout, H, W]: F.interpolate(x, scale_factor=2, mode='nearest') followed by Conv_0 of the
+ * ddpm net's Upsample (reference models/layers.py:576-590), with the upsample read inside the
+ * Winograd kernel's patch load (the full-resolution input is never materialised).  U from
+ * bpk_conv3x3_wino_filter_f32.  Needs Cin % 16 == 0, Cout % 128 == 0, H % 8, W % 16 == 0
+ * (bpk_conv3x3_wino_up2_supported). */
+int bpk_conv3x3_wino_up2_supported(int N, int Cin, int Cout, int H, int W);
+int bpk_conv3x3_wino_up2_f32(const float* x, const float* U, const float* bias, float* y, int N,
+                             int Cin, int Cout, int H, int W, void* stream);
 /* Weight gradient of the same conv (the backward-filter convolution cuDNN / MIOpen runs
  * for nn.Conv2d's autograd): dw [Cout, Cin, 3, 3] = d(sum y * gy)/dw for x [N, Cin, H, W],
  * gy [N, Cout, H, W].  Winograd F(2x2,3x3): per transform position a split-K GEMM

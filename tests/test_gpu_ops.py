@@ -1215,3 +1215,51 @@ def test_conv3x3_winograd_large_launch(hip, mode):
         part, R, cnt = gn_partials(out)
         m = out.reshape(N, cout, hw // 8, 8, hw // 16, 16).mean((3, 5)).reshape(N, cout, R)
         assert (part[..., 0] - m).abs().max().item() <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("N,cin,cout,h,w", [(2, 128, 128, 8, 16), (3, 256, 256, 16, 8),
+                                             (1, 16, 128, 32, 32), (2, 64, 256, 4, 24)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_conv3x3_up2_fused_nearest_upsample(hip, N, cin, cout, h, w, with_bias):
+    """conv3x3(nearest_x2(x)) with the upsample read in the Winograd patch load (ddpm
+    Upsample, reference layers.py:576-590) vs a float64 interpolate + direct conv; 2e-5 of
+    max|ref| as the plain Winograd conv.  Gradients (x, w, b) vs torch autograd of
+    interpolate + F.conv2d, 3e-5 of max|ref| as the Winograd backward test."""
+    from op.conv import conv3x3_up2, up2_supported
+    g = torch.Generator().manual_seed(N * 100 + cin + h)
+    x = torch.randn(N, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(cout, generator=g) if with_bias else None
+    xu = F.interpolate(x.double(), scale_factor=2, mode="nearest")
+    ref = F.conv2d(xu, wt.double(), None if b is None else b.double(), padding=1)
+    assert up2_supported(x.to(hip), wt.to(hip))
+    out = conv3x3_up2(x.to(hip), wt.to(hip), None if b is None else b.to(hip)).double().cpu()
+    assert out.shape == ref.shape
+    assert (out - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+    # autograd
+    xg = x.to(hip).requires_grad_()
+    wg = wt.to(hip).requires_grad_()
+    bg = None if b is None else b.to(hip).requires_grad_()
+    go = torch.randn(ref.shape, generator=g).to(hip)
+    ins = (xg, wg) + (() if bg is None else (bg,))
+    got = torch.autograd.grad(conv3x3_up2(xg, wg, bg), ins, go)
+    exp = torch.autograd.grad(F.conv2d(F.interpolate(xg, scale_factor=2, mode="nearest"), wg, bg,
+                                       padding=1), ins, go)
+    for a, r in zip(got, exp):
+        assert (a - r).abs().max().item() <= 3e-5 * r.abs().max().item()
+
+
+def test_ddpm_upsample_module_fused_equals_unfused(hip, monkeypatch):
+    """layers.Upsample(with_conv=True) takes the fused kernel and matches the interpolate +
+    Conv_0 path it replaces (BPK_WINO_UP2=0 equivalent), eval and under autograd."""
+    from models import layers
+    from op import conv as conv_op
+    torch.manual_seed(0)
+    m = layers.Upsample(128, with_conv=True).to(hip)
+    x = torch.randn(2, 128, 16, 16, device=hip)
+    with torch.no_grad():
+        fused = m(x)
+        monkeypatch.setattr(conv_op, "_WINO_UP2", False)
+        plain = m(x)
+    assert fused.shape == (2, 128, 32, 32)
+    assert (fused - plain).abs().max().item() <= 1e-5 * plain.abs().max().item()
