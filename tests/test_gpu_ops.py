@@ -1263,3 +1263,20 @@ def test_ddpm_upsample_module_fused_equals_unfused(hip, monkeypatch):
         plain = m(x)
     assert fused.shape == (2, 128, 32, 32)
     assert (fused - plain).abs().max().item() <= 1e-5 * plain.abs().max().item()
+
+
+@pytest.mark.parametrize("hw", [(64, 64), (7, 12), (33, 64), (64, 4)])
+def test_upfirdn2d_fir_pad2_asymmetric_taps(hip, hw):
+    """The 1:1 FIR with pad (2, 2) and an asymmetric random 4x4 kernel -- the flip of the
+    true convolution is visible -- on 37 planes (every base alignment of the odd-pitch
+    output; the rolling kernel's tail-column path for 2^k widths) vs the oracle."""
+    from op import upfirdn2d
+    from oracle.upfirdn2d_ref import upfirdn2d_np
+    H, W = hw
+    g = torch.Generator().manual_seed(7 * H + W)
+    x = torch.randn(37, 1, H, W, generator=g)
+    k = torch.randn(4, 4, generator=g).numpy().astype(np.float32)
+    y = upfirdn2d(x.to(hip), torch.tensor(k, device=hip), pad=(2, 2)).cpu().numpy()
+    ref = upfirdn2d_np(x.numpy(), k, (1, 1), (1, 1), (2, 2, 2, 2))
+    assert y.shape == ref.shape == (37, 1, H + 1, W + 1)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
