@@ -264,10 +264,18 @@ def gen_dps256(seed=31):
     t_probe = [0.9, 0.4]
     probes = np.stack([funcs[0](tp, x.numpy().reshape(-1).astype(np.float64))
                        for tp in t_probe]).astype(np.float32)
+    # a short stretch of the reference's own RK45 solve at 256^2 (scipy solve_ivp on the
+    # captured ODE function, the tolerances of the reference's get_solver): accepted steps,
+    # nfev and the final state
+    t_span = (0.5, 0.45)
+    sol = real_ivp(funcs[0], t_span, x.numpy().reshape(-1).astype(np.float64), method="RK45",
+                   rtol=1e-3, atol=1e-3)
     _save("cfg_dps256.npz", mask=mask.numpy(), origin=origin.numpy(), x=x.numpy(),
           labels=labels.numpy(), y=y.numpy(), obs_noise=draws[0].numpy(),
           t_probe=np.array(t_probe), probes=probes, variance=np.array(cfg.inverse.variance),
-          seed=np.array(seed), **_structure(cfg, model))
+          seed=np.array(seed), solve_t_span=np.array(t_span), solve_t=sol.t,
+          solve_y=sol.y[:, -1].astype(np.float64), solve_nfev=np.array(sol.nfev),
+          **_structure(cfg, model))
 
 
 def gen_pinn64():
@@ -363,6 +371,11 @@ def main(which):
                                        103, "euler_maruyama", "langevin", 0.075, 1, 25, 2),
         "ncddpmpp128_pc": lambda: gen_pc("ncddpmpp128_pc", _ncddpmpp128(nc_ddpmpp), 104,
                                          "ancestral_sampling", "none", 0.16, 1, 25, 1),
+        # the whole N = 1000 trajectory of the benchmark configuration (2000 evaluations,
+        # B = 1; ~25 min on 8 host threads)
+        "ncsnpp128_pc_long": lambda: gen_pc("ncsnpp128_pc_long",
+                                            _ncsnpp128(cifar10_ncsnpp_continuous), 105,
+                                            "euler_maruyama", "langevin", 0.075, 1, 1000, 1),
         "dps256": gen_dps256,
         "pinn64": gen_pinn64,
     }
