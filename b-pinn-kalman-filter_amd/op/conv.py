@@ -391,7 +391,7 @@ def _small_img(x):
 #    choice is written back (a run can replay another run's table exactly);
 #  * under torch.distributed with world size > 1 the choice of rank 0 is broadcast, so
 #    every rank runs the same kernels (the calls are SPMD: every rank reaches each new key
-#    in the same order).
+#    in the same order; code only some ranks run goes inside `local_choices()`).
 _PICK_FIRST = os.environ.get("BPK_CONV_PICK", "") == "first"
 _TABLE_PATH = os.environ.get("BPK_CONV_TABLE")
 
@@ -419,10 +419,25 @@ def _save_table():
     os.replace(tmp, _TABLE_PATH)
 
 
+_LOCAL_ONLY = [False]
+
+
+@contextlib.contextmanager
+def local_choices():
+    """Inside this block new choices are NOT broadcast: for code that only some ranks run
+    (a rank-0-only measurement), where a collective would wait for ranks that never come."""
+    prev, _LOCAL_ONLY[0] = _LOCAL_ONLY[0], True
+    try:
+        yield
+    finally:
+        _LOCAL_ONLY[0] = prev
+
+
 def _agree(c: int) -> int:
     """Rank 0's choice on every rank (identity when not distributed)."""
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if (_LOCAL_ONLY[0] or not (dist.is_available() and dist.is_initialized())
+            or dist.get_world_size() == 1):
         return c
     dev = "cpu" if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
     t = torch.tensor([c], dtype=torch.int64, device=dev)

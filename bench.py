@@ -956,7 +956,9 @@ def main():
     roof = None
     if ctx.rank == 0 and not args.no_roofline:
         log("dominant-kernel roofline (right after the sampler: same clock regime)")
-        roof = conv_roofline(dev, B)
+        from op.conv import local_choices
+        with local_choices():  # rank 0 only: no collective may start in here
+            roof = conv_roofline(dev, B)
 
     # ---------------------------------------------------------------- DSM train step
     train = None
@@ -1029,7 +1031,9 @@ def main():
         up_roof = None
         if not args.no_roofline:
             log("upfirdn2d rooflines")
-            up_roof = upfirdn_rooflines(dev, B)
+            from op.conv import local_choices
+            with local_choices():
+                up_roof = upfirdn_rooflines(dev, B)
         model_tflops = evals_per_s * NCSNPP_GFLOP_PER_EVAL / 1e3
         result = {
             "metric": "PC-sampler score-net evals/s (NCSN++ 128x128x1, EM + Langevin)",

@@ -83,3 +83,23 @@ def test_ranks_take_rank0_choice():
     for r in res:
         assert r[2] is None, r[2]
     assert [r[1] for r in res] == [1, 1]
+
+
+def test_local_choices_skip_the_broadcast(monkeypatch):
+    from op import conv
+
+    def boom(*a, **k):
+        raise AssertionError("collective inside local_choices()")
+    import torch.distributed as dist
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda: 2)
+    monkeypatch.setattr(dist, "get_backend", lambda *a: "gloo")
+    monkeypatch.setattr(dist, "broadcast", boom)
+    with conv.local_choices():
+        assert conv._agree(1) == 1
+    try:
+        conv._agree(1)
+    except AssertionError:
+        pass
+    else:
+        raise AssertionError("the broadcast should run outside local_choices()")
