@@ -1132,6 +1132,20 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
     const float bv = bias ? bias[co] : 0.f;
     const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
     float lm = 0.f, lm2 = 0.f;
+    // residual tail: all eight skip vectors of this lane requested before the first is used
+    // (one exposed memory latency; loaded per store, the compiler waited for each in turn)
+    f4 skv[2][2][2];
+    if (skip) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            skv[mb][h][e] = *reinterpret_cast<const f4*>(
+                &skip[obase + (int64_t)(oy0 + 2 * (2 * mb + (kq >> 1)) + h) * g.W + ox0 +
+                      8 * (kq & 1) + 4 * e]);
+    }
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
       const int oy = oy0 + 2 * (2 * mb + (kq >> 1));
@@ -1154,7 +1168,7 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
           }
           const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
           if (skip) {
-            const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+            const f4 sk = skv[mb][h][e];
 #pragma unroll
             for (int c = 0; c < 4; ++c) v[c] = div_rn(sk[c] + v[c], g.div, rdiv);
           }
