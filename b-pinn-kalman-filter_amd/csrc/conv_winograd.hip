@@ -198,17 +198,31 @@ __device__ inline void store_tile(const float* s_w, const float* __restrict__ sk
   const int64_t plane = (int64_t)g.H * g.W;
   constexpr int kIt = kWN / 2;
   float mm[kIt], qq[kIt];
-#pragma unroll
-  for (int it = 0; it < kIt; ++it) {
+  auto out_off = [&](int it) {
     const int q = it * 64 + lane;
     const int co = q >> 5;                 // 32 float4 per cout (8 rows x 4)
     const int rem = q & 31;
     const int row = rem >> 2, c4 = rem & 3;
+    return (int64_t)n * g.CoutS * plane + (int64_t)(cout_w + co) * plane +
+           (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
+  };
+  // residual tail: every skip vector of the tile requested before the first is used (one
+  // exposed memory latency, as the 16-cin kernel's epilogue)
+  f4 skv[kIt];
+  if (skip) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) skv[it] = *reinterpret_cast<const f4*>(&skip[out_off(it)]);
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int q = it * 64 + lane;
+    const int co = q >> 5;
+    const int rem = q & 31;
+    const int row = rem >> 2, c4 = rem & 3;
     f4 v = *reinterpret_cast<const f4*>(&s_w[co * kOS + row * kOutCols + 4 * c4]);
-    const int64_t o = (int64_t)n * g.CoutS * plane + (int64_t)(cout_w + co) * plane +
-                      (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
+    const int64_t o = out_off(it);
     if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
-      const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+      const f4 sk = skv[it];
       v = f4{(sk[0] + v[0]) / g.div, (sk[1] + v[1]) / g.div, (sk[2] + v[2]) / g.div,
              (sk[3] + v[3]) / g.div};
     }

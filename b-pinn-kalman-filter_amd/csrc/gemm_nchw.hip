@@ -124,13 +124,38 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
 
   // acc[i][j][rr] = Y[m0 + 64 wm + 16 i + 4 kq + rr][p0 + 64 wp + 16 j + jj]
   float* yn = Y + (int64_t)n * g.M * g.P;
+  // the 16 bias values of this lane requested together (loaded per row before a store
+  // group, the compiler waited for each in turn: 16 exposed latencies per workgroup)
+  float bbv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = m0 + 64 * wm + 16 * i + 4 * kq + rr;
+      bbv[i][rr] = (bias && m < g.M) ? bias[m] : 0.f;
+    }
+  // a whole 128-row tile in range (every NCSN++ / DDPM++ shape): one straight-line store
+  // block -- the per-row guard put each store group in its own branch, and the wait counter
+  // (vmcnt counts stores on gfx9) was drained to 0 at every one of them
+  if (m0 + kBM <= g.M) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = m0 + 64 * wm + 16 * i + 4 * kq + rr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          yn[(int64_t)m * g.P + p0 + 64 * wp + 16 * j + jj] = acc[i][j][rr] + bbv[i][rr];
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int m = m0 + 64 * wm + 16 * i + 4 * kq + rr;
       if (m >= g.M) continue;
-      const float bb = bias ? bias[m] : 0.f;
+      const float bb = bbv[i][rr];
 #pragma unroll
       for (int j = 0; j < 4; ++j) yn[(int64_t)m * g.P + p0 + 64 * wp + 16 * j + jj] = acc[i][j][rr] + bb;
     }
