@@ -433,6 +433,11 @@ def local_choices():
         _LOCAL_ONLY[0] = prev
 
 
+def _rank() -> int:
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 def _agree(c: int) -> int:
     """Rank 0's choice on every rank (identity when not distributed)."""
     import torch.distributed as dist
@@ -464,7 +469,8 @@ def _decide(key, timers):
         c = _agree(min(range(len(timers)), key=ts.__getitem__))
         if _TABLE_PATH:
             _TABLE[ks] = c
-            _save_table()
+            if _rank() == 0:  # one writer (every rank holds the same, agreed choices)
+                _save_table()
     _CHOICE[key] = c
     return c
 
