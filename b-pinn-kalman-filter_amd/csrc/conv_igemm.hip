@@ -268,6 +268,47 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
   }
 
   // epilogue: acc[mb][nb][i] = C[m0 + WTM wm + 16 mb + 4 kq + i][n0 + WTN wn + 16 nb + jj]
+  // forward bias: the lane's NBM x 4 values requested together before the stores (loaded per
+  // store, each was waited for in turn)
+  float bbv[NBM][4];
+#pragma unroll
+  for (int mb = 0; mb < NBM; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * WTM + mb * 16 + 4 * kq + i;
+      bbv[mb][i] = (MODE == 0 && g.splits == 1 && bias && m < g.M) ? bias[m] : 0.f;
+    }
+  // a whole tile in range (MODE 0 / 1, or split-K slabs): straight-line stores.  With the
+  // per-element guards below every store sat in its own branch and the wait counter (vmcnt
+  // counts stores on gfx9) was drained to 0 before each one.
+  if (MODE != 2 && m0 + TM <= g.M && n0 + TN <= g.Ncol) {
+#pragma unroll
+    for (int nb = 0; nb < NBN; ++nb) {
+      const int col = n0 + wn * WTN + nb * 16 + jj;
+      int64_t obase, ostride;
+      if (g.splits > 1) {
+        obase = (int64_t)blockIdx.z * g.M * g.Ncol + col;
+        ostride = g.Ncol;
+      } else if (MODE == 0) {
+        const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
+        obase = (int64_t)n * g.Cout * g.HoWo + pix;
+        ostride = g.HoWo;
+      } else {
+        const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
+        obase = (int64_t)n * g.Cin * g.HW + pix;
+        ostride = g.HW;
+      }
+      float* dst = g.splits > 1 ? ws : out;
+#pragma unroll
+      for (int mb = 0; mb < NBM; ++mb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wm * WTM + mb * 16 + 4 * kq + i;
+          dst[obase + (int64_t)m * ostride] = acc[mb][nb][i] + bbv[mb][i];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int nb = 0; nb < NBN; ++nb) {
     const int col = n0 + wn * WTN + nb * 16 + jj;
@@ -304,7 +345,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
           else
             out[obase + (int64_t)m * ostride] = v;
         } else {
-          if (MODE == 0 && bias) v += bias[m];
+          if (MODE == 0 && bias) v += bbv[mb][i];
           out[obase + (int64_t)m * ostride] = v;
         }
       }
