@@ -422,7 +422,7 @@ int launch_stream(const float* x, const float* k, float* out, int major, int in_
 // 10 / 8 rows for the 4-row strips) at ~half the registers.  The next input row's loads are
 // issued before the current row's arithmetic (one row of prefetch).
 //   out row oy reads input rows oy*DOWN - P0 + i, i < 4: input row t feeds tap i = t - oy*DOWN + P0.
-template <int DOWN, int P0, int SEGW, int NOC, bool TAIL>
+template <int DOWN, int P0, int SEGW, int NOC, bool TAIL, int RB = 0>
 __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ x,
                                                        const float* __restrict__ kern,
                                                        float* __restrict__ out, int in_h,
@@ -575,7 +575,37 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
   const int t1 = (oye - 1) * DOWN - P0 + 3;
   float cur[LV], nxt[LV], left[LV], right[LV];
   load_row(t0, cur);
-  if constexpr (DOWN == 1) {
+  if constexpr (DOWN == 1 && RB > 0) {
+    // RB = rows (compile time): the strip's output rows stay in registers and are stored
+    // after its last input row, so no row load is issued behind a store (gfx9 counts stores in
+    // vmcnt: waiting for such a load also waited for the store before it)
+    float ob[RB][NOCT];
+#pragma unroll
+    for (int it = 0; it < RB + 3; ++it) {
+      const int t = t0 + it;
+      if (t <= t1) {
+        if (t < t1) load_row(t + 1, nxt);
+        edges(t, cur, left, right);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hsum(3 - k, cur, left, right, acc[k]);
+      }
+      if (it >= 3) {
+#pragma unroll
+        for (int oc = 0; oc < NOCT; ++oc) ob[it >= 3 ? it - 3 : 0][oc] = acc[0][oc];
+      }
+#pragma unroll
+      for (int oc = 0; oc < NOCT; ++oc) {
+        acc[0][oc] = acc[1][oc];
+        acc[1][oc] = acc[2][oc];
+        acc[2][oc] = acc[3][oc];
+        acc[3][oc] = 0.f;
+      }
+#pragma unroll
+      for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) store(oyb + r, ob[r]);
+  } else if constexpr (DOWN == 1) {
     // acc[k] = output row t + P0 - 3 + k (tap 3 - k of input row t); after row t, acc[0] is
     // complete
     for (int t = t0; t <= t1; ++t) {
@@ -632,7 +662,7 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
   }
 }
 
-template <int DOWN, int P0, int SEGW, int NOC, bool TAIL = false>
+template <int DOWN, int P0, int SEGW, int NOC, bool TAIL = false, int RB = 0>
 int launch_roll(const float* x, const float* k, float* out, int major, int in_h, int in_w, int kh,
                 int kw, int out_h, int out_w, int rows, hipStream_t st) {
   const int strips_x = TAIL ? 1 : (int)bpk::ceil_div(out_w, SEGW * NOC);
@@ -641,7 +671,7 @@ int launch_roll(const float* x, const float* k, float* out, int major, int in_h,
   if (n <= 0) return BPK_OK;
   const int64_t blocks = bpk::ceil_div(n, 4 * (64 / SEGW));
   BPK_REQUIRE(blocks < (int64_t)INT32_MAX, "upfirdn2d: grid too large");
-  hipLaunchKernelGGL((upfirdn2d_roll<DOWN, P0, SEGW, NOC, TAIL>), dim3((unsigned)blocks), dim3(256),
+  hipLaunchKernelGGL((upfirdn2d_roll<DOWN, P0, SEGW, NOC, TAIL, RB>), dim3((unsigned)blocks), dim3(256),
                      0, st, x, k, out, in_h, in_w, kh, kw, out_h, out_w, rows, strips_x, strips_y, n);
   BPK_LAUNCH_CHECK("upfirdn2d_roll");
   return BPK_OK;
@@ -711,6 +741,18 @@ bool try_roll(const float* x, const float* k, float* out, int major, int in_h, i
 #undef BPK_ROLLT2
     }
     const int lanes4 = (out_w - 1) / 4;  // 2^k + 1 wide: four columns per lane + the tail
+    // output rows kept in registers and stored after the strip's last input row: [64,128,64,64]
+    // 0.559 -> 0.610 of the HBM peak (tools/gpu_r03_s18.sh, twice); BPK_UPFIRDN_FIR_RB=0: off
+    static const bool rb_env = !(getenv("BPK_UPFIRDN_FIR_RB") && getenv("BPK_UPFIRDN_FIR_RB")[0] == '0');
+    if (rb_env && rows == 5 && out_h % 5 == 0) {
+#define BPK_ROLLTB(SW) \
+  return (*rc = launch_roll<1, 2, SW, 4, true, 5>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+      if (lanes4 == 64) BPK_ROLLTB(64);
+      if (lanes4 == 32) BPK_ROLLTB(32);
+      if (lanes4 == 16) BPK_ROLLTB(16);
+      if (lanes4 == 8) BPK_ROLLTB(8);
+#undef BPK_ROLLTB
+    }
 #define BPK_ROLLT(SW) \
   return (*rc = launch_roll<1, 2, SW, 4, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
     if (lanes4 == 64) BPK_ROLLT(64);
