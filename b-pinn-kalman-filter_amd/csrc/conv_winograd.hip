@@ -1214,332 +1214,9 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   WINO_TS(5);
 }
 
-// Persistent form of the pipelined kernel (NB = 1: 4 waves x 16 couts = 64 couts, 32
-// tiles, two workgroups per CU).  The grid holds at most as many workgroups as fit on the
-// chip at once; workgroup l processes `ipw` consecutive work items of ONE image (an item =
-// one 8 x 16 pixel region x 64 output channels; the cout blocks of a region adjacent) as
-// ONE continuous chunk stream: the patch
-// loads, the patch stores, the V transform and the U loads of an item's first chunks run
-// inside the previous item's last chunks exactly as between the chunks of one item, so the
-// per-workgroup prologue (one memory latency + a transform) and the launch / drain of a
-// workgroup are paid once per workgroup instead of once per item.  The output transform
-// stores straight from registers (each lane owns 2 rows x 8 pixels of one channel per
-// M-block: two 16-B stores per row) so the V buffers stay live across the item boundary.
-// One image per workgroup: the GroupNorm prologue's (s, t) table is loaded to LDS once.
-struct WinoItem {
-  int n, oy0, ox0, cout0;
-};
-
-template <bool PRE>
-__global__ __launch_bounds__(256, 2) void wino_f23_persist_kernel(
-    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
-    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    float2* __restrict__ stats, WinoGeo g, int ipw, int wpi, int xcd_remap) {
-  constexpr int kPatch = kCK * kPR * kPCp;
-  constexpr int kVBuf = kCK * kM * kVS;
-  __shared__ float s_patch_raw[2][kPatch];                                   // 2 x 5.9 KB
-  __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];               // 2 x 20.5 KB
-  __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];  // PRE: (s, t) of every input channel
-
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int kq = lane >> 4, jj = lane & 15;
-  const int64_t G = gridDim.x;
-  int64_t l = blockIdx.x;
-  // workgroups on one XCD (blockIdx % 8 under round-robin placement) take consecutive
-  // logical indices: the same image, neighbouring regions
-  if (xcd_remap) l = (l % 8) * (G / 8) + l / 8;
-  const int n = __builtin_amdgcn_readfirstlane((int)(l / wpi));
-  const int first = __builtin_amdgcn_readfirstlane((int)(l % wpi) * ipw);
-  const int cnt = ipw;
-  const int nch = g.Cin / kCK;
-  const int64_t plane = (int64_t)g.H * g.W;
-
-  // item (within this workgroup's image) -> geometry, forced scalar
-  auto decode = [&](int i) {
-    const unsigned q = (unsigned)(first + min(i, cnt - 1));
-    const unsigned cbs = (unsigned)g.cout_blocks, rxs = (unsigned)g.regions_x;
-    const unsigned r0 = q / cbs;
-    WinoItem w;
-    w.n = n;
-    w.cout0 = __builtin_amdgcn_readfirstlane((int)(q - r0 * cbs) * 64);
-    w.ox0 = __builtin_amdgcn_readfirstlane((int)(r0 % rxs) * kOutCols);
-    w.oy0 = __builtin_amdgcn_readfirstlane((int)(r0 / rxs) * kOutRows);
-    return w;
-  };
-
-  f4 acc[16][2];
-#pragma unroll
-  for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
-
-  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
-
-  // ---- load cursor: the chunk whose patch is loaded next (item li, chunk lk)
-  constexpr int kPos = kPR * kPC;  // 180
-  const int pt = tid < kPos ? tid : 0;
-  const int ppy = pt / kPC, ppx = pt - ppy * kPC;
-  const int pdst = ppy * kPCp + ppx;
-  int li = 0, lk = 0;
-  WinoItem lit = decode(0);
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(x + (int64_t)n * g.Cin * plane), 0, (int)(g.Cin * plane * 4),
-      0x00020000);
-  int poff;
-  bool pin_cur;
-  auto set_load_item = [&]() {
-    const int iy = lit.oy0 - 1 + ppy, ix = lit.ox0 - 1 + ppx;
-    pin_cur = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-    const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
-    poff = (cy * g.W + cx) * 4;
-  };
-  set_load_item();
-  // loaded values and what the store needs of them: in-image bit and the chunk index
-  float pv[kCK];
-  bool pin_ld;
-  int k_ld = 0;
-  auto load_patch = [&]() {
-    const int k = li < cnt ? lk : nch - 1;  // past the end: re-load the last chunk
-    const int soff = k * kCK * (int)plane * 4;
-#pragma unroll
-    for (int c = 0; c < kCK; ++c)
-      pv[c] = __uint_as_float(
-          __builtin_amdgcn_raw_buffer_load_b32(xrs, poff, soff + c * (int)plane * 4, 0));
-    pin_ld = pin_cur;
-    k_ld = k;
-    if (li < cnt && ++lk == nch) {
-      lk = 0;
-      ++li;
-      lit = decode(li);
-      set_load_item();
-    }
-  };
-  auto store_patch_from = [&](const float* src, int kc, bool pin, float* sp) {
-#pragma unroll
-    for (int c = 0; c < kCK; ++c) {
-      float v = src[c];
-      if (PRE) {
-        const float2 st = s_ss[kc * kCK + c];
-        v = silu_f(v * st.x + st.y);
-      }
-      sp[pdst + c * (kPR * kPCp)] = pin ? v : 0.f;
-    }
-  };
-
-  // ---- U cursor: the chunk whose B operands are loaded next
-  int ui = 0, uk = 0;
-  int uoff;
-  auto set_u_item = [&]() {
-    const WinoItem w = decode(ui);
-    uoff = ((kq * g.Cout + w.cout0 + wave * 16 + jj) * 16) * 4;
-  };
-  set_u_item();
-  f4 uo[2][4];
-  auto u_soff = [&](int ks) {
-    const int k = ui < cnt ? uk : nch - 1;
-    return ((k * kCK + 4 * ks) * g.Cout) * 64;
-  };
-  auto load_u_half = [&](int ks, int q) {
-    using u4 = __attribute__((ext_vector_type(4))) unsigned;
-    const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, u_soff(ks), 0);
-    uo[ks][q] = __builtin_bit_cast(f4, w);
-  };
-  auto advance_u = [&]() {
-    if (ui < cnt && ++uk == nch) {
-      uk = 0;
-      ++ui;
-      set_u_item();
-    }
-  };
-
-  const int tc = tid >> 5, tm = tid & 31;
-  const int tty = tm / kTC, ttx = tm - tty * kTC;
-  float d[4][4];
-  auto read_d = [&](const float* sp) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) d[i][j] = sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j];
-  };
-  auto write_v = [&](float* sv) {
-    float t[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      t[0][j] = d[0][j] - d[2][j];
-      t[1][j] = d[1][j] + d[2][j];
-      t[2][j] = d[2][j] - d[1][j];
-      t[3][j] = d[1][j] - d[3][j];
-    }
-    f4* dst = reinterpret_cast<f4*>(&sv[(tc * kM + tm) * kVS]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
-  };
-
-  // ---- prologue: chunks 0-2, U(0) and the GroupNorm table issued before the first wait
-  float pv0[kCK], pv1[kCK];
-  int k0c, k1c;
-  bool pin0, pin1;
-  load_patch();
-#pragma unroll
-  for (int c = 0; c < kCK; ++c) pv0[c] = pv[c];
-  pin0 = pin_ld;
-  k0c = k_ld;
-  load_patch();
-#pragma unroll
-  for (int c = 0; c < kCK; ++c) pv1[c] = pv[c];
-  pin1 = pin_ld;
-  k1c = k_ld;
-  load_patch();
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) load_u_half(ks, q);
-  advance_u();
-  if (PRE) {
-    for (int c = tid; c < g.Cin; c += 256) s_ss[c] = pre[(int64_t)n * g.Cin + c];
-    __syncthreads();
-  }
-  store_patch_from(pv0, k0c, pin0, s_patch_raw[0]);
-  store_patch_from(pv1, k1c, pin1, s_patch_raw[1]);
-  __syncthreads();
-  read_d(s_patch_raw[0]);
-  write_v(s_v[0]);
-  __syncthreads();
-
-  f4 a[4];
-  auto a_src = [&](const float* sv, int grp) {
-    const int ks = grp >> 1, mb = grp & 1;
-    return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
-  };
-  {
-    const f4* src = a_src(s_v[0], 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a[q] = src[q];
-  }
-
-  // ---- epilogue of one item: output transform straight to global memory, one 16-B
-  // strip (2 tiles x 2 pixels of one row) at a time to keep few temporaries live
-  int ci = 0;  // compute cursor (item)
-  auto epilogue = [&]() {
-    const WinoItem w = decode(ci);
-    const int co = w.cout0 + wave * 16 + jj;
-    const float bv = bias ? bias[co] : 0.f;
-    const int64_t obase = ((int64_t)w.n * g.Cout + co) * plane;
-    // GroupNorm partial statistics of channel co over the region: this lane's 32 values
-    // (sum, then sum of squared deviations from the lane mean), merged over the 4 lanes
-    // jj + 16 kq with equal counts (symmetric butterfly: every lane gets the same bits)
-    float lm = 0.f, lm2 = 0.f, lcnt = 0.f;  // running (mean, M2, count) of this lane's values
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
-      // tiles m = 16 mb + 4 kq + rg: tile row 2 mb + kq / 2, tile cols 4 (kq & 1) + rg
-      const int oy = w.oy0 + 2 * (2 * mb + (kq >> 1));
-      const int ox = w.ox0 + 8 * (kq & 1);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {      // output row 2 ty + h
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {    // tiles rg = 2e, 2e + 1
-          f4 v;
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int rg = 2 * e + u;
-            float t[4];  // row h of A^T M, A^T = [[1,1,1,0],[0,1,-1,-1]]
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              t[j] = h == 0 ? acc[j][mb][rg] + acc[4 + j][mb][rg] + acc[8 + j][mb][rg]
-                            : acc[4 + j][mb][rg] - acc[8 + j][mb][rg] - acc[12 + j][mb][rg];
-            v[2 * u] = t[0] + t[1] + t[2] + bv;
-            v[2 * u + 1] = t[1] - t[2] - t[3] + bv;
-          }
-          const int64_t o = obase + (int64_t)(oy + h) * g.W + ox + 4 * e;
-          if (skip) {  // residual block tail, same operation order as bpk_residual_rescale_f32
-            const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) v[c] = (sk[c] + v[c]) / g.div;
-          }
-          *reinterpret_cast<f4*>(&y[o]) = v;
-          if (stats) {  // Chan merge of this 4-value strip into the running statistics
-            const float sm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
-            float sm2 = 0.f;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) sm2 = fmaf(v[c] - sm, v[c] - sm, sm2);
-            const float d = sm - lm, nt = lcnt + 4.f;
-            lm = lm + d * (4.f / nt);
-            lm2 = (lm2 + sm2) + d * d * (lcnt * 4.f / nt);
-            lcnt = nt;
-          }
-        }
-      }
-    }
-    if (stats) {
-      float m = lm, m2 = lm2;
-      merge_stats(m, m2, __shfl_xor(m, 16, 64), __shfl_xor(m2, 16, 64), 32.f);
-      merge_stats(m, m2, __shfl_xor(m, 32, 64), __shfl_xor(m2, 32, 64), 64.f);
-      if (kq == 0) {
-        const int R = g.regions_x * g.regions_y;
-        const int region = (w.oy0 / kOutRows) * g.regions_x + w.ox0 / kOutCols;
-        stats[((int64_t)w.n * g.Cout + co) * R + region] = make_float2(m, m2);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
-  };
-
-  auto step = [&](auto sb_c) {
-    constexpr int SB = decltype(sb_c)::value;
-    const float* sv = s_v[SB];
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp) {
-      const int ks = grp >> 1, mb = grp & 1;
-      __builtin_amdgcn_sched_barrier(0);
-      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);                          // patch(q+1)
-      if (grp == 1) write_v(s_v[SB ^ 1]);                                 // V(q+1)
-      if (grp == 2) store_patch_from(pv, k_ld, pin_ld, s_patch_raw[SB]);  // patch(q+2)
-      if (grp == 3) load_patch();                                         // patch(q+3)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp)
-          acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[q][pp], uo[ks][q][pp], acc[4 * q + pp][mb], 0, 0, 0);
-        if (grp < 3) a[q] = a_src(sv, grp + 1)[q];
-        if (mb == 1) load_u_half(ks, q);  // U(q+1)
-      }
-    }
-    advance_u();
-    __syncthreads();
-  };
-  auto read_a0 = [&](const float* sv) {
-    const f4* src = a_src(sv, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a[q] = src[q];
-  };
-  // nch is even (host check), so every item starts on LDS buffer 0
-  for (; ci < cnt; ++ci) {
-    for (int k = 0; k < nch; k += 2) {
-      step(std::integral_constant<int, 0>{});
-      read_a0(s_v[1]);
-      step(std::integral_constant<int, 1>{});
-      if (k + 2 < nch) read_a0(s_v[0]);
-    }
-    epilogue();  // before the next item's A reads, so those registers are free here
-    read_a0(s_v[0]);
-  }
-}
-
 }  // namespace
 
 static int cout_padded(int Cout) { return (Cout + 63) / 64 * 64; }
-
-// the software-pipelined kernel (=2: 128 couts per workgroup) unless BPK_WINO_PIPE=0
-static int wino_pipe_env() {
-  static const int v = [] {
-    const char* e = getenv("BPK_WINO_PIPE");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
 
 extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
   return (int64_t)16 * Cin * cout_padded(Cout) * (int64_t)sizeof(float);
@@ -1567,9 +1244,9 @@ extern "C" int bpk_conv3x3_wino_filter_ft_f32(const float* weight, float* U, int
 }
 
 extern "C" int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W) {
-  // Cout % 64 != 0 (multiples of 16): padded to 64 couts, software-pipelined kernel only
+  // Cout % 64 != 0 (multiples of 16): padded to 64 couts, software-pipelined kernel
   return N > 0 && Cin > 0 && Cin % kCK == 0 && Cout % 16 == 0 && H % kOutRows == 0 &&
-         W % kOutCols == 0 && (Cout % 64 == 0 || wino_pipe_env() != 0);
+         W % kOutCols == 0;
 }
 
 extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, const float* pre,
@@ -1583,83 +1260,23 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
   BPK_REQUIRE(bpk_conv3x3_wino_supported(N, Cin, Cout, H, W),
               "conv3x3_wino: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin %% 8, "
               "Cout %% 16, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
-  // NB = 1 (64 couts per workgroup, two workgroups per CU: 2-4 % faster on the NCSN++
-  // shapes than NB = 2) unless BPK_WINO_NB=2 asks for the one-workgroup-per-CU form
-  static const int nb_env = [] {
-    const char* e = getenv("BPK_WINO_NB");
-    return e ? atoi(e) : 1;
-  }();
-  const int pipe_env = wino_pipe_env();
   const int CoutP = cout_padded(Cout);
-  // BPK_WINO_PERSIST=1: the persistent form for the GroupNorm-prologue convs (=2: for every
-  // conv).  Opt-in: it removes the per-workgroup fixed cost (~2 chunks) but its main loop runs
-  // ~9 % slower, a net loss for Cin >= 256 (profiles/r01_conv_persist_sweep.txt).
-  static const int persist_env = [] {
-    const char* e = getenv("BPK_WINO_PERSIST");
-    return e ? atoi(e) : 0;
-  }();
-  if (pipe_env == 1 && (persist_env == 2 || (persist_env == 1 && pre)) && Cin % (2 * kCK) == 0 &&
-      !x2 && (!pre || Cin <= kPreMaxCin) && Cout == CoutP) {
-    WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div, Cin, Cout};
-    // as many workgroups as are resident at once (2 per CU), each on consecutive items of
-    // one image: ipw = items per workgroup divides the items of an image
-    static int slots = 0;
-    if (slots == 0) {
-      int dev = 0, cus = 0, occ = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wino_f23_persist_kernel<true>, 256, 0);
-      slots = std::max(8, cus * std::max(1, occ));
-    }
-    const int ipi = g.regions_x * g.regions_y * g.cout_blocks;
-    int ipw = 1;
-    while ((int64_t)N * (ipi / ipw) > slots && ipw < ipi) {
-      ++ipw;
-      while (ipi % ipw) ++ipw;
-    }
-    const int wpi = ipi / ipw;
-    const int64_t G = (int64_t)N * wpi;
-    BPK_REQUIRE(G < (1LL << 31), "conv3x3_wino: grid too large");
-    const int remap = (G % 8 == 0) ? 1 : 0;
-    const float2* pre2 = reinterpret_cast<const float2*>(pre);
-    hipStream_t st = bpk::as_stream(stream);
-    if (pre)
-      hipLaunchKernelGGL((wino_f23_persist_kernel<true>), dim3((unsigned)G), dim3(256), 0, st, x,
-                         U, bias, skip, pre2, y, stats2, g, ipw, wpi, remap);
-    else
-      hipLaunchKernelGGL((wino_f23_persist_kernel<false>), dim3((unsigned)G), dim3(256), 0, st, x,
-                         U, bias, skip, pre2, y, stats2, g, ipw, wpi, remap);
-    BPK_LAUNCH_CHECK("conv3x3_wino_persist");
-    return BPK_OK;
-  }
-  BPK_REQUIRE(!x2 || (pipe_env && (!pre || Cin <= kPreMaxCin)),
+  // Kernel choice (each form measured against the others on the NCSN++ / DDPM++ shapes;
+  // the rejected variants -- a persistent form, 128-cout NB = 2 blocks, the 4-wave residual
+  // tail -- are gone, numbers in DESIGN.md section 4):
+  //   * wino_f23_k16_kernel: CoutP % 128 == 0 and 16-cin chunks (every NCSN++ conv);
+  //   * wino_f23_pipe_kernel: the other shapes (8-wave / 128-cout form for the GroupNorm
+  //     prologue convs without a residual tail, 4 waves / 64 couts otherwise);
+  //   * wino_f23_kernel: a GroupNorm prologue over more than kPreMaxCin input channels.
+  const bool pipe_ok = !pre || Cin <= kPreMaxCin;
+  BPK_REQUIRE(!x2 || pipe_ok,
               "conv3x3_wino: a second input source needs the pipelined kernel");
-  BPK_REQUIRE(Cout == CoutP || (pipe_env && (!pre || Cin <= kPreMaxCin)),
+  BPK_REQUIRE(Cout == CoutP || pipe_ok,
               "conv3x3_wino: Cout %% 64 != 0 needs the pipelined kernel (Cin <= %d with pre)",
               kPreMaxCin);
-  if (pipe_env && (!pre || Cin <= kPreMaxCin)) {
-    // software-pipelined kernel; BPK_WINO_PIPE=2 selects 128 couts per workgroup
-    const int pnb = (pipe_env == 2 && Cout % 128 == 0) ? 2 : 1;
-    // the 8-wave, 128-cout workgroup form (CoutP % 128 == 0) for the GroupNorm-prologue convs
-    // without a residual tail: +2-3 % on those NCSN++ shapes, while the residual-tail form
-    // loses 1-3 % (its epilogue reads skip with no co-resident workgroup to cover it;
-    // profiles/r02_wino_w8.txt).  BPK_WINO_W8=0: never, 2: every pipelined launch, 3: every
-    // launch without a residual tail.
-    static const int w8_env = [] {
-      const char* e = getenv("BPK_WINO_W8");
-      return e ? atoi(e) : 1;
-    }();
-    const bool w8_case = w8_env == 2 || (w8_env == 1 && pre && !skip) || (w8_env == 3 && !skip);
-    const int wg = (w8_case && pnb == 1 && CoutP % 128 == 0) ? 8 : 4;
-    // the 16-cin chunk form of the 8-wave kernel (BPK_WINO_K16: 0 off, 1 = where the 8-wave
-    // form runs, 2 = every launch it supports, the default: the weighted NCSN++ PRE-conv mix
-    // 0.705 (8-cin forms) -> 0.716 (K16=1) -> 0.720 (K16=2) of the f32 MFMA peak, one box)
-    static const int k16_env = [] {
-      const char* e = getenv("BPK_WINO_K16");
-      return e ? atoi(e) : 2;
-    }();
-    const bool k16 = k16_env && pnb == 1 && CoutP % 128 == 0 && Cin % 16 == 0 && C1 % 16 == 0 &&
-                     (k16_env == 2 || wg == 8);
+  if (pipe_ok) {
+    const int wg = (pre && !skip && CoutP % 128 == 0) ? 8 : 4;
+    const bool k16 = CoutP % 128 == 0 && Cin % 16 == 0 && C1 % 16 == 0;
     if (k16) {
       WinoGeo gk{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / 128, div, C1, Cout};
       const int64_t items = (int64_t)N * gk.regions_x * gk.regions_y * gk.cout_blocks;
@@ -1677,7 +1294,7 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
       BPK_LAUNCH_CHECK("conv3x3_wino_k16");
       return BPK_OK;
     }
-    WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * pnb * wg / 4), div,
+    WinoGeo g{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / (64 * wg / 4), div,
               C1, Cout};
     const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
     BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
@@ -1687,14 +1304,9 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
 #define WINO_PIPE(NB_, PRE_, TAIL_)                                                           \
   hipLaunchKernelGGL((wino_f23_pipe_kernel<NB_, PRE_, 4, TAIL_>), dim3((unsigned)blocks), dim3(256), 0, st, \
                      x, U, bias, skip, pre2, y, stats2, g, remap, x2)
-    // BPK_WINO_TAIL=0: no peeled tail chunks (A/B)
-    static const int tail_env = [] {
-      const char* e = getenv("BPK_WINO_TAIL");
-      return e ? atoi(e) : 1;
-    }();
     const int nch = Cin / kCK;
-    // (GroupNorm-prologue form only: the plain form spills with it)
-    const bool tail = tail_env && pre && nch % 2 == 0 && nch >= 4;
+    // peeled tail chunks (GroupNorm-prologue form only: the plain form spills with them)
+    const bool tail = pre && nch % 2 == 0 && nch >= 4;
 #define WINO_PIPE8(PRE_, TAIL_)                                                                 \
   hipLaunchKernelGGL((wino_f23_pipe_kernel<1, PRE_, 8, TAIL_>), dim3((unsigned)blocks), dim3(512), \
                      0, st, x, U, bias, skip, pre2, y, stats2, g, remap, x2)
@@ -1704,8 +1316,6 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
       } else {
         WINO_PIPE8(false, false);
       }
-    } else if (pnb == 2) {
-      if (pre) WINO_PIPE(2, true, false); else WINO_PIPE(2, false, false);
     } else if (tail) {
       WINO_PIPE(1, true, true);
     } else {
@@ -1716,8 +1326,7 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
     BPK_LAUNCH_CHECK("conv3x3_wino_pipe");
     return BPK_OK;
   }
-  const int nb = (Cout % 128 == 0 && nb_env == 2) ? 2 : 1;
-  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / (64 * nb), div, Cin, Cout};
+  WinoGeo g{N, Cin, Cout, H, W, W / kOutCols, H / kOutRows, Cout / 64, div, Cin, Cout};
   const int64_t blocks = (int64_t)N * g.regions_x * g.regions_y * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -1726,19 +1335,15 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
 #define WINO_LAUNCH(NB_, PRE_)                                                                 \
   hipLaunchKernelGGL((wino_f23_kernel<NB_, PRE_>), dim3((unsigned)blocks), dim3(256), 0, st, x, \
                      U, bias, skip, pre2, y, stats2, g, remap)
-  if (nb == 2) {
-    if (pre) WINO_LAUNCH(2, true); else WINO_LAUNCH(2, false);
-  } else {
-    if (pre) WINO_LAUNCH(1, true); else WINO_LAUNCH(1, false);
-  }
+  if (pre) WINO_LAUNCH(1, true); else WINO_LAUNCH(1, false);
 #undef WINO_LAUNCH
   BPK_LAUNCH_CHECK("conv3x3_wino");
   return BPK_OK;
 }
 
 extern "C" int bpk_conv3x3_wino_up2_supported(int N, int Cin, int Cout, int H, int W) {
-  return bpk_conv3x3_wino_supported(N, Cin, Cout, H, W) && wino_pipe_env() != 0 &&
-         Cin % 16 == 0 && cout_padded(Cout) % 128 == 0;
+  return bpk_conv3x3_wino_supported(N, Cin, Cout, H, W) && Cin % 16 == 0 &&
+         cout_padded(Cout) % 128 == 0;
 }
 
 // y = conv3x3(nearest_x2(x)) + bias for x [N, Cin, H/2, W/2], y [N, Cout, H, W]: the 16-cin

@@ -32,10 +32,7 @@ constexpr int kCB = 32;              // cin per workgroup
 constexpr int kOB = 64;              // cout per workgroup
 constexpr int kT = 8;                // tiles per K-chunk (1 tile row x 8 tile cols)
 constexpr int kXR = 4, kXC = 18;     // input patch rows / cols
-constexpr int kXCp = kXC + 1;
 constexpr int kRec = 20;             // LDS stride of one 16-position record
-constexpr int kXPer = kCB * kXR * kXC / 256;  // 9 patch elements per thread
-constexpr int kGPer = kOB * kT / 256;         // 2 gradient tiles per thread
 
 struct WgradGeo {
   int N, Cin, Cout, H, W;
@@ -44,161 +41,9 @@ struct WgradGeo {
   int64_t chunks;          // N * strips_y * strips_x
 };
 
-__global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restrict__ x,
-                                                            const float* __restrict__ gy,
-                                                            float* __restrict__ part, WgradGeo g,
-                                                            int xcd_remap) {
-  __shared__ float s_x[kCB * kXR * kXCp];                            //  9.7 KB
-  __shared__ __attribute__((aligned(16))) float s_v[kT * kCB * kRec];  // 20.5 KB
-  __shared__ __attribute__((aligned(16))) float s_g[kT * kOB * kRec];  // 41.0 KB
-
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int kq = lane >> 4, jj = lane & 15;
-  int64_t nblk = (int64_t)gridDim.x;
-  int64_t b = blockIdx.x;
-  if (xcd_remap) b = (b % 8) * (nblk / 8) + b / 8;
-  // logical order: split outermost, so the cin / cout blocks of one K-range (which read
-  // the same x / dy strips) are consecutive and share one XCD's L2
-  const int ob = (int)(b % g.cout_blocks);
-  const int cbk = (int)((b / g.cout_blocks) % g.cin_blocks);
-  const int split = (int)(b / ((int64_t)g.cout_blocks * g.cin_blocks));
-  const int cin0 = cbk * kCB, cout0 = ob * kOB;
-  const int64_t k_begin = g.chunks * split / g.splits;
-  const int64_t k_end = g.chunks * (split + 1) / g.splits;
-
-  const int64_t plane = (int64_t)g.H * g.W;
-  f4 acc[16][2];
-#pragma unroll
-  for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
-
-  float xv[kXPer];
-  unsigned xmask = 0;
-  float2 gv[kGPer][2];
-  auto load_chunk = [&](int64_t ck) {
-    const int sx = (int)(ck % g.strips_x);
-    const int64_t r = ck / g.strips_x;
-    const int sy = (int)(r % g.strips_y);
-    const int n = (int)(r / g.strips_y);
-    const int oy0 = 2 * sy, ox0 = 16 * sx;
-    const float* xn = x + ((int64_t)n * g.Cin + cin0) * plane;
-    xmask = 0;
-#pragma unroll
-    for (int e = 0; e < kXPer; ++e) {
-      const int i = tid + 256 * e;
-      const int c = i / (kXR * kXC);
-      const int rr = i - c * (kXR * kXC);
-      const int py = rr / kXC, px = rr - py * kXC;
-      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
-      const bool inb = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-      const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
-      xv[e] = xn[(int64_t)c * plane + cy * g.W + cx];
-      xmask |= inb ? (1u << e) : 0u;
-    }
-    const float* gn = gy + ((int64_t)n * g.Cout + cout0) * plane + (int64_t)oy0 * g.W + ox0;
-#pragma unroll
-    for (int e = 0; e < kGPer; ++e) {
-      const int id = tid + 256 * e;
-      const int co = id >> 3, tx = id & 7;
-      const float* src = gn + (int64_t)co * plane + 2 * tx;
-      gv[e][0] = *reinterpret_cast<const float2*>(src);
-      gv[e][1] = *reinterpret_cast<const float2*>(src + g.W);
-    }
-  };
-
-  if (k_begin < k_end) load_chunk(k_begin);
-  for (int64_t ck = k_begin; ck < k_end; ++ck) {
-    // 1. patch -> LDS; Gbar = A dY A^T (A = [[1,0],[1,1],[1,-1],[0,-1]]) -> LDS records
-#pragma unroll
-    for (int e = 0; e < kXPer; ++e) {
-      const int i = tid + 256 * e;
-      const int c = i / (kXR * kXC);
-      const int rr = i - c * (kXR * kXC);
-      const int py = rr / kXC, px = rr - py * kXC;
-      s_x[(c * kXR + py) * kXCp + px] = ((xmask >> e) & 1u) ? xv[e] : 0.f;
-    }
-#pragma unroll
-    for (int e = 0; e < kGPer; ++e) {
-      const int id = tid + 256 * e;
-      const int co = id >> 3, tx = id & 7;
-      const float a = gv[e][0].x, bb = gv[e][0].y, c = gv[e][1].x, d = gv[e][1].y;
-      const float rows[4][2] = {{a, bb}, {a + c, bb + d}, {a - c, bb - d}, {-c, -d}};
-      f4* dst = reinterpret_cast<f4*>(&s_g[(tx * kOB + co) * kRec]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = rows[i][0], q = rows[i][1];
-        dst[i] = f4{p, p + q, p - q, -q};
-      }
-    }
-    __syncthreads();
-    // 2. V = B^T d B for one (cin, tile) per thread
-    {
-      const int c = tid >> 3, tx = tid & 7;
-      float d[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[i][j] = s_x[(c * kXR + i) * kXCp + 2 * tx + j];
-      float t[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        t[0][j] = d[0][j] - d[2][j];
-        t[1][j] = d[1][j] + d[2][j];
-        t[2][j] = d[2][j] - d[1][j];
-        t[3][j] = d[1][j] - d[3][j];
-      }
-      f4* dst = reinterpret_cast<f4*>(&s_v[(tx * kCB + c) * kRec]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
-    }
-    __syncthreads();
-    // 3. next chunk in flight during the MFMAs (the last chunk re-loads itself: the same
-    //    loads every iteration keep the compiler's vmcnt bookkeeping exact)
-    load_chunk(min(ck + 1, k_end - 1));
-    // 4. acc[p][mb] += V_p[tile][cin] * Gbar_p[tile][cout] over the chunk's 8 tiles
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int tile = 4 * ks + kq;
-      f4 bq[4], a0[4], a1[4];
-      const f4* bs = reinterpret_cast<const f4*>(&s_g[(tile * kOB + 16 * wave + jj) * kRec]);
-      const f4* as0 = reinterpret_cast<const f4*>(&s_v[(tile * kCB + jj) * kRec]);
-      const f4* as1 = reinterpret_cast<const f4*>(&s_v[(tile * kCB + 16 + jj) * kRec]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bq[q] = bs[q];
-        a0[q] = as0[q];
-        a1[q] = as1[q];
-      }
-#pragma unroll
-      for (int p = 0; p < 16; ++p) {
-        acc[p][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[p >> 2][p & 3], bq[p >> 2][p & 3],
-                                                         acc[p][0], 0, 0, 0);
-        acc[p][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[p >> 2][p & 3], bq[p >> 2][p & 3],
-                                                         acc[p][1], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-
-  // partial dU: acc[p][mb][r] = dU_p[cin0 + 16mb + 4kq + r][cout0 + 16 wave + jj]
-  const int co = cout0 + 16 * wave + jj;
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ci = cin0 + 16 * mb + 4 * kq + r;
-      f4* dst = reinterpret_cast<f4*>(part + (((int64_t)split * g.Cin + ci) * g.Cout + co) * 16);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = f4{acc[4 * q][mb][r], acc[4 * q + 1][mb][r], acc[4 * q + 2][mb][r],
-                    acc[4 * q + 3][mb][r]};
-    }
-}
-
-// Software-pipelined weight gradient (default).  Same decomposition as wino_wgrad_kernel
-// (workgroup = 32 cin x 64 cout over a K-range of 8-tile chunks), reorganized like the
-// forward pipe kernel:
+// Software-pipelined weight gradient (workgroup = 32 cin x 64 cout over a K-range of 8-tile
+// chunks; round 1's unpipelined form of the same decomposition was 1.3x slower and is gone),
+// organized like the forward pipe kernel:
 //   * the B operands (Gbar = A dY A^T, one (tile, cout) record per lane and k-step) are
 //     built in registers by the lane that consumes them, from a 2 x 2 gradient tile it
 //     loads itself (two 8-byte loads), one chunk ahead -- no LDS traffic for the gradient;
@@ -568,19 +413,9 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino_wgrad: grid too large");
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
-  // the software-pipelined kernel unless BPK_WGRAD_PIPE=0
-  static const int pipe_env = [] {
-    const char* e = getenv("BPK_WGRAD_PIPE");
-    return e ? atoi(e) : 1;
-  }();
   float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
-  BPK_REQUIRE(pipe_env || !db, "conv3x3_wino_wgrad: the bias gradient needs the pipelined kernel");
-  if (pipe_env)
-    hipLaunchKernelGGL(wino_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
-                       workspace, part_b, g, remap);
-  else
-    hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
-                       workspace, g, remap);
+  hipLaunchKernelGGL(wino_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
+                     workspace, part_b, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
   BPK_REQUIRE(bpk::ceil_div(pairs, 16) < (1LL << 31), "conv3x3_wino_wgrad: too many pairs");

@@ -277,15 +277,9 @@ __global__ __launch_bounds__(256) void gs_grad2(
   }
 }
 
-// channel slices per block: S x the threads of one-per-location where C allows
-// (BPK_GS_SLICES=1: one thread per location, the A/B baseline)
-inline int slices_for(int C) {
-  static const bool one = [] {
-    const char* e = getenv("BPK_GS_SLICES");
-    return e && e[0] == '1';
-  }();
-  return one ? 1 : (C >= 16 ? 8 : (C >= 4 ? 4 : 1));
-}
+// channel slices per block: S x the threads of one-per-location where C allows (one thread
+// per location took 186 us vs ~25 us per call on the PINN shapes, round 2)
+inline int slices_for(int C) { return C >= 16 ? 8 : (C >= 4 ? 4 : 1); }
 
 unsigned blocks_for(int64_t total) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(bpk::ceil_div(total, 256), 256 * 32));

@@ -627,6 +627,8 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
   } else {
     // rows in pairs: row t = oy*2 - P0 + 2 (taps 2 of oy, 0 of oy + 1) and t + 1 (taps 3, 1);
     // acc[0] = output oy, acc[1] = oy + 1.  Prologue: rows t0, t0 + 1 (taps 0, 1 of oyb).
+    // RB > 0 (= rows, out_h % RB == 0): the strip's output rows stay in registers and are
+    // stored after its last input row, as in the FIR form above.
     load_row(t0 + 1, nxt);
     edges(t0, cur, left, right);
     hsum(0, cur, left, right, acc[0]);
@@ -638,6 +640,34 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
     hsum(1, cur, left, right, acc[0]);
 #pragma unroll
     for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+    if constexpr (RB > 0) {
+      float ob[RB][NOCT];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        t = (oyb + r) * 2 - P0 + 2;  // cur holds row t
+        load_row(t + 1, nxt);
+        edges(t, cur, left, right);
+        hsum(2, cur, left, right, acc[0]);
+        hsum(0, cur, left, right, acc[1]);
+#pragma unroll
+        for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+        if (r + 1 < RB) load_row(t + 2, nxt);
+        edges(t + 1, cur, left, right);
+        hsum(3, cur, left, right, acc[0]);
+        hsum(1, cur, left, right, acc[1]);
+#pragma unroll
+        for (int oc = 0; oc < NOCT; ++oc) {
+          ob[r][oc] = acc[0][oc];
+          acc[0][oc] = acc[1][oc];
+          acc[1][oc] = 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) store(oyb + r, ob[r]);
+      return;
+    }
     for (int oy = oyb; oy < oye; ++oy) {
       t = oy * 2 - P0 + 2;  // cur holds row t
       load_row(t + 1, nxt);
@@ -677,29 +707,19 @@ int launch_roll(const float* x, const float* k, float* out, int major, int in_h,
   return BPK_OK;
 }
 
-// Strip height of the rolling kernel.  BPK_UPFIRDN_ROLL: 0 = off (the 4-row upfirdn2d_stream
-// strips), N > 0 = N rows everywhere; unset = automatic: down2 -> about 32 k waves
-// (tools/gpu_upfirdn_roll.sh on MI355X: [64,128,128,128] best at 8 rows, [64,256,64,64] at 4,
-// i.e. 32 k waves both), the odd-width 1:1 FIR -> the divisor of the height in 5..8 (65 = 13 x 5;
-// 5 and 6 rows: 0.59 of HBM vs 0.45 for the 4-row stream strips).
-int roll_env() {
-  static const int r = [] {
-    const char* e = getenv("BPK_UPFIRDN_ROLL");
-    return e ? atoi(e) : -1;
-  }();
+// Strip height of the rolling kernel: down2 -> about 32 k waves (tools/gpu_upfirdn_roll.sh on
+// MI355X: [64,128,128,128] best at 8 rows, [64,256,64,64] at 4, i.e. 32 k waves both), as a
+// power of two (2..16) so the strip's rows can be held in registers (RB); the odd-width 1:1 FIR
+// -> the divisor of the height in 5..8 (65 = 13 x 5; 5 and 6 rows: 0.59 of HBM vs 0.45 for the
+// 4-row stream strips).
+int roll_rows_down2(int major, int out_h, int strips_x, int segs) {
+  const double per = (double)major * out_h * strips_x / (32768.0 * segs);
+  int r = 2;
+  while (r < 16 && 2 * r <= per * 1.4142) r *= 2;
   return r;
 }
 
-int roll_rows_down2(int major, int out_h, int strips_x, int segs) {
-  const int r = roll_env();
-  if (r >= 0) return r;
-  const double per = (double)major * out_h * strips_x / (32768.0 * segs);
-  return std::max(3, std::min(64, (int)(per + 0.5)));
-}
-
 int roll_rows_fir(int out_h) {
-  const int r = roll_env();
-  if (r >= 0) return r;
   for (int c = 5; c <= 8; ++c)
     if (out_h % c == 0) return c;
   return 6;
@@ -707,14 +727,25 @@ int roll_rows_fir(int out_h) {
 
 bool try_roll(const float* x, const float* k, float* out, int major, int in_h, int in_w, int kh,
               int kw, int down, int p0, int out_h, int out_w, hipStream_t st, int* rc) {
-  if (roll_env() == 0) return false;
   const bool a16 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && in_w % 4 == 0;
   if (down == 2 && a16 && (p0 == 1 || p0 == 2)) {
     const int lanes = (int)bpk::ceil_div(out_w, 2);  // two output columns per lane
     const int sw = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
     const int rows = roll_rows_down2(major, out_h, (int)bpk::ceil_div(out_w, 2 * sw), 64 / sw);
-#define BPK_ROLL2(P, SW) \
-  return (*rc = launch_roll<2, P, SW, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+    // rows held in registers and stored after the strip's last input row when they tile the
+    // plane (every power-of-two plane; [64,128,128,128] and [64,256,64,64] both)
+#define BPK_ROLL2R(P, SW, RB) \
+  return (*rc = launch_roll<2, P, SW, 2, false, RB>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
+#define BPK_ROLL2(P, SW)                         \
+  do {                                           \
+    if (out_h % rows == 0) {                     \
+      if (rows == 2) BPK_ROLL2R(P, SW, 2);       \
+      if (rows == 4) BPK_ROLL2R(P, SW, 4);       \
+      if (rows == 8) BPK_ROLL2R(P, SW, 8);       \
+      if (rows == 16) BPK_ROLL2R(P, SW, 16);     \
+    }                                            \
+    BPK_ROLL2R(P, SW, 0);                        \
+  } while (0)
     if (p0 == 1) {
       if (sw == 8) BPK_ROLL2(1, 8);
       if (sw == 16) BPK_ROLL2(1, 16);
@@ -725,26 +756,15 @@ bool try_roll(const float* x, const float* k, float* out, int major, int in_h, i
     if (sw == 16) BPK_ROLL2(2, 16);
     if (sw == 32) BPK_ROLL2(2, 32);
     BPK_ROLL2(2, 64);
+#undef BPK_ROLL2R
 #undef BPK_ROLL2
   }
   if (down == 1 && p0 == 2 && (out_w & 1) && kw == 4 && a16) {
     const int rows = roll_rows_fir(out_h);
-    static const bool noc2 = getenv("BPK_UPFIRDN_FIR_NOC2") != nullptr;
-    if (noc2) {  // two columns per lane + the tail (8-byte loads / stores)
-      const int lanes2 = (out_w - 1) / 2;
-#define BPK_ROLLT2(SW) \
-  return (*rc = launch_roll<1, 2, SW, 2, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
-      if (lanes2 == 64) BPK_ROLLT2(64);
-      if (lanes2 == 32) BPK_ROLLT2(32);
-      if (lanes2 == 16) BPK_ROLLT2(16);
-      if (lanes2 == 8) BPK_ROLLT2(8);
-#undef BPK_ROLLT2
-    }
     const int lanes4 = (out_w - 1) / 4;  // 2^k + 1 wide: four columns per lane + the tail
     // output rows kept in registers and stored after the strip's last input row: [64,128,64,64]
-    // 0.559 -> 0.610 of the HBM peak (tools/gpu_r03_s18.sh, twice); BPK_UPFIRDN_FIR_RB=0: off
-    static const bool rb_env = !(getenv("BPK_UPFIRDN_FIR_RB") && getenv("BPK_UPFIRDN_FIR_RB")[0] == '0');
-    if (rb_env && rows == 5 && out_h % 5 == 0) {
+    // 0.559 -> 0.610 of the HBM peak (round 3, one box, twice)
+    if (rows == 5 && out_h % 5 == 0) {
 #define BPK_ROLLTB(SW) \
   return (*rc = launch_roll<1, 2, SW, 4, true, 5>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
       if (lanes4 == 64) BPK_ROLLTB(64);
@@ -768,8 +788,6 @@ bool try_roll(const float* x, const float* k, float* out, int major, int in_h, i
 bool try_stream(const float* x, const float* k, float* out, int major, int in_h, int in_w,
                 int kh, int kw, int up, int down, int p0, int out_h, int out_w, hipStream_t st,
                 int* rc) {
-  static const char* mode = getenv("BPK_UPFIRDN_PATH");
-  if (mode && mode[0] == 't') return false;  // BPK_UPFIRDN_PATH=tiled forces the LDS kernel
   if (kh > 4 || kw > 4 || (reinterpret_cast<uintptr_t>(x) & 7) ||
       (reinterpret_cast<uintptr_t>(out) & 7))
     return false;
@@ -780,18 +798,8 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
   if (up == 1 && try_roll(x, k, out, major, in_h, in_w, kh, kw, down, p0, out_h, out_w, st, rc))
     return true;
   if (up == 1 && down == 2) {
-    // two output columns per lane (16-byte input loads) where rows allow it; BPK_UPFIRDN_NOC1=1
-    // keeps one column per lane (8-byte loads) everywhere
-    static const bool noc1 = getenv("BPK_UPFIRDN_NOC1") != nullptr;
-    static const int r2 = [] {
-      const char* e = getenv("BPK_UPFIRDN_R2");
-      return e ? atoi(e) : 4;
-    }();
-    if (!noc1 && in_w % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-      if (r2 == 8) {
-        if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 8, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
-        if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 8, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
-      }
+    // two output columns per lane (16-byte input loads) where rows allow it
+    if (in_w % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
       if (p0 == 1) return (*rc = launch_stream<1, 2, 1, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
       if (p0 == 2) return (*rc = launch_stream<1, 2, 2, 4, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
     }
@@ -802,37 +810,23 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
     if (p0 == 2 && (out_w & 1) && kw == 4) {
       // odd width 2^k + 1 (the FIR pad(2, 2) of conv_downsample_2d): a segment of
       // (out_w - 1) / 2 lanes with the tail column on its last lane
+      // (reached only when the rolling kernel above does not apply: a misaligned input).
+      // 4-row strips with 4 columns per lane (16-byte row loads), else 8 rows with 2 columns
+      // per lane; round 1 on [64,128,64,64] -> 65^2: 39.8 % / 32.6 % of the HBM peak
       const int lanes = (out_w - 1) / 2;
-      static const int rt = [] {
-        const char* e = getenv("BPK_UPFIRDN_RT");
-        return e ? atoi(e) : 4;
-      }();
-      // BPK_UPFIRDN_RT: 4 (default) / 8 = strip height with 4 columns per lane (16-byte row
-      // loads); 2 = 8 rows with 2 columns per lane.  [64,128,64,64] -> 65^2 on MI355X:
-      // 0.086 / 0.088 / 0.105 ms (39.8 / 38.8 / 32.6 % of HBM peak); before the tail path a
-      // half-idle 64-lane segment took 0.135 ms (25 %)
 #define BPK_TAIL2(SW) \
   return (*rc = launch_stream_seg<1, 1, 2, 8, SW, 0, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true)
 #define BPK_TAIL4(SW, RR) \
   return (*rc = launch_stream_seg<1, 1, 2, RR, SW, 4, true>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true)
       const int lanes4 = (out_w - 1) / 4;
-      if (rt == 2) {
-        if (lanes == 64) BPK_TAIL2(64);
-        if (lanes == 32) BPK_TAIL2(32);
-        if (lanes == 16) BPK_TAIL2(16);
-        if (lanes == 8) BPK_TAIL2(8);
-      } else if ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && in_w % 4 == 0) {
-        if (rt == 4) {
-          if (lanes4 == 64) BPK_TAIL4(64, 4);
-          if (lanes4 == 32) BPK_TAIL4(32, 4);
-          if (lanes4 == 16) BPK_TAIL4(16, 4);
-          if (lanes4 == 8) BPK_TAIL4(8, 4);
-        }
-        if (lanes4 == 64) BPK_TAIL4(64, 8);
-        if (lanes4 == 32) BPK_TAIL4(32, 8);
-        if (lanes4 == 16) BPK_TAIL4(16, 8);
-        if (lanes4 == 8) BPK_TAIL4(8, 8);
+      if ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && in_w % 4 == 0) {
+        if (lanes4 == 64) BPK_TAIL4(64, 4);
+        if (lanes4 == 32) BPK_TAIL4(32, 4);
+        if (lanes4 == 16) BPK_TAIL4(16, 4);
+        if (lanes4 == 8) BPK_TAIL4(8, 4);
       }
+      if (lanes == 64) BPK_TAIL2(64);
+      if (lanes == 32) BPK_TAIL2(32);
       if (lanes == 16) BPK_TAIL2(16);  // 33-wide
       if (lanes == 8) BPK_TAIL2(8);    // 17-wide
 #undef BPK_TAIL2
@@ -842,10 +836,8 @@ bool try_stream(const float* x, const float* k, float* out, int major, int in_h,
     if (p0 == 2) return BPK_STREAM(1, 1, 2, 8);
   }
   if (up == 2 && down == 1 && p0 == 2) {
-    // four output columns per lane (8-byte input loads, 16-byte stores) when rows allow it;
-    // BPK_UPFIRDN_UP2=1 keeps two
-    static const bool up2 = getenv("BPK_UPFIRDN_UP2") != nullptr;
-    if (!up2 && out_w % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0)
+    // four output columns per lane (8-byte input loads, 16-byte stores) when rows allow it
+    if (out_w % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0)
       return (*rc = launch_stream<2, 1, 2, 16, 4>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, st), true);
     return BPK_STREAM(2, 1, 2, 16);
   }

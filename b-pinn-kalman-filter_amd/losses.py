@@ -16,7 +16,6 @@ The PINN step functions live in pinn_kalman/.
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -26,7 +25,7 @@ from models import utils as mutils
 from sde_lib import VESDE, VPSDE
 
 
-_ADAM_FUSED = os.environ.get("BPK_ADAM_FUSED", "1") != "0"
+_ADAM_FUSED = True
 
 
 def get_optimizer(config, params, lr_mul=1.0, is_bpinn=False):

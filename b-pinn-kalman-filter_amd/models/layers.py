@@ -7,7 +7,6 @@ the fused HIP ops of `op.norm_act` (GroupNorm + bias + SiLU, residual rescale).
 from __future__ import annotations
 
 import math
-import os
 
 import numpy as np
 import torch
@@ -101,13 +100,13 @@ def ddpm_conv1x1(in_planes, out_planes, stride=1, bias=True, init_scale=1., padd
     return conv
 
 
-_WINO_ENABLED = os.environ.get("BPK_CONV", "winograd") != "miopen"
-_IN_FUSED = os.environ.get("BPK_IN_FUSED", "1") != "0"
-# GroupNorm partial statistics from the producing conv's epilogue (BPK_GN_STATS=0: off)
-_GN_STATS = os.environ.get("BPK_GN_STATS", "1") != "0"
-_GEMM1X1 = os.environ.get("BPK_GEMM1X1", "1") != "0"  # 1x1 convs on the MFMA GEMM kernels
-# ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs (BPK_DDPM_FUSED=0: off)
-_DDPM_FUSED = os.environ.get("BPK_DDPM_FUSED", "1") != "0"
+# Fusion switches: module constants (each measured against the unfused form, DESIGN.md
+# section 4); tests flip them to compare against the unfused composition.
+_WINO_ENABLED = True  # 3x3 convs on the Winograd kernels (False: MIOpen)
+_IN_FUSED = True      # InstanceNorm+ELU (+ backward, double backward) as one kernel each
+_GN_STATS = True      # GroupNorm partial statistics from the producing conv's epilogue
+_GEMM1X1 = True       # 1x1 convs on the MFMA GEMM kernels
+_DDPM_FUSED = True    # ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs
 
 
 def _is_3x3(x, conv: nn.Conv2d):
@@ -303,7 +302,7 @@ class Upsample(nn.Module):
         B, C, H, W = x.shape
         if (self.with_conv and _WINO_ENABLED and x.is_cuda
                 and conv_op.up2_supported(x, self.Conv_0.weight)):
-            # the upsample read inside the Winograd conv's patch load (BPK_WINO_UP2=0: off)
+            # the upsample read inside the Winograd conv's patch load
             return conv_op.conv3x3_up2(x, self.Conv_0.weight, self.Conv_0.bias)
         h = F.interpolate(x, (H * 2, W * 2), mode="nearest")
         return self.Conv_0(h) if self.with_conv else h

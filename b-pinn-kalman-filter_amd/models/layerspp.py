@@ -12,7 +12,6 @@ Per block the arithmetic is re-scheduled for the GPU:
 from __future__ import annotations
 
 import math
-import os
 
 import numpy as np
 import torch
@@ -23,11 +22,10 @@ from op.norm_act import residual_rescale
 
 from . import layers, up_or_down_sampling
 
-# attention at inference: q, k, v as one GEMM over the stacked NIN weights (BPK_ATTN_QKV=0: off)
-_ATTN_QKV = os.environ.get("BPK_ATTN_QKV", "1") != "0"
-# ... and softmax(q^T k) v as one fused kernel (csrc/attention.hip; BPK_ATTN_FUSED=0: bmm +
-# softmax + bmm)
-_ATTN_FUSED = os.environ.get("BPK_ATTN_FUSED", "1") != "0"
+# attention at inference: q, k, v as one GEMM over the stacked NIN weights
+_ATTN_QKV = True
+# ... and softmax(q^T k) v as one fused kernel (csrc/attention.hip; False: bmm + softmax + bmm)
+_ATTN_FUSED = True
 
 conv1x1 = layers.ddpm_conv1x1
 conv3x3 = layers.ddpm_conv3x3

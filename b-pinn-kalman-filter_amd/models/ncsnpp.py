@@ -10,7 +10,6 @@ hipGraph.
 from __future__ import annotations
 
 import functools
-import os
 
 import numpy as np
 import torch
@@ -20,10 +19,10 @@ from op.norm_act import residual_rescale
 
 from . import layers, layerspp, utils
 
-# up-path skip concatenations read as two sources at inference (BPK_PAIR=0: torch.cat)
-_PAIR = os.environ.get("BPK_PAIR", "1") != "0"
-# all residual blocks' time-embedding projections as one GEMM at inference (BPK_TEMB_BANK=0: off)
-_TEMB_BANK = os.environ.get("BPK_TEMB_BANK", "1") != "0"
+# up-path skip concatenations read as two sources at inference (False: torch.cat)
+_PAIR = True
+# all residual blocks' time-embedding projections as one GEMM at inference
+_TEMB_BANK = True
 conv3x3 = layerspp.conv3x3
 default_initializer = layers.default_init
 _SQRT2 = np.sqrt(2.)

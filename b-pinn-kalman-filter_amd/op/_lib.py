@@ -128,7 +128,7 @@ def exported_symbols() -> list:
     return sorted(parse_header().keys())
 
 
-_PRUNE = os.environ.get("BPK_GRAD_PRUNE", "1") != "0"
+_PRUNE = True
 
 
 def mark_inputs(ctx, *args):

@@ -191,8 +191,7 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=Fa
     return y
 
 
-_WGRAD = os.environ.get("BPK_WINO_WGRAD", "1") != "0"
-_WGRAD_PIPE = os.environ.get("BPK_WGRAD_PIPE", "1") != "0"  # the kernel with the bias gradient
+_WGRAD = True  # 3x3 weight gradients on the Winograd kernel (False: MIOpen / igemm)
 
 
 def wgrad_supported(x, weight):
@@ -358,7 +357,8 @@ def conv2d_weight_igemm_raw(x, wshape, gy, stride=1, padding=0, bias_grad=False)
 # eager call of each (op, shapes) times both once and caches the faster; under graph
 # capture an unseen call takes the implicit-GEMM kernel.  BPK_IGEMM=2: always igemm.
 _IG_MODE = os.environ.get("BPK_IGEMM", "1")
-_CHOICE: dict = {}
+_CHOICE: dict = {}        # agreed choices (broadcast from rank 0 under torch.distributed)
+_CHOICE_LOCAL: dict = {}  # choices made inside local_choices(): this rank's own, never agreed
 
 
 def _time_us(fn, reps=3):
@@ -375,8 +375,8 @@ def _time_us(fn, reps=3):
 # Small images (H * W <= 32 x 32, the PINN pyramids' lower levels, CIFAR's 8^2 / 4^2): the
 # Winograd kernels' per-workgroup set-up is a large share of a short launch, so 3x3 convs
 # there are timed against the implicit-GEMM kernel once per distinct call and the faster
-# kept (BPK_CONV3_SELECT=0: Winograd whenever it fits).
-_SEL3 = os.environ.get("BPK_CONV3_SELECT", "1") != "0"
+# kept.
+_SEL3 = True
 _SEL3_MAX_HW = 32 * 32
 
 
@@ -452,12 +452,18 @@ def _agree(c: int) -> int:
 
 def _decide(key, timers):
     """Index of the candidate to run for `key`: cached, from the table, or timed once
-    (None under graph capture for a key never decided eagerly)."""
+    (None under graph capture for a key never decided eagerly).  A choice made inside
+    `local_choices()` is kept apart from the agreed ones, so a later SPMD call of the same key
+    still goes through the broadcast on every rank (otherwise rank 0 would skip it and the
+    other ranks would wait in it)."""
+    local = _LOCAL_ONLY[0]
     c = _CHOICE.get(key)
+    if c is None and local:
+        c = _CHOICE_LOCAL.get(key)
     if c is not None:
         return c
     ks = _key_str(key)
-    if ks in _TABLE:
+    if ks in _TABLE and 0 <= _TABLE[ks] < len(timers):
         c = _TABLE[ks]
     elif _PICK_FIRST:
         c = 0
@@ -467,11 +473,11 @@ def _decide(key, timers):
         with torch.no_grad():
             ts = [_time_us(f) for f in timers]
         c = _agree(min(range(len(timers)), key=ts.__getitem__))
-        if _TABLE_PATH:
-            _TABLE[ks] = c
+        if _TABLE_PATH and not local:  # a table entry written by another candidate list
+            _TABLE[ks] = c             # (out of range above) is overwritten here
             if _rank() == 0:  # one writer (every rank holds the same, agreed choices)
                 _save_table()
-    _CHOICE[key] = c
+    (_CHOICE_LOCAL if local else _CHOICE)[key] = c
     return c
 
 
@@ -556,17 +562,15 @@ def _wgrad_impl(x, gy, wshape, want_b):
     """(dw, db or None) without autograd: the Winograd weight gradient (+ bias) when the
     shape qualifies, MIOpen backward-weights otherwise."""
     if wgrad_supported(x, tuple(wshape)):
-        if (_small_img(x) and _WGRAD_PIPE and x.is_cuda and x.dtype == torch.float32
+        if (_small_img(x) and x.is_cuda and x.dtype == torch.float32
                 and igemm_supported(x, tuple(wshape), 1, 1)):
             key = ("w3", tuple(x.shape), tuple(wshape))
             dw, db = _pick_any(key, [
                 lambda: conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True),
                 lambda: conv2d_weight_igemm_raw(x, tuple(wshape), gy, 1, 1, True)])
             return dw, (db if want_b else None)
-        if _WGRAD_PIPE:
-            dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
-            return dw, (db if want_b else None)
-        dw = conv3x3_wgrad_raw(x, gy, wshape)
+        dw, db = conv3x3_wgrad_raw(x, gy, wshape, bias_grad=True)
+        return dw, (db if want_b else None)
     elif igemm_supported(x, tuple(wshape), 1, 1):
         return conv2d_weight_select(x, tuple(wshape), gy, 1, 1, want_b)
     else:
@@ -595,7 +599,7 @@ def _fwd_ft_impl(x, w):
     return _fwd_impl(x, _flip_t(w))
 
 
-_FT = os.environ.get("BPK_CONV_FT", "1") != "0"  # 0: explicit flipped weight copies
+_FT = True  # the filter transform reads the weight flipped / transposed (False: a copy)
 
 
 def _conv_ft_any(x, w):
@@ -760,7 +764,7 @@ def up2_supported(x, weight):
     return bool(lib.bpk_conv3x3_wino_up2_supported(N, C, weight.shape[0], 2 * H, 2 * W))
 
 
-_WINO_UP2 = os.environ.get("BPK_WINO_UP2", "1") != "0"
+_WINO_UP2 = True
 
 
 def _up2_raw(x, weight, bias):

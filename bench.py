@@ -3,12 +3,17 @@
 BASELINE.json metric "PC-sampler score-net evals/s + train steps/s, NCSN++ 128^2 @1/2/4/8
 MI355X", workload configs[2] (SURVEY.md 8d cfg #3): NCSN++ hyper-parameters of
 configs/vp/cifar10_ncsnpp_continuous.py at 128x128x1, continuous VP-SDE N = 1000,
-Euler-Maruyama predictor + Langevin corrector (snr 0.075, 1 corrector step), batch 64 per
-GPU (weak scaling).  A "step" = one PC step over the batch = 2 score-net evaluations per
+Euler-Maruyama predictor + Langevin corrector (snr 0.075, 1 corrector step), global batch
+64 sharded 64/N per GPU (strong scaling: BASELINE configs[2] "batch=64, 1->8 GPUs", SURVEY
+8(e) "64 -> 8/GPU"; the reference's nn.DataParallel scatters one global batch,
+models/utils.py:93).  A "step" = one PC step over the batch = 2 score-net evaluations per
 sample (corrector + predictor), fused update kernels, the whole step replayed from a
 hipGraph.  Synthetic data: prior noise + random-init weights (no checkpoints offline).
+The other phases shard their own config's global batch the same way (DSM train 64, PINN 64,
+DPS 16, nc_ddpmpp 64, CIFAR 128); the ns_step simulator runs independent replicas (256 per
+GPU).  `--weak` (or an explicit per-GPU `--batch`) gives every rank the whole batch.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch 64] [--weak]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  value = score-net evals/s of the whole job.
@@ -47,7 +52,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=64,
+                    help="configs[2] global batch, sharded global/N per GPU (strong scaling)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: every rank runs the whole global batch of every phase")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="explicit per-GPU batch of the sampler / DSM / PINN / nc_ddpmpp phases "
+                         "(weak scaling; e.g. --batch 8 at N=1 is the per-rank work of N=8)")
     ap.add_argument("--train-steps", type=int, default=6)
     ap.add_argument("--train-warmup", type=int, default=2)
     ap.add_argument("--no-train", action="store_true")
@@ -76,6 +87,23 @@ def parse():
                          "the same fp32 Winograd kernels for the forward and avoids minutes of "
                          "backward-conv searches")
     return ap.parse_args()
+
+
+def shard(args, world, global_b, explicit=True):
+    """Per-rank batch of a phase whose config fixes the global batch `global_b`: global/N
+    (strong scaling), the whole batch per rank with --weak, or the explicit
+    per-GPU --batch for the phases that take it."""
+    if explicit and args.batch is not None:
+        return args.batch
+    if args.weak:
+        return global_b
+    if global_b % world:
+        raise SystemExit(f"[bench] global batch {global_b} does not shard over {world} ranks")
+    return global_b // world
+
+
+def scaling_mode(args):
+    return "weak" if (args.weak or args.batch is not None) else "strong"
 
 
 def build_model(dev, seed=0):
@@ -616,7 +644,7 @@ def bench_ncddpmpp(args, ctx, dev):
     with torch.no_grad():
         for prm in model.parameters():
             prm.add_(torch.randn_like(prm) * 0.01)
-    B = args.batch
+    B = shard(args, ctx.world_size, args.global_batch)
     sde = sde_lib.VPSDE(c.model.beta_min, c.model.beta_max, c.model.num_scales)
     eng = sampling.PCEngine(sde, (B, 1, 128, 128), sampling.AncestralSamplingPredictor,
                             sampling.NoneCorrector, c.sampling.snr, 1, continuous=False,
@@ -634,7 +662,8 @@ def bench_ncddpmpp(args, ctx, dev):
             "ncddpmpp_ms_per_step": round(dt / args.ncddpmpp_steps * 1e3, 2),
             "ncddpmpp_tflops": round(B * ctx.world_size * args.ncddpmpp_steps * 300.53e9 / dt / 1e12, 2),
             "ncddpmpp_config": "configs[2] literal: nc_ddpmpp (ddpm, 300.53 GFLOP/eval) 128x128x1, "
-                               "ancestral + none, discrete, B=64/GPU"}
+                               f"ancestral + none, discrete, global batch {B * ctx.world_size}, "
+                               f"{B}/GPU"}
 
 
 def pinn_batch(c, B, dev, seed=0):
@@ -680,7 +709,7 @@ def bench_cifar_train(args, ctx, dev):
     state = dict(optimizer=opt, model=tmodel, ema=ema, step=0)
     step_fn = losses.get_step_fn(sde, train=True, optimize_fn=losses.optimization_manager(c),
                                  reduce_mean=True, continuous=True)
-    B = c.training.batch_size
+    B = shard(args, ctx.world_size, c.training.batch_size, explicit=False)
     batch = torch.rand(B, 3, 32, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(ctx.rank))
     for _ in range(2):
         step_fn(state, batch)
@@ -699,10 +728,12 @@ def bench_cifar_train(args, ctx, dev):
             "cifar_train_ms_per_step": round(dt / args.cifar_steps * 1e3, 2),
             "cifar_train_global_batch": B * ctx.world_size,
             "cifar_train_loss": round(float(loss.item()), 5),
-            "cifar_config": "configs[1]: cifar10_ncsnpp_continuous 32x32x3, batch 128/GPU",
+            "cifar_config": f"configs[1]: cifar10_ncsnpp_continuous 32x32x3, global batch "
+                            f"{B * ctx.world_size}, {B}/GPU",
             "roofline_cifar_train": step_roofline(
                 tally, args.cifar_steps / dt, "configs[1] DSM train step, NCSN++ CIFAR-10 32x32x3 "
-                "B=128/GPU", survey_direct=8.36e12, traffic_key="step cifar")}
+                f"B={B}/GPU", survey_direct=8.36e12 * B / 128,
+                traffic_key="step cifar" if B == 128 else None)}
 
 
 def _pinn_run(args, ctx, dev):
@@ -722,7 +753,8 @@ def _pinn_run(args, ctx, dev):
     step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
                                       ctx=ctx)
     operator = get_operator(c)
-    batch = pinn_batch(c, args.batch, dev, seed=ctx.rank)
+    B = shard(args, ctx.world_size, c.training.batch_size)
+    batch = pinn_batch(c, B, dev, seed=ctx.rank)
     for _ in range(args.pinn_warmup):
         step_fn(state, operator, batch)
     tally, _ = counted(lambda: step_fn(state, operator, batch), dev)
@@ -736,28 +768,29 @@ def _pinn_run(args, ctx, dev):
     ctx.barrier()
     torch.cuda.synchronize(dev)
     dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
-    return dt, (loss, pinn_loss, data_loss), tally
+    return dt, (loss, pinn_loss, data_loss), tally, B
 
 
 def bench_pinn(args, ctx, dev):
     """configs[3]: one PINN train step (get_pinn_step_fn: FlowNet + PressureNet forward,
     equation_mse with create_graph first derivatives and second derivatives -- correlation,
     grid_sample grad2 and the InstanceNorm+ELU double backward on HIP --, backward, two
-    Adams, EMA) at pinn_pde, batch 64/GPU, 64x64; gradients averaged over ranks with RCCL.
+    Adams, EMA) at pinn_pde, global batch 64 sharded over the ranks, 64x64; gradients averaged
+    over ranks with RCCL.
     Eager (the hipGraph replay of this step was withdrawn)."""
-    dt, losses_, tally = _pinn_run(args, ctx, dev)
+    dt, losses_, tally, B = _pinn_run(args, ctx, dev)
     roof = None
     if tally is not None:
         roof = step_roofline(tally, args.pinn_steps / dt, "configs[3] PINN train step (FlowNet + "
                              "PressureNet fwd, equation_mse 1st/2nd derivatives, backward, 2x Adam, "
-                             "EMA), B=64/GPU 64x64; latency-bound: ~10k launches per step",
+                             f"EMA), B={B}/GPU 64x64; latency-bound: ~10k launches per step",
                              traffic_key="step pinn")
         roof["bound_note"] = ("mfma is the nominal bound; the step is launch/latency-bound (small "
                               "images, ~10k kernels), so frac is low by construction")
     return {"roofline_pinn": roof, "pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
             "pinn_ms_per_step": round(dt / args.pinn_steps * 1e3, 2),
             "pinn_mode": "eager",
-            "pinn_global_batch": args.batch * ctx.world_size,
+            "pinn_global_batch": B * ctx.world_size,
             "pinn_losses": [round(float(v.item()), 6) for v in losses_],
             "pinn_config": "configs[3]: pinn_pde (FlowNet 2.49M + PressureNet 7.54M), 64x64"}
 
@@ -777,7 +810,7 @@ def bench_dps(args, ctx, dev):
     from models import utils as mutils
     c = nc_ddpmpp.get_config()
     c.data.image_size = 256
-    c.training.batch_size = 16
+    c.training.batch_size = shard(args, ctx.world_size, 16, explicit=False)
     c.device = dev
     c.inverse = ConfigDict(dict(operator="inpaint", invert=False, ratio=0.5, sampler="dps",
                                 variance=0.1, solver="RK45", max_steps=args.dps_steps))
@@ -815,12 +848,13 @@ def bench_dps(args, ctx, dev):
     return {"dps_nfe_per_s": round(nfe / dt, 3), "dps_sample_nfe_per_s": round(nfe * B * ctx.world_size / dt, 2),
             "dps_nfe_timed": nfe, "dps_global_batch": B * ctx.world_size,
             "dps_finite": bool(torch.isfinite(x).all().item()),
-            "dps_config": "configs[4]: nc_ddpmpp_inpaint_dps @256x256 (ddpm net), B=16/GPU, RK45",
+            "dps_config": f"configs[4]: nc_ddpmpp_inpaint_dps @256x256 (ddpm net), global batch "
+                          f"{B * ctx.world_size}, {B}/GPU, RK45",
             "roofline_dps": step_roofline(tally, nfe / dt, "configs[4] DPS function evaluation "
-                                          "(ddpm 256x256 forward + input gradient through the net, "
-                                          "B=16/GPU)", unit_of_work="nfe",
+                                          f"(ddpm 256x256 forward + input gradient through the net, "
+                                          f"B={B}/GPU)", unit_of_work="nfe",
                                           survey_direct=2 * 1198.88e9 * B,
-                                          traffic_key="step dps")}
+                                          traffic_key="step dps" if B == 16 else None)}
 
 
 _PHASE = ["start"]
@@ -892,6 +926,8 @@ def _plumbing(args, ctx):
         torch.distributed.all_reduce(t)
     if ctx.rank == 0:
         print(json.dumps({"metric": "plumbing", "value": float(t.item()), "n_gpus": ctx.world_size,
+                          "per_gpu_batch": shard(args, ctx.world_size, args.global_batch),
+                          "scaling": scaling_mode(args),
                           "backend": torch.distributed.get_backend() if ctx.world_size > 1 else None}),
               flush=True)
     if ctx.world_size > 1:
@@ -920,7 +956,7 @@ def main():
     dev = torch.device("cuda", ctx.local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     world = ctx.world_size
-    B = args.batch
+    B = shard(args, world, args.global_batch)
     c, model = build_model(dev)
     model.eval()
 
@@ -997,9 +1033,9 @@ def main():
                  "train_tflops_direct_basis": round(args.train_steps * B * world * NCSNPP_GFLOP_PER_TRAIN_SAMPLE
                                                     / tdt / 1e3, 2),
                  "roofline_train": step_roofline(
-                     tally, args.train_steps / tdt, "configs[2] DSM train step, NCSN++ 128x128x1 B=64/GPU "
-                     "(fwd + bwd-data + wgrad + clip + Adam + EMA)", survey_direct=63.9e12,
-                     traffic_key="step train")}
+                     tally, args.train_steps / tdt, f"configs[2] DSM train step, NCSN++ 128x128x1 B={B}/GPU "
+                     "(fwd + bwd-data + wgrad + clip + Adam + EMA)", survey_direct=63.9e12 * B / 64,
+                     traffic_key="step train" if B == 64 else None)}
 
     cifar = None
     if args.cifar_steps > 0 and not args.no_train:
@@ -1033,17 +1069,20 @@ def main():
             log("upfirdn2d rooflines")
             from op.conv import local_choices
             with local_choices():
-                up_roof = upfirdn_rooflines(dev, B)
+                up_roof = upfirdn_rooflines(dev, 64)  # the 8(d) shapes, whatever the sharding
         model_tflops = evals_per_s * NCSNPP_GFLOP_PER_EVAL / 1e3
         result = {
             "metric": "PC-sampler score-net evals/s (NCSN++ 128x128x1, EM + Langevin)",
             "value": round(evals_per_s, 3), "unit": "score-net evals/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling_mode(args), "vs_baseline": None,
+            "dtype": "f32",
             "data": "synthetic (prior noise, random-init weights)",
             "config": {"workload": "configs[2]: NCSN++ 128x128x1 PC sampler, VP-SDE N=1000, "
-                                   "euler_maruyama + langevin (snr 0.075), batch 64/GPU",
+                                   f"euler_maruyama + langevin (snr 0.075), global batch {B * world} "
+                                   f"= {B}/GPU x {world}",
                        "model": "ncsnpp (62.69M params)", "global_batch": B * world,
+                       "per_gpu_batch": B,
                        "seq_len": None, "parallelism": f"dp{world} (batch-sharded, RCCL)",
                        "hip_graph": eng.graph is not None,
                        "dist_backend": torch.distributed.get_backend() if world > 1 else None,

@@ -28,6 +28,20 @@ def test_gpus_2_spawns_two_ranks_and_relays_one_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["backend"] == "gloo"
     assert d["value"] == 3.0  # all-reduce of rank ids + 1 over both ranks
+    # configs[2] strong scaling by default: global batch 64 sharded 32 per rank
+    assert d["per_gpu_batch"] == 32 and d["scaling"] == "strong"
+
+
+def test_weak_flag_keeps_the_whole_batch_per_rank():
+    rc, out, err = _run(["--gpus", "2", "--plumbing", "--weak"])
+    assert rc == 0, err[-2000:]
+    d = json.loads(out.strip().splitlines()[-1])
+    assert d["per_gpu_batch"] == 64 and d["scaling"] == "weak"
+
+
+def test_global_batch_must_shard_evenly():
+    rc, out, err = _run(["--gpus", "2", "--plumbing", "--global-batch", "7"])
+    assert rc != 0 and "does not shard" in err
 
 
 def test_gpus_1_runs_in_process():

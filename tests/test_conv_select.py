@@ -103,3 +103,65 @@ def test_local_choices_skip_the_broadcast(monkeypatch):
         pass
     else:
         raise AssertionError("the broadcast should run outside local_choices()")
+
+
+def test_out_of_range_table_entry_is_retimed(tmp_path, monkeypatch):
+    """A table written by a build with a longer candidate list: the entry is ignored, the
+    candidates are timed and the entry is overwritten (no IndexError, no silent igemm)."""
+    from op import conv
+    key = ("fwd", (1, 4, 8, 8), (4, 4, 3, 3), (1, 1), (1, 1), False)
+    path = tmp_path / "t.json"
+    path.write_text(json.dumps({conv._key_str(key): 5}))
+    monkeypatch.setattr(conv, "_TABLE_PATH", str(path))
+    monkeypatch.setattr(conv, "_TABLE", conv._load_table())
+    monkeypatch.setattr(conv, "_CHOICE", {})
+    monkeypatch.setattr(conv, "_PICK_FIRST", False)
+    monkeypatch.setattr(conv.torch.cuda, "is_current_stream_capturing", lambda: False)
+    times = iter([4.0, 1.0])
+    monkeypatch.setattr(conv, "_time_us", lambda f: next(times))
+    assert conv._decide(key, [None, None]) == 1
+    assert json.loads(path.read_text()) == {conv._key_str(key): 1}
+
+
+def _local_then_spmd_worker(rank, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE="2", LOCAL_RANK=str(rank))
+        sys.path[:0] = [os.path.join(HERE, "..", "b-pinn-kalman-filter_amd"), os.path.join(HERE, "..")]
+        import torch.distributed as dist
+        from op import conv
+        dist.init_process_group("gloo")
+        conv._TABLE_PATH = None
+        conv._PICK_FIRST = False
+        conv.torch.cuda.is_current_stream_capturing = lambda: False
+        key = ("fwd", "shared")
+        if rank == 0:  # a rank-0-only phase (bench.py's roofline) decides the key first
+            times = iter([1.0, 3.0, 3.0, 1.0])  # local: candidate 0; SPMD: candidate 1
+            conv._time_us = lambda f: next(times)
+            with conv.local_choices():
+                assert conv._decide(key, [None, None]) == 0
+        else:
+            times = iter([1.0, 3.0])
+            conv._time_us = lambda f: next(times)
+        # every rank reaches the key: the broadcast must run on both (else rank 1 hangs)
+        c = conv._decide(key, [None, None])
+        q.put((rank, c, None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_local_choice_does_not_short_circuit_a_later_spmd_call():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35000 + os.getpid() % 2000
+    ps = [ctx.Process(target=_local_then_spmd_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in ps), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[2] is None, r[2]
+    assert [r[1] for r in res] == [1, 1]  # rank 0's SPMD timing, agreed

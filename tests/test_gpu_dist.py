@@ -295,26 +295,26 @@ def test_rccl_all_reduce_captures_in_a_hip_graph():
 
 def test_bench_gpus_2_matches_world_1_samples():
     """`python bench.py --gpus 2` (gloo, both ranks on the one device) launches two ranks,
-    reports n_gpus 2 and produces the samples of the single-rank run (Philox noise keyed by
-    the global sample index; the Langevin batch-mean norm summed over ranks)."""
+    shards the global batch (strong scaling, the configs[2] form: --global-batch 8 -> 4 per
+    rank), reports n_gpus 2 and produces the samples of the single-rank run (Philox noise
+    keyed by the global sample index; the Langevin batch-mean norm summed over ranks)."""
     import json
     import subprocess
     bench = os.path.join(HERE, "..", "bench.py")
-    common = ["--steps", "3", "--warmup", "1", "--batch", "8", "--no-train", "--no-pinn",
+    common = ["--steps", "3", "--warmup", "1", "--global-batch", "8", "--no-train", "--no-pinn",
               "--no-dps", "--ns-steps", "0", "--ncddpmpp-steps", "0", "--no-cpu-baseline",
               "--no-roofline", "--sample-sums"]
     out = {}
-    for n, b in ((1, "8"), (2, "4")):
+    for n in (1, 2):
         env = dict(os.environ, BPK_DIST_BACKEND="gloo")
         env.pop("WORLD_SIZE", None)
-        args = list(common)
-        args[args.index("--batch") + 1] = b   # per-rank batch: global 8 either way
-        p = subprocess.run([sys.executable, bench, "--gpus", str(n)] + args, env=env,
+        p = subprocess.run([sys.executable, bench, "--gpus", str(n)] + common, env=env,
                            capture_output=True, text=True, timeout=400)
         assert p.returncode == 0, p.stderr[-3000:]
         out[n] = json.loads(p.stdout.strip().splitlines()[-1])
     assert out[1]["n_gpus"] == 1 and out[2]["n_gpus"] == 2
-    assert out[2]["config"]["global_batch"] == 8
+    assert out[2]["scaling"] == "strong"
+    assert out[2]["config"]["global_batch"] == 8 and out[2]["config"]["per_gpu_batch"] == 4
     a, b = np.array(out[1]["sample_sums"]), np.array(out[2]["sample_sums"])
     assert a.shape == b.shape == (8,)
     np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-3 * np.abs(a).max())

@@ -51,6 +51,24 @@ def test_upfirdn2d_ncsnpp_modes_vs_oracle(hip, shape, up, down, pad, gain):
     np.testing.assert_allclose(y, ref, rtol=0, atol=2e-6)
 
 
+@pytest.mark.parametrize("shape", [(64, 128, 128, 128), (64, 256, 64, 64), (24, 512, 128, 128),
+                                   (2, 8, 38, 64), (5, 3, 64, 256)])
+def test_upfirdn2d_down2_row_rolling_strips(hip, shape):
+    """down2 pad(1,1) on the row-rolling kernel at every strip form it takes: strips of 8, 4 and
+    16 output rows held in registers (the 8(d) shapes and a bigger one), a height the strip does
+    not divide (per-row stores) and a 64-lane segment; vs the same FIR as a stride-2 conv on the
+    flipped taps (F.conv2d, fp32)."""
+    from op import upfirdn2d
+    g = torch.Generator(device=hip).manual_seed(sum(shape))
+    x = torch.randn(*shape, device=hip, generator=g)
+    k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32, device=hip)
+    y = upfirdn2d(x, k, down=2, pad=(1, 1))
+    N, C, H, W = shape
+    ref = F.conv2d(x.view(N * C, 1, H, W), k.flip(0, 1)[None, None], stride=2, padding=1)
+    assert y.shape == (N, C, H // 2, W // 2)
+    assert (y - ref.view_as(y)).abs().max().item() <= 2e-6
+
+
 def test_upfirdn2d_second_order_gradcheck_f64(hip):
     from op import upfirdn2d
     k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, device=hip)
@@ -473,10 +491,10 @@ def test_conv3x3_small_channel_groupnorm_prologue_and_skip(hip):
         assert (tail - (skip + ref) / 2.0).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
-def test_conv3x3_winograd_persistent_many_items(hip):
-    """The persistent Winograd kernel streams several work items per workgroup (more items
-    than resident workgroups, uneven split): GroupNorm prologue + residual tail at that size
-    vs the unfused composition in float64 (1e-5 relative)."""
+def test_conv3x3_winograd_many_items_odd_batch(hip):
+    """More work items than resident workgroups on an odd batch and non-power-of-two plane
+    (11 x 6 x 5 regions, the XCD remap off): GroupNorm prologue + residual tail vs the
+    unfused composition in float64 (1e-5 relative)."""
     from op.conv import conv3x3
     from op.norm_act import group_norm_affine
     g = torch.Generator().manual_seed(11)
@@ -1153,18 +1171,27 @@ def test_fused_attention_matches_fp32_reference(hip, B, C, P, scale):
     assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
-def test_attention_block_fused_equals_bmm_path(hip, monkeypatch):
-    """AttnBlockpp at inference with the fused attention kernel vs the same block on the
-    bmm + softmax + bmm path (1e-5 relative)."""
+@pytest.mark.parametrize("block", ["AttnBlockpp", "AttnBlock"])
+def test_attention_block_fused_equals_bmm_path(hip, monkeypatch, block):
+    """AttnBlockpp (NCSN++) and AttnBlock (the ddpm net of nc_ddpmpp / DPS, routed through the
+    same stacked q/k/v GEMM) at inference with the fused attention kernel vs the same block on
+    the bmm + softmax + bmm path (1e-5 relative); the fused kernel must actually run."""
+    import models.layers as lay
     import models.layerspp as lpp
+    from op import attention as attn_op
     g = torch.Generator().manual_seed(5)
-    blk = lpp.AttnBlockpp(256, skip_rescale=True, init_scale=0.1).to(hip).eval()
+    blk = (lpp.AttnBlockpp(256, skip_rescale=True, init_scale=0.1) if block == "AttnBlockpp"
+           else lay.AttnBlock(256)).to(hip).eval()
     with torch.no_grad():
         for p in blk.parameters():
             p.add_(torch.randn(p.shape, generator=g).to(hip) * 0.05)
     x = torch.randn(4, 256, 16, 16, generator=g).to(hip)
+    calls = []
+    real = attn_op.attention
+    monkeypatch.setattr(attn_op, "attention", lambda *a, **k: calls.append(1) or real(*a, **k))
     with torch.no_grad():
         fused = blk(x)
+        assert calls, "the fused attention kernel did not run"
         monkeypatch.setattr(lpp, "_ATTN_FUSED", False)
         ref = blk(x)
     assert (fused - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
