@@ -97,6 +97,9 @@ struct WinoGeo {
   int CoutS;  // couts stored (y, skip, stats channel count); Cout = CoutS rounded up to 64
   int up;     // 16-cin kernel only: 1 = x is [N, Cin, H/2, W/2], convolved as its nearest x2
               // upsample (the ddpm net's Upsample + Conv_0, reference layers.py:576-590)
+  int ksplit; // 16-cin kernel only: > 1 = split-K over the input channels; workgroup s of a tile
+              // contracts chunks [s, s + 1) * nch / ksplit and writes its raw partial output to
+              // y + s * N * CoutS * H * W (no bias / tail / statistics: wino_splitk_reduce_kernel)
 };
 
 constexpr int kVS = 20;                  // LDS stride of one (cin, tile) V record (16 + pad)
@@ -958,7 +961,10 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   unsigned cb, rx, ry;
   unsigned r = udivmod(b, (unsigned)g.cout_blocks, cb);
   r = udivmod(r, (unsigned)g.regions_x, rx);
-  const int n = (int)udivmod(r, (unsigned)g.regions_y, ry);
+  r = udivmod(r, (unsigned)g.regions_y, ry);
+  unsigned nn;
+  const int ks_idx = (int)udivmod(r, (unsigned)g.N, nn);  // split-K slice (0 unless ksplit > 1)
+  const int n = (int)nn;
   const int oy0 = (int)ry * kOutRows, ox0 = (int)rx * kOutCols;
   const int cout_w = (int)cb * 128 + wave * 16;
   const int ph = __builtin_amdgcn_readfirstlane(tid >> 8);  // channels 8 ph .. 8 ph + 7
@@ -971,7 +977,8 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   const float* xn = x + (int64_t)n * g.C1 * xplane;
   const float2* pre_n = PRE ? pre + (int64_t)n * g.Cin : nullptr;
   const int kq = lane >> 4, jj = lane & 15;
-  const int nch = g.Cin / CK;
+  const int nch = g.Cin / CK / max(g.ksplit, 1);  // chunks of this workgroup
+  const int kb = ks_idx * nch;                    // its first chunk
 
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(xn), 0, (int)(g.C1 * xplane * 4), 0x00020000);
@@ -996,7 +1003,7 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   }
   float pv[8];
   auto load_patch_part = [&](float* dst, int k, int c0, int cn) {
-    const int cc = min(k, nch - 1) * CK;
+    const int cc = (kb + min(k, nch - 1)) * CK;
     const bool second = cc >= g.C1;
     const int soff = ((second ? cc - g.C1 : cc) + ph * 8) * (int)xplane * 4;
 #pragma unroll
@@ -1005,7 +1012,7 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
           second ? xrs2 : xrs, poff, soff + c * (int)xplane * 4, 0));
   };
   auto store_patch_part = [&](const float* src, float* sp, int k, int c0, int cn) {
-    const int cb0 = min(k, nch - 1) * CK + ph * 8;
+    const int cb0 = (kb + min(k, nch - 1)) * CK + ph * 8;
 #pragma unroll
     for (int c = c0; c < c0 + cn; ++c) {
       float v = src[c];
@@ -1019,7 +1026,9 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   // B operands: uo[ks & 1][q] = U[c0 + 4 ks + kq][cout_w + jj][4q..4q + 3]
   f4 uo[2][4];
   const int uoff = ((kq * g.Cout + cout_w + jj) * 16) * 4;
-  auto u_soff = [&](int k, int ks) { return ((min(k, nch - 1) * CK + 4 * ks) * g.Cout) * 64; };
+  auto u_soff = [&](int k, int ks) {
+    return (((kb + min(k, nch - 1)) * CK + 4 * ks) * g.Cout) * 64;
+  };
   auto load_u = [&](int slot, int k, int ks) {
     const int soff = u_soff(k, ks);
 #pragma unroll
@@ -1144,7 +1153,7 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   if (cout_w < g.CoutS) {
     const int co = cout_w + jj;
     const float bv = bias ? bias[co] : 0.f;
-    const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
+    const int64_t obase = ((int64_t)(ks_idx * g.N + n) * g.CoutS + co) * plane;
     float lm = 0.f, lm2 = 0.f;
     // residual tail: all eight skip vectors of this lane requested before the first is used
     // (one exposed memory latency; loaded per store, the compiler waited for each in turn)
@@ -1212,6 +1221,51 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
     }
   }
   WINO_TS(5);
+}
+
+// Split-K epilogue: y = sum_s part[s] + bias, or (skip + that) / div, and the GroupNorm partial
+// statistics of the stored values, as the 16-cin kernel's own epilogue (the partial slabs are
+// summed in a fixed order: deterministic).  One workgroup = 8 channels x one 8 x 16 region of
+// one image; a half-wave holds one channel's 128 values (the store_tile mapping).
+__global__ __launch_bounds__(256) void wino_splitk_reduce_kernel(
+    const float* __restrict__ part, int S, const float* __restrict__ bias,
+    const float* __restrict__ skip, float* __restrict__ y, float2* __restrict__ stats,
+    WinoGeo g) {
+  const int lane = threadIdx.x & 63;
+  const int q = threadIdx.x;
+  unsigned b = blockIdx.x, reg, cg;
+  const unsigned R = (unsigned)(g.regions_x * g.regions_y);
+  unsigned r = udivmod(b, R, reg);
+  const int n = (int)udivmod(r, (unsigned)(g.CoutS / 8), cg);
+  const int co = (int)cg * 8 + (q >> 5);
+  const int rem = q & 31;
+  const int row = rem >> 2, c4 = rem & 3;
+  const int oy0 = (int)(reg / g.regions_x) * kOutRows, ox0 = (int)(reg % g.regions_x) * kOutCols;
+  const int64_t plane = (int64_t)g.H * g.W;
+  const int64_t slab = (int64_t)g.N * g.CoutS * plane;
+  const int64_t o = ((int64_t)n * g.CoutS + co) * plane + (int64_t)(oy0 + row) * g.W + ox0 + 4 * c4;
+  f4 v = *reinterpret_cast<const f4*>(&part[o]);
+  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f4*>(&part[s * slab + o]);
+  const float bv = bias ? bias[co] : 0.f;
+  v += f4{bv, bv, bv, bv};
+  if (skip) {
+    const f4 sk = *reinterpret_cast<const f4*>(&skip[o]);
+    const float rdiv = 1.f / g.div;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = div_rn(sk[c] + v[c], g.div, rdiv);
+  }
+  *reinterpret_cast<f4*>(&y[o]) = v;
+  if (!stats) return;
+  float mm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+  float qq = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) qq = fmaf(v[e] - mm, v[e] - mm, qq);
+  merge_stats(mm, qq, dpp_f<0xB1>(mm), dpp_f<0xB1>(qq), 4.f);
+  merge_stats(mm, qq, dpp_f<0x4E>(mm), dpp_f<0x4E>(qq), 8.f);
+  merge_stats(mm, qq, dpp_f<0x141>(mm), dpp_f<0x141>(qq), 16.f);
+  merge_stats(mm, qq, dpp_f<0x140>(mm), dpp_f<0x140>(qq), 32.f);
+  merge_stats(mm, qq, __shfl_xor(mm, 16, 64), __shfl_xor(qq, 16, 64), 64.f);
+  if ((lane & 31) == 0) stats[((int64_t)n * g.CoutS + co) * R + reg] = make_float2(mm, qq);
 }
 
 }  // namespace
@@ -1338,6 +1392,66 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
   if (pre) WINO_LAUNCH(1, true); else WINO_LAUNCH(1, false);
 #undef WINO_LAUNCH
   BPK_LAUNCH_CHECK("conv3x3_wino");
+  return BPK_OK;
+}
+
+// Split-K for 16-cin launches that leave most CUs idle (the 32^2 / 16^2 levels at the small
+// per-GPU batches of a batch-sharded run: B = 8 -> 128 / 32 workgroups on 256 CUs): the input
+// channels are split into S slices (S a power of two, at least 2 chunks per slice), so that
+// items x S is at most one workgroup per CU, then a reduce kernel applies the epilogue.
+static int wino_splits(int N, int Cin, int C1, int Cout, int H, int W) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int CoutP = cout_padded(Cout);
+  if (!bpk_conv3x3_wino_supported(N, Cin, Cout, H, W) || CoutP % 128 || Cin % 16 || C1 % 16)
+    return 1;
+  const int64_t items = (int64_t)N * (H / kOutRows) * (W / kOutCols) * (CoutP / 128);
+  const int nch = Cin / 16;
+  int S = 1;
+  while (items * S * 2 <= cus && nch % (2 * S) == 0 && nch / (2 * S) >= 2) S *= 2;
+  return S;
+}
+
+extern "C" int64_t bpk_conv3x3_wino_splitk_bytes(int N, int Cin, int C1, int Cout, int H, int W) {
+  const int S = wino_splits(N, Cin, C1, Cout, H, W);
+  return S > 1 ? (int64_t)S * N * Cout * H * W * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int bpk_conv3x3_wino_splitk_f32(const float* x, const float* x2, int C1,
+                                           const float* pre, const float* U, const float* bias,
+                                           const float* skip, float div, float* y, float* stats,
+                                           float* workspace, int N, int Cin, int Cout, int H,
+                                           int W, void* stream) {
+  const int S = wino_splits(N, Cin, x2 ? C1 : Cin, Cout, H, W);
+  if (S <= 1)
+    return bpk_conv3x3_wino_ex_f32(x, x2, C1, pre, U, bias, skip, div, y, stats, N, Cin, Cout, H,
+                                   W, stream);
+  if (!x2) C1 = Cin;
+  BPK_REQUIRE(workspace != nullptr, "conv3x3_wino_splitk: workspace is NULL");
+  BPK_REQUIRE(Cout % 16 == 0, "conv3x3_wino_splitk: Cout %% 16 != 0");
+  const int CoutP = cout_padded(Cout);
+  WinoGeo gk{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / 128, div, C1, Cout, 0, S};
+  const int64_t items = (int64_t)N * gk.regions_x * gk.regions_y * gk.cout_blocks * S;
+  BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino_splitk: grid too large");
+  const float2* kpre = reinterpret_cast<const float2*>(pre);
+  hipStream_t st = bpk::as_stream(stream);
+  const int remap = (items % 8 == 0) ? 1 : 0;
+  if (pre)
+    hipLaunchKernelGGL((wino_f23_k16_kernel<true>), dim3((unsigned)items), dim3(512), 0, st, x, U,
+                       nullptr, nullptr, kpre, workspace, nullptr, gk, remap, x2);
+  else
+    hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3((unsigned)items), dim3(512), 0, st, x,
+                       U, nullptr, nullptr, kpre, workspace, nullptr, gk, remap, x2);
+  BPK_LAUNCH_CHECK("conv3x3_wino_splitk");
+  const int64_t rblocks = (int64_t)N * (Cout / 8) * gk.regions_x * gk.regions_y;
+  BPK_REQUIRE(Cout % 8 == 0 && rblocks < (1LL << 31), "conv3x3_wino_splitk: reduce grid");
+  hipLaunchKernelGGL(wino_splitk_reduce_kernel, dim3((unsigned)rblocks), dim3(256), 0, st,
+                     workspace, S, bias, skip, y, reinterpret_cast<float2*>(stats), gk);
+  BPK_LAUNCH_CHECK("conv3x3_wino_splitk_reduce");
   return BPK_OK;
 }
 

@@ -31,7 +31,7 @@ using f4 = __attribute__((ext_vector_type(4))) float;
 constexpr int kCB = 32;              // cin per workgroup
 constexpr int kOB = 64;              // cout per workgroup
 constexpr int kT = 8;                // tiles per K-chunk (1 tile row x 8 tile cols)
-constexpr int kXR = 4, kXC = 18;     // input patch rows / cols
+constexpr int kXR = 4;               // input patch rows
 constexpr int kRec = 20;             // LDS stride of one 16-position record
 
 struct WgradGeo {

@@ -31,6 +31,8 @@ constexpr int kBS = 132;   // B row stride (floats)
 struct GemmGeo {
   int N, M, P, K1, K2, ldw;
   int tiles_m, tiles_p;
+  int ksplit;  // > 1: split-K; workgroup slice s contracts chunks [s, s + 1) * nch / ksplit and
+               // stores its raw partial to Y + s * N * M * P (gemm_splitk_reduce_kernel adds)
 };
 
 __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
@@ -51,9 +53,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
   const int tm = (int)(b % g.tiles_m);
   int64_t r = b / g.tiles_m;
   const int tp = (int)(r % g.tiles_p);
-  const int n = (int)(r / g.tiles_p);
+  r /= g.tiles_p;
+  const int n = (int)(r % g.N);
+  const int ks_idx = (int)(r / g.N);  // split-K slice (0 unless ksplit > 1)
   const int m0 = tm * kBM, p0 = tp * kBP;
-  const int nch1 = g.K1 / kKC, nch = nch1 + g.K2 / kKC;
+  const int nch1 = g.K1 / kKC;
+  const int ncs = (nch1 + g.K2 / kKC) / max(g.ksplit, 1);  // chunks of this workgroup
+  const int cb = ks_idx * ncs;                              // its first chunk
+  const int nch = cb + ncs;                                 // one past its last
 
   f4 acc[4][4];
 #pragma unroll
@@ -90,13 +97,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
     }
   };
 
-  load(0);
+  load(cb);
   store(0);
-  load(1);
+  load(cb + 1);
   __syncthreads();
 
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
+  for (int c = cb; c < nch; ++c) {
+    const int buf = (c - cb) & 1;
     // operands of this chunk
     f4 a[4];
     float bv[4][4];
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
   }
 
   // acc[i][j][rr] = Y[m0 + 64 wm + 16 i + 4 kq + rr][p0 + 64 wp + 16 j + jj]
-  float* yn = Y + (int64_t)n * g.M * g.P;
+  float* yn = Y + ((int64_t)ks_idx * g.N + n) * g.M * g.P;
   // the 16 bias values of this lane requested together (loaded per row before a store
   // group, the compiler waited for each in turn: 16 exposed latencies per workgroup)
   float bbv[4][4];
@@ -159,6 +166,24 @@ __global__ __launch_bounds__(256, 2) void gemm_nchw_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) yn[(int64_t)m * g.P + p0 + 64 * wp + 16 * j + jj] = acc[i][j][rr] + bb;
     }
+}
+
+
+// y[n][m][p] = sum_s part[s][n][m][p] + bias[m] (fixed order), 4 pixels per thread
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const f4* __restrict__ part,
+                                                                 int S, int64_t slab4,
+                                                                 const float* __restrict__ bias,
+                                                                 f4* __restrict__ y, int M,
+                                                                 int P4) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= slab4) return;
+  f4 v = part[i];
+  for (int s = 1; s < S; ++s) v += part[s * slab4 + i];
+  if (bias) {
+    const float b = bias[(int)((i / P4) % M)];
+    v += f4{b, b, b, b};
+  }
+  y[i] = v;
 }
 
 
@@ -329,7 +354,7 @@ extern "C" int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K
               "P %% 128, K %% 16 == 0)", N, M, P, K1, K2);
   BPK_REQUIRE(ldw >= K1 + K2 && ldw % 4 == 0, "gemm_nchw: bad weight row stride %d", ldw);
   BPK_REQUIRE(K2 == 0 || X2 != nullptr, "gemm_nchw: K2 > 0 needs X2");
-  GemmGeo g{N, M, P, K1, K2, ldw, (M + kBM - 1) / kBM, P / kBP};
+  GemmGeo g{N, M, P, K1, K2, ldw, (M + kBM - 1) / kBM, P / kBP, 1};
   const int64_t blocks = (int64_t)N * g.tiles_m * g.tiles_p;
   BPK_REQUIRE(blocks < (1LL << 31), "gemm_nchw: grid too large");
   const int remap = (blocks % 8 == 0) ? 1 : 0;
@@ -337,6 +362,53 @@ extern "C" int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K
                      bpk::as_stream(stream), W, X1, K2 ? W + K1 : W, K2 ? X2 : X1, bias, Y, g,
                      remap);
   BPK_LAUNCH_CHECK("gemm_nchw");
+  return BPK_OK;
+}
+
+// Split-K for launches that leave most of the chip idle (the 16^2 / 32^2 levels at the
+// per-GPU batch of a batch-sharded run: M = 256, P = 256, N = 8 -> 32 workgroups): S slices of
+// at least 4 K-chunks, S a power of two, items x S up to the resident workgroups (2 per CU).
+static int gemm_splits(int N, int M, int P, int K1, int K2) {
+  static const int slots = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return 2 * (n > 0 ? n : 256);
+  }();
+  if (!bpk_gemm_nchw_supported(N, M, P, K1, K2) || P % 4) return 1;
+  const int64_t items = (int64_t)N * ((M + kBM - 1) / kBM) * (P / kBP);
+  const int nch = (K1 + K2) / kKC;
+  int S = 1;
+  while (items * S * 2 <= slots && nch % (2 * S) == 0 && nch / (2 * S) >= 4) S *= 2;
+  return S;
+}
+
+extern "C" int64_t bpk_gemm_nchw_splitk_bytes(int N, int M, int P, int K1, int K2) {
+  const int S = gemm_splits(N, M, P, K1, K2);
+  return S > 1 ? (int64_t)S * N * M * P * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int bpk_gemm_nchw_splitk_f32(const float* W, int ldw, const float* X1, int K1,
+                                        const float* X2, int K2, const float* bias, float* Y,
+                                        float* workspace, int N, int M, int P, void* stream) {
+  const int S = gemm_splits(N, M, P, K1, K2);
+  if (S <= 1) return bpk_gemm_nchw_f32(W, ldw, X1, K1, X2, K2, bias, Y, N, M, P, stream);
+  BPK_REQUIRE(ldw >= K1 + K2 && ldw % 4 == 0, "gemm_nchw: bad weight row stride %d", ldw);
+  BPK_REQUIRE(K2 == 0 || X2 != nullptr, "gemm_nchw: K2 > 0 needs X2");
+  BPK_REQUIRE(workspace != nullptr, "gemm_nchw_splitk: workspace is NULL");
+  GemmGeo g{N, M, P, K1, K2, ldw, (M + kBM - 1) / kBM, P / kBP, S};
+  const int64_t blocks = (int64_t)N * g.tiles_m * g.tiles_p * S;
+  BPK_REQUIRE(blocks < (1LL << 31), "gemm_nchw: grid too large");
+  hipStream_t st = bpk::as_stream(stream);
+  hipLaunchKernelGGL(gemm_nchw_kernel, dim3((unsigned)blocks), dim3(256), 0, st, W, X1,
+                     K2 ? W + K1 : W, K2 ? X2 : X1, nullptr, workspace, g,
+                     (blocks % 8 == 0) ? 1 : 0);
+  BPK_LAUNCH_CHECK("gemm_nchw_splitk");
+  const int64_t slab4 = (int64_t)N * M * P / 4;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)bpk::ceil_div(slab4, 256)),
+                     dim3(256), 0, st, reinterpret_cast<const f4*>(workspace), S, slab4, bias,
+                     reinterpret_cast<f4*>(Y), M, P / 4);
+  BPK_LAUNCH_CHECK("gemm_nchw_splitk_reduce");
   return BPK_OK;
 }
 

@@ -627,8 +627,10 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
   } else {
     // rows in pairs: row t = oy*2 - P0 + 2 (taps 2 of oy, 0 of oy + 1) and t + 1 (taps 3, 1);
     // acc[0] = output oy, acc[1] = oy + 1.  Prologue: rows t0, t0 + 1 (taps 0, 1 of oyb).
-    // RB > 0 (= rows, out_h % RB == 0): the strip's output rows stay in registers and are
-    // stored after its last input row, as in the FIR form above.
+    // (Holding the strip's rows in registers and storing them after its last input row, as
+    // the FIR form does, measured slower here: 0.60 -> 0.44 of HBM on [64,128,128,128],
+    // 0.63 -> 0.47 on [64,256,64,64], round 4 -- the two in-flight accumulators already keep
+    // the stores off the loads' critical path.)
     load_row(t0 + 1, nxt);
     edges(t0, cur, left, right);
     hsum(0, cur, left, right, acc[0]);
@@ -640,34 +642,6 @@ __global__ __launch_bounds__(256) void upfirdn2d_roll(const float* __restrict__ 
     hsum(1, cur, left, right, acc[0]);
 #pragma unroll
     for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
-    if constexpr (RB > 0) {
-      float ob[RB][NOCT];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        t = (oyb + r) * 2 - P0 + 2;  // cur holds row t
-        load_row(t + 1, nxt);
-        edges(t, cur, left, right);
-        hsum(2, cur, left, right, acc[0]);
-        hsum(0, cur, left, right, acc[1]);
-#pragma unroll
-        for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
-        if (r + 1 < RB) load_row(t + 2, nxt);
-        edges(t + 1, cur, left, right);
-        hsum(3, cur, left, right, acc[0]);
-        hsum(1, cur, left, right, acc[1]);
-#pragma unroll
-        for (int oc = 0; oc < NOCT; ++oc) {
-          ob[r][oc] = acc[0][oc];
-          acc[0][oc] = acc[1][oc];
-          acc[1][oc] = 0.f;
-        }
-#pragma unroll
-        for (int c = 0; c < LV; ++c) cur[c] = nxt[c];
-      }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) store(oyb + r, ob[r]);
-      return;
-    }
     for (int oy = oyb; oy < oye; ++oy) {
       t = oy * 2 - P0 + 2;  // cur holds row t
       load_row(t + 1, nxt);
@@ -708,15 +682,12 @@ int launch_roll(const float* x, const float* k, float* out, int major, int in_h,
 }
 
 // Strip height of the rolling kernel: down2 -> about 32 k waves (tools/gpu_upfirdn_roll.sh on
-// MI355X: [64,128,128,128] best at 8 rows, [64,256,64,64] at 4, i.e. 32 k waves both), as a
-// power of two (2..16) so the strip's rows can be held in registers (RB); the odd-width 1:1 FIR
-// -> the divisor of the height in 5..8 (65 = 13 x 5; 5 and 6 rows: 0.59 of HBM vs 0.45 for the
-// 4-row stream strips).
+// MI355X: [64,128,128,128] best at 8 rows, [64,256,64,64] at 4, i.e. 32 k waves both), the
+// odd-width 1:1 FIR -> the divisor of the height in 5..8 (65 = 13 x 5; 5 and 6 rows: 0.59 of
+// HBM vs 0.45 for the 4-row stream strips).
 int roll_rows_down2(int major, int out_h, int strips_x, int segs) {
   const double per = (double)major * out_h * strips_x / (32768.0 * segs);
-  int r = 2;
-  while (r < 16 && 2 * r <= per * 1.4142) r *= 2;
-  return r;
+  return std::max(3, std::min(64, (int)(per + 0.5)));
 }
 
 int roll_rows_fir(int out_h) {
@@ -732,20 +703,8 @@ bool try_roll(const float* x, const float* k, float* out, int major, int in_h, i
     const int lanes = (int)bpk::ceil_div(out_w, 2);  // two output columns per lane
     const int sw = lanes <= 8 ? 8 : lanes <= 16 ? 16 : lanes <= 32 ? 32 : 64;
     const int rows = roll_rows_down2(major, out_h, (int)bpk::ceil_div(out_w, 2 * sw), 64 / sw);
-    // rows held in registers and stored after the strip's last input row when they tile the
-    // plane (every power-of-two plane; [64,128,128,128] and [64,256,64,64] both)
-#define BPK_ROLL2R(P, SW, RB) \
-  return (*rc = launch_roll<2, P, SW, 2, false, RB>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
-#define BPK_ROLL2(P, SW)                         \
-  do {                                           \
-    if (out_h % rows == 0) {                     \
-      if (rows == 2) BPK_ROLL2R(P, SW, 2);       \
-      if (rows == 4) BPK_ROLL2R(P, SW, 4);       \
-      if (rows == 8) BPK_ROLL2R(P, SW, 8);       \
-      if (rows == 16) BPK_ROLL2R(P, SW, 16);     \
-    }                                            \
-    BPK_ROLL2R(P, SW, 0);                        \
-  } while (0)
+#define BPK_ROLL2(P, SW) \
+  return (*rc = launch_roll<2, P, SW, 2>(x, k, out, major, in_h, in_w, kh, kw, out_h, out_w, rows, st), true)
     if (p0 == 1) {
       if (sw == 8) BPK_ROLL2(1, 8);
       if (sw == 16) BPK_ROLL2(1, 16);
@@ -756,7 +715,6 @@ bool try_roll(const float* x, const float* k, float* out, int major, int in_h, i
     if (sw == 16) BPK_ROLL2(2, 16);
     if (sw == 32) BPK_ROLL2(2, 32);
     BPK_ROLL2(2, 64);
-#undef BPK_ROLL2R
 #undef BPK_ROLL2
   }
   if (down == 1 && p0 == 2 && (out_w & 1) && kw == 4 && a16) {

@@ -179,11 +179,17 @@ def conv3x3_fwd_raw(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=Fa
     if stats:
         R = (H // 8) * (W // 16)
         part = torch.empty((N, Cout, R, 2), dtype=torch.float32, device=x.device)
-    check(lib.bpk_conv3x3_wino_ex_f32(
+    # split-K over the input channels when the launch would leave most CUs idle (small
+    # per-GPU batches at the 32^2 / 16^2 levels); the workspace comes from the caching
+    # allocator (the graph's pool under capture)
+    nws = lib.bpk_conv3x3_wino_splitk_bytes(N, C, C1 if x2 is not None else C, Cout, H, W)
+    ws = torch.empty(nws // 4, dtype=torch.float32, device=x.device) if nws > 0 else None
+    check(lib.bpk_conv3x3_wino_splitk_f32(
         x.data_ptr(), None if x2 is None else x2.data_ptr(), C1,
         None if pr is None else pr.data_ptr(), U.data_ptr(),
         None if b is None else b.data_ptr(), None if sk is None else sk.data_ptr(), float(div),
-        y.data_ptr(), None if part is None else part.data_ptr(), N, C, Cout, H, W,
+        y.data_ptr(), None if part is None else part.data_ptr(),
+        None if ws is None else ws.data_ptr(), N, C, Cout, H, W,
         stream_ptr(x.device)), "conv3x3_wino")
     flops.wino3x3("wino_dgrad" if ft else "wino_fwd", N, C, Cout, H, W)
     if part is not None:
@@ -843,6 +849,18 @@ def gemm1x1_supported(x, weight, x2=None):
     return bool(lib.bpk_gemm_nchw_supported(N, weight.shape[0], H * W, K1, K2))
 
 
+def _gemm_nchw(w, ldw, x, K1, x2, K2, b, y, N, M, P):
+    """bpk_gemm_nchw_f32, split over K (workspace from the caching allocator) when the launch
+    would leave most CUs idle (bpk_gemm_nchw_splitk_bytes > 0)."""
+    nws = lib.bpk_gemm_nchw_splitk_bytes(N, M, P, K1, K2)
+    ws = torch.empty(nws // 4, dtype=torch.float32, device=x.device) if nws > 0 else None
+    check(lib.bpk_gemm_nchw_splitk_f32(w.data_ptr(), ldw, x.data_ptr(), K1,
+                                       None if x2 is None else x2.data_ptr(), K2,
+                                       None if b is None else b.data_ptr(), y.data_ptr(),
+                                       None if ws is None else ws.data_ptr(), N, M, P,
+                                       stream_ptr(x.device)), "conv1x1")
+
+
 def conv1x1(x, weight, bias=None, x2=None):
     """1x1 conv of NCHW x (or of the channel concatenation [x, x2], without building it)
     with weight [Cout, Cin(, 1, 1)] (+ bias): the MFMA GEMM kernel.  Inference only."""
@@ -858,10 +876,7 @@ def conv1x1(x, weight, bias=None, x2=None):
     w = weight.detach().reshape(M, K1 + K2).contiguous()
     b = None if bias is None else bias.detach().contiguous()
     y = torch.empty((N, M, H, W), dtype=torch.float32, device=x.device)
-    check(lib.bpk_gemm_nchw_f32(w.data_ptr(), K1 + K2, x.data_ptr(), K1,
-                                None if x2 is None else x2.data_ptr(), K2,
-                                None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
-                                stream_ptr(x.device)), "conv1x1")
+    _gemm_nchw(w, K1 + K2, x, K1, x2, K2, b, y, N, M, H * W)
     flops.add("gemm1x1", 2.0 * N * M * (K1 + K2) * H * W)
     return y
 
@@ -889,9 +904,7 @@ def _gemm1x1_raw(x, w2d, bias=None):
     M = w.shape[0]
     b = None if bias is None else bias.detach().contiguous()
     y = torch.empty((N, M, H, W), dtype=torch.float32, device=x.device)
-    check(lib.bpk_gemm_nchw_f32(w.data_ptr(), K, x.data_ptr(), K, None, 0,
-                                None if b is None else b.data_ptr(), y.data_ptr(), N, M, H * W,
-                                stream_ptr(x.device)), "conv1x1")
+    _gemm_nchw(w, K, x, K, None, 0, b, y, N, M, H * W)
     flops.add("gemm1x1", 2.0 * N * M * K * H * W)
     return y
 

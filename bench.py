@@ -365,10 +365,11 @@ def _cpu_threads():
 
 def cpu_baseline(n_samples):
     """The oracle (torch-CPU restatement of the reference path, same aten op sequence) on the
-    host cores: one warm-up PC step on 1 sample, then 1 PC step (EM + Langevin = 2 evals per
-    sample) on n_samples.  Deviation from BASELINE.md's plan (B = 64 x 3 steps = 384 evals,
-    ~5 min at ~1.4 evals/s): a bounded 2 x n_samples-eval sample keeps the default bench
-    within minutes; evals/s does not depend on the number of steps."""
+    host cores: one warm-up PC step on n_samples (the timed shapes: oneDNN builds its
+    primitives per shape), then 1 timed PC step (EM + Langevin = 2 evals per sample) on the
+    same n_samples.  Deviation from SURVEY 8(d)'s plan (B = 64 x 3 steps = 384 evals, ~5 min
+    at ~1.3 evals/s): a bounded 2 x n_samples-eval sample keeps the default bench within
+    minutes; evals/s does not depend on the number of steps."""
     from configs.vp import nc_ncsnpp_128
     from oracle import nets_ref, score_sde_ref
     import models  # noqa: F401
@@ -381,8 +382,8 @@ def cpu_baseline(n_samples):
     params = nets_ref.init_params(mutils.create_model(c, wrap=False).state_dict())
     sde = score_sde_ref.SDESpec("vp", N=1000)
     mf = lambda x, t: nets_ref.forward(params, c, x, t)
-    score_sde_ref.pc_sample(mf, sde, torch.randn(1, 1, 128, 128), "euler_maruyama", "langevin",
-                            0.075, 1, True, n_iters=1)
+    score_sde_ref.pc_sample(mf, sde, torch.randn(n_samples, 1, 128, 128), "euler_maruyama",
+                            "langevin", 0.075, 1, True, n_iters=1)
     t0 = time.perf_counter()
     score_sde_ref.pc_sample(mf, sde, torch.randn(n_samples, 1, 128, 128), "euler_maruyama",
                             "langevin", 0.075, 1, True, n_iters=1)
@@ -390,8 +391,9 @@ def cpu_baseline(n_samples):
     return {"value": round(2 * n_samples / dt, 4), "unit": "score-net evals/s", "cores": cores,
             "kind": "port", "cpu": _cpu_model(),
             "sample": f"oracle/nets_ref + score_sde_ref: 1 PC step (EM+Langevin) on {n_samples} "
-                      f"samples of 128x128x1 = {2 * n_samples} evals in {dt:.1f}s (plan: B=64 x 3 "
-                      "steps; bounded sample, same per-eval work)"}
+                      f"samples of 128x128x1 = {2 * n_samples} evals in {dt:.1f}s after a warm-up "
+                      "step at the same batch (plan: B=64 x 3 steps; bounded sample, same "
+                      "per-eval work)"}
 
 
 def cpu_train_baselines():
@@ -543,19 +545,31 @@ def cpu_dps_baseline(nfe=1):
                       f"at B=1: 1 warm-up + {nfe} timed, {dt:.2f}s each"}
 
 
-def cpu_ns_baseline():
-    """The C restatement of the reference ns_step (oracle/ns_step_ref.c, single thread) on a
-    bounded sample: B = 16 replicas of 192x192, 3 full steps (velocity, pressure, density)."""
+def cpu_ns_baseline(steps=100):
+    """The C restatement of the reference ns_step (oracle/ns_step_ref.c) on the host cores:
+    one 192x192 replica per thread (ctypes releases the GIL inside the C calls, so the
+    replicas -- independent, as the simulator's batch -- run in parallel), 1 warm-up + `steps`
+    timed full steps (velocity, pressure, density)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import ns_step_ref
-    f, v, p = _ns_fields(np.random.default_rng(0), 16, 192)
-    ns_step_ref.full_step(f, v, p, 0.0025, 0.005)
-    t0 = time.perf_counter()
-    for _ in range(3):
-        f, v, p = ns_step_ref.full_step(f, v, p, 0.0025, 0.005)
-    dt = time.perf_counter() - t0
-    return {"value": round(3 * 16 * 192 * 192 / dt / 1e9, 4), "unit": "Gsite/s", "cores": 1,
-            "kind": "port", "sample": "oracle/ns_step_ref.c (gcc -O2, 1 thread): 3 full steps of "
-                                      f"16 x 192^2, {dt:.2f}s"}
+    cores = _cpu_threads()
+    f, v, p = _ns_fields(np.random.default_rng(0), cores, 192)
+
+    def run(b, k):
+        cur = (f[b:b + 1].copy(), v[b:b + 1].copy(), p[b:b + 1].copy())
+        for _ in range(k):
+            cur = ns_step_ref.full_step(*cur, 0.0025, 0.005)
+        return cur
+
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(lambda b: run(b, 1), range(cores)))
+        t0 = time.perf_counter()
+        list(ex.map(lambda b: run(b, steps), range(cores)))
+        dt = time.perf_counter() - t0
+    return {"value": round(steps * cores * 192 * 192 / dt / 1e9, 4), "unit": "Gsite/s",
+            "cores": cores, "kind": "port",
+            "sample": f"oracle/ns_step_ref.c (gcc -O2): {cores} replicas of 192^2, one per thread, "
+                      f"{steps} full steps each after 1 warm-up, {dt:.2f}s"}
 
 
 def _ns_fields(rng, B, n):

@@ -379,6 +379,17 @@ int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, const float
                             const float* U, const float* bias, const float* skip, float div,
                             float* y, float* stats, int N, int Cin, int Cout, int H, int W,
                             void* stream);
+/* Split-K form of bpk_conv3x3_wino_ex_f32 for launches that would leave most CUs idle (the
+ * 32^2 / 16^2 levels at the per-GPU batch of a batch-sharded run, SURVEY 8(e): 64 -> 8/GPU):
+ * the input channels are split into S slices whose raw partial outputs go to `workspace`,
+ * then one reduce launch applies bias, the residual tail and the statistics (fixed summation
+ * order: deterministic).  splitk_bytes() = the workspace this shape needs, 0 = no split (then
+ * the entry is bpk_conv3x3_wino_ex_f32 and workspace may be NULL).  Same contract otherwise. */
+int64_t bpk_conv3x3_wino_splitk_bytes(int N, int Cin, int C1, int Cout, int H, int W);
+int bpk_conv3x3_wino_splitk_f32(const float* x, const float* x2, int C1, const float* pre,
+                                const float* U, const float* bias, const float* skip, float div,
+                                float* y, float* stats, float* workspace, int N, int Cin, int Cout,
+                                int H, int W, void* stream);
 /* y = conv3x3(nearest_x2(x)) + bias (bias may be NULL) for x [N, Cin, H/2, W/2] and y
  * [N, Cout, H, W]: F.interpolate(x, scale_factor=2, mode='nearest') followed by Conv_0 of the
  * ddpm net's Upsample (reference models/layers.py:576-590), with the upsample read inside the
@@ -427,6 +438,14 @@ int bpk_conv3x3_small_f32(const float* x, const float* pre, const float* weight,
 int bpk_gemm_nchw_supported(int N, int M, int P, int K1, int K2);
 int bpk_gemm_nchw_f32(const float* W, int ldw, const float* X1, int K1, const float* X2, int K2,
                       const float* bias, float* Y, int N, int M, int P, void* stream);
+/* Split-K form for launches too small to fill the chip (the 16^2 / 32^2 levels at the per-GPU
+ * batch of a batch-sharded run): S slices of K write raw partials to `workspace`, one reduce
+ * launch sums them in a fixed order and adds the bias.  splitk_bytes() = the workspace this
+ * shape needs, 0 = no split (then the entry is bpk_gemm_nchw_f32, workspace may be NULL). */
+int64_t bpk_gemm_nchw_splitk_bytes(int N, int M, int P, int K1, int K2);
+int bpk_gemm_nchw_splitk_f32(const float* W, int ldw, const float* X1, int K1, const float* X2,
+                             int K2, const float* bias, float* Y, float* workspace, int N, int M,
+                             int P, void* stream);
 
 /* Channel self-attention of the score networks' attention blocks at inference, one kernel:
  *   out[b, c, i] = sum_j V[b, c, j] softmax_j(scale * sum_c' Q[b, c', i] K[b, c', j])

@@ -629,11 +629,17 @@ def test_conv3x3_double_backward_any_shape(hip, cin, cout, hw):
 
 @pytest.mark.parametrize("N,k1,k2,m,hw", [(2, 64, 0, 128, 16), (3, 128, 64, 256, 32),
                                           (1, 256, 256, 128, 16), (2, 16, 48, 384, 32),
-                                          (2, 96, 0, 32, 16), (1, 64, 32, 80, 16)])
+                                          (2, 96, 0, 32, 16), (1, 64, 32, 80, 16),
+                                          (8, 256, 0, 256, 16), (8, 512, 0, 768, 16),
+                                          (4, 128, 128, 144, 16), (8, 256, 256, 256, 32)])
 def test_conv1x1_gemm_matches_fp32_reference(hip, N, k1, k2, m, hw):
     """MFMA 1x1-conv GEMM (one or two sources along K) vs float64 (1e-5 relative); the
-    two-source form equals conv1x1 of the concatenation."""
-    from op.conv import conv1x1
+    two-source form equals conv1x1 of the concatenation.  The small-batch cases take the
+    split-K form (bpk_gemm_nchw_splitk_f32: the 16^2 / 32^2 levels at 8 samples per GPU),
+    incl. a split that crosses the two sources and an M that is not a multiple of 128."""
+    from op.conv import conv1x1, lib
+    if N >= 4:
+        assert lib.bpk_gemm_nchw_splitk_bytes(N, m, hw * hw, k1, k2) > 0
     g = torch.Generator().manual_seed(k1 + k2 + m)
     x1 = torch.randn(N, k1, hw, hw, generator=g)
     x2 = torch.randn(N, k2, hw, hw, generator=g) if k2 else None
@@ -1242,6 +1248,50 @@ def test_conv3x3_winograd_large_launch(hip, mode):
         part, R, cnt = gn_partials(out)
         m = out.reshape(N, cout, hw // 8, 8, hw // 16, 16).mean((3, 5)).reshape(N, cout, R)
         assert (part[..., 0] - m).abs().max().item() <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("mode", ["pre_stats", "pre_skip", "plain", "two_sources", "dgrad"])
+@pytest.mark.parametrize("N,cin,cout,hw", [(8, 256, 256, 16), (8, 512, 256, 16), (8, 256, 256, 32),
+                                           (2, 128, 256, 16), (3, 256, 128, 32)])
+def test_conv3x3_winograd_split_k(hip, mode, N, cin, cout, hw):
+    """The split-K form (bpk_conv3x3_wino_splitk_f32) that the small per-GPU batches of a
+    batch-sharded run take at the 32^2 / 16^2 levels: the launch is split (workspace > 0), and
+    output, residual tail, two-source input, backward-data and the GroupNorm partial statistics
+    match F.conv2d / the statistics of the output (1e-5 relative)."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3, conv3x3_fwd_raw, gn_partials, lib
+    assert lib.bpk_conv3x3_wino_splitk_bytes(N, cin, cin, cout, hw, hw) > 0
+    g = torch.Generator().manual_seed(N * 1000 + cin + hw)
+    x = (torch.randn(N, cin, hw, hw, generator=g) * 1.5).to(hip)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(hip)
+    b = torch.randn(cout, generator=g).to(hip)
+    st = torch.stack([torch.rand(N, cin, generator=g) + 0.5, torch.randn(N, cin, generator=g) * 0.3], -1).to(hip)
+    skip = torch.randn(N, cout, hw, hw, generator=g).to(hip)
+    with torch.no_grad():
+        a = F.silu(x * st[..., 0, None, None] + st[..., 1, None, None])
+        if mode == "plain":
+            out, ref = conv3x3_fwd_raw(x, w, b), F.conv2d(x, w, b, padding=1)
+        elif mode == "pre_stats":
+            out, ref = conv3x3(x, w, b, pre=st, stats=True), F.conv2d(a, w, b, padding=1)
+        elif mode == "pre_skip":
+            out = conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=st, stats=True)
+            ref = (skip + F.conv2d(a, w, b, padding=1)) / 2 ** 0.5
+        elif mode == "two_sources":
+            out = conv3x3_fwd_raw(x[:, :48].contiguous(), w, b, pre=st, stats=True,
+                                  x2=x[:, 48:].contiguous())
+            ref = F.conv2d(a, w, b, padding=1)
+        else:  # dx = conv(gy, flip_t(w)): the Winograd backward-data form
+            gy = torch.randn(N, cout, hw, hw, generator=g).to(hip)
+            out = conv3x3_fwd_raw(gy, w, ft=True)
+            ref = torch.nn.grad.conv2d_input(x.shape, w, gy, padding=1)
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() <= 1e-5 * scale
+    if mode in ("pre_stats", "pre_skip", "two_sources"):
+        part, R, cnt = gn_partials(out)
+        m = out.reshape(N, cout, hw // 8, 8, hw // 16, 16).mean((3, 5)).reshape(N, cout, R)
+        v = out.reshape(N, cout, hw // 8, 8, hw // 16, 16).var((3, 5), unbiased=False).reshape(N, cout, R)
+        assert (part[..., 0] - m).abs().max().item() <= 1e-5 * scale
+        assert (part[..., 1] / cnt - v).abs().max().item() <= 1e-4 * v.abs().max().item()
 
 
 @pytest.mark.parametrize("N,cin,cout,h,w", [(2, 128, 128, 8, 16), (3, 256, 256, 16, 8),
