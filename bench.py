@@ -172,19 +172,49 @@ WINO_MIX = [  # (cin, cout, hw, PRE+stats convs per forward, PRE+residual+stats 
     (512, 256, 16, 5, 0)]
 
 
-def _pmc(key):
-    """HBM bytes of a roofline kernel from the newest committed PMC passes that measured it
-    (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction;
-    profiles/r0*_pmc_traffic.json, tools/pmc_summary.py)."""
+CSRC = os.path.join(REPO, "b-pinn-kalman-filter_amd", "csrc")
+# the kernel sources each PMC entry's counted dispatches come from ("*": every source)
+PMC_SOURCES = {"wino_pre_mix": ["conv_winograd.hip"], "upfirdn2d": ["upfirdn2d.hip"],
+               "ns_step": ["ns_step.hip"], "step": ["*"]}
+
+
+def src_sha1(names):
+    """{file: sha1} of the listed csrc/ sources ("*": all of them), as tools/pmc_summary.py
+    records them next to the counters it summarises."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r0*_pmc_traffic.json")),
+    import hashlib
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h"))) \
+        if names == ["*"] else [os.path.join(CSRC, n) for n in names]
+    return {os.path.basename(f): hashlib.sha1(open(f, "rb").read()).hexdigest() for f in files}
+
+
+def _pmc_entry(key, section="traffic"):
+    """The newest committed PMC entry for `key` (profiles/r0*_pmc_<section>.json) whose
+    recorded kernel sources are the ones this tree builds; None when the entry was measured
+    on other kernels (or carries no source record): counters of a kernel that no longer
+    runs are never attached to a live measurement."""
+    import glob
+    want = next(v for k, v in PMC_SOURCES.items() if key.startswith(k))
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"r0*_pmc_{section}.json")),
                        reverse=True):
         try:
             with open(path) as f:
-                return json.load(f)[key]["traffic_bytes"]
+                e = json.load(f)[key]
         except (OSError, KeyError, ValueError):
             continue
+        rec = e.get("src_sha1") if isinstance(e, dict) else None
+        if rec is None or rec != src_sha1(want):
+            return None
+        return e, os.path.basename(path)
     return None
+
+
+def _pmc(key):
+    """HBM bytes of a roofline kernel (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
+    gfx950 correction; tools/pmc_summary.py), or None when no PMC pass measured the kernels
+    this tree runs."""
+    got = _pmc_entry(key)
+    return None if got is None else got[0]["traffic_bytes"]
 
 
 def step_roofline(tally, steps_per_s, what, unit_of_work="step", survey_direct=None,
@@ -223,19 +253,15 @@ def counted(fn, dev):
 def _ns_valu_cycles():
     """SIMD-cycles of VALU issue per ns_step full step at B=256, 192^2: SQ_ACTIVE_INST_VALU
     (quad-cycles) x 4 of the velocity launch + the pressure/density launch, from the committed
-    PMC pass (profiles/r0*_pmc_sq.json; the instruction stream does not depend on the data)."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r0*_pmc_sq.json")), reverse=True):
-        try:
-            with open(path) as f:
-                runs = json.load(f)["ns_step launches (3 full steps)"]
-        except (OSError, KeyError, ValueError):
-            continue
-        per = {}
-        for r in runs:
-            per.setdefault(r["_grid"], []).append(4.0 * r["SQ_ACTIVE_INST_VALU"])
-        return sum(sum(v) / len(v) for v in per.values()), os.path.basename(path)
-    return None, None
+    PMC pass of the kernels this tree builds (profiles/r0*_pmc_sq.json, src_sha1 checked; the
+    instruction stream does not depend on the data)."""
+    got = _pmc_entry("ns_step launches (3 full steps)", "sq")
+    if got is None:
+        return None, None
+    per = {}
+    for r in got[0]["runs"]:
+        per.setdefault(r["_grid"], []).append(4.0 * r["SQ_ACTIVE_INST_VALU"])
+    return sum(sum(v) / len(v) for v in per.values()), got[1]
 
 
 def wino_mix_times(dev, batch, reps=10):
@@ -637,8 +663,10 @@ def _ns_valu_roofline(t_step):
     return {"bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
             "unit": "T SIMD-issue-cycles/s", "frac": round(ach / peak, 4), "traffic": None,
             "kernel": "ns_step full step (velocity + pressure/density launches)",
-            "basis": f"VALU-active SIMD-cycles per step {cyc:.4g} (SQ_ACTIVE_INST_VALU x 4, {src}) "
-                     "/ live step time, vs 1024 SIMDs x 2.4 GHz"}
+            "profile_derived": src,
+            "basis": f"VALU-active SIMD-cycles per step {cyc:.4g} (SQ_ACTIVE_INST_VALU x 4 from the "
+                     f"PMC pass {src} of these kernel sources) / live step time, vs 1024 SIMDs x "
+                     "2.4 GHz"}
 
 
 def bench_ncddpmpp(args, ctx, dev):

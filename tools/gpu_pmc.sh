@@ -1,11 +1,15 @@
 #!/bin/bash
-# Round-3 PMC passes: one counter group per rocprofv3 run, each under its own limit; output
-# directories are named <mode>_<group> (tools/pmc_summary.py gpurun_out/pmc3 r03).
+# PMC passes: one counter group per rocprofv3 run, each under its own limit; output
+# directories are named <mode>_<group> under gpurun_out/pmc_$TAG (summarise with
+# tools/pmc_summary.py gpurun_out/pmc_$TAG $TAG on the same tree: it records the kernel
+# sources' sha1, which bench.py checks before it uses an entry).
 # $1 = kernels (single-kernel passes) | steps (whole-step traffic; $2 = modes)
-mkdir -p gpurun_out/pmc3; export TMPDIR=/tmp
+TAG=${TAG:-r04}
+D=gpurun_out/pmc_$TAG
+mkdir -p $D; export TMPDIR=/tmp
 run() {  # script mode group counters...
   local script=$1 mode=$2 grp=$3; shift 3
-  timeout -s KILL ${PMC_LIMIT:-240} rocprofv3 --pmc "$@" -d gpurun_out/pmc3/${mode}_$grp -o pmc --output-format csv -- python $script $mode > gpurun_out/pmc3/${mode}_$grp.log 2>&1 || { echo "pass $mode $grp failed"; grep -v "^[WE]2026\|^    @" gpurun_out/pmc3/${mode}_$grp.log | tail -12; exit 1; }
+  timeout -s KILL ${PMC_LIMIT:-240} rocprofv3 --pmc "$@" -d $D/${mode}_$grp -o pmc --output-format csv -- python $script $mode > $D/${mode}_$grp.log 2>&1 || { echo "pass $mode $grp failed"; grep -v "^[WE]2026\|^    @" $D/${mode}_$grp.log | tail -12; exit 1; }
   echo "pass $mode $grp ok"
 }
 if [ "${1:-kernels}" = kernels ]; then
@@ -21,9 +25,9 @@ run tools/prof_r02.py ns sq SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_
 else
 for m in ${2:-train cifar pinn dps}; do
   run tools/prof_steps.py $m fetch FETCH_SIZE
-  python tools/pmc_summary.py gpurun_out/pmc3 r03 reduce-step $m FETCH_SIZE && rm -rf gpurun_out/pmc3/${m}_fetch
+  python tools/pmc_summary.py $D $TAG reduce-step $m FETCH_SIZE && rm -rf $D/${m}_fetch
   run tools/prof_steps.py $m write WRITE_SIZE
-  python tools/pmc_summary.py gpurun_out/pmc3 r03 reduce-step $m WRITE_SIZE && rm -rf gpurun_out/pmc3/${m}_write
+  python tools/pmc_summary.py $D $TAG reduce-step $m WRITE_SIZE && rm -rf $D/${m}_write
 done
 fi
 echo PMC_DONE

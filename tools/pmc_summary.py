@@ -62,7 +62,21 @@ def load(pattern, keep):
             agg[int(r["Dispatch_Id"])][r["Counter_Name"]] = \
                 agg[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             agg[int(r["Dispatch_Id"])]["_grid"] = int(r["Grid_Size"])
+            agg[int(r["Dispatch_Id"])]["_kernel"] = r["Kernel_Name"].split("(")[0]
     return [agg[d] for d in sorted(agg)]
+
+
+def provenance(key, recs=()):
+    """What bench.py checks before it attaches an entry to a live measurement: the sha1 of
+    the kernel sources the counted dispatches were built from (this tree = the tree the GPU
+    pass ran) and the kernel symbols counted."""
+    import bench
+    src = next(v for k, v in bench.PMC_SOURCES.items() if key.startswith(k))
+    out = {"src_sha1": bench.src_sha1(src)}
+    names = sorted({r["_kernel"] for r in recs if "_kernel" in r})
+    if names:
+        out["kernels"] = names
+    return out
 
 
 def main():
@@ -75,7 +89,8 @@ def main():
     out = {"wino_pre_mix": {
         "traffic_bytes": 1024.0 * (2 * sum(mix_f) + sum(mix_w)),
         "fetch_bytes_x2": 2048.0 * sum(mix_f), "write_bytes": 1024.0 * sum(mix_w),
-        "launches": n, "note": "one NCSN++ 128^2 forward's PRE-conv mix at B=64 (bench.WINO_MIX)"}}
+        "launches": n, "note": "one NCSN++ 128^2 forward's PRE-conv mix at B=64 (bench.WINO_MIX)",
+        **provenance("wino_pre_mix", load(pdir("mix", "fetch"), wino))}}
     up = lambda k: "upfirdn" in k
     uf = load(pdir("upfirdn", "fetch"), up)
     uw = load(pdir("upfirdn", "write"), up)
@@ -83,7 +98,8 @@ def main():
         f = sum(d["FETCH_SIZE"] for d in uf[3 * i:3 * i + 3]) / 3
         w = sum(d["WRITE_SIZE"] for d in uw[3 * i:3 * i + 3]) / 3
         out["upfirdn2d " + name] = {"traffic_bytes": 1024.0 * (2 * f + w),
-                                    "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w}
+                                    "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w,
+                                    **provenance("upfirdn2d", uf[3 * i:3 * i + 3])}
     ns = lambda k: "k_fused" in k
     nf = load(pdir("ns", "fetch"), ns)
     nw = load(pdir("ns", "write"), ns)
@@ -91,7 +107,8 @@ def main():
     w = sum(d["WRITE_SIZE"] for d in nw) / 3
     out["ns_step full step B256 192^2"] = {"traffic_bytes": 1024.0 * (2 * f + w),
                                             "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w,
-                                            "note": "both fused launches of one full step"}
+                                            "note": "both fused launches of one full step",
+                                            **provenance("ns_step", nf)}
     if TAG != "r02":
         units = {"train": "step", "cifar": "step", "pinn": "step", "dps": "nfe"}
         for mode, unit in units.items():
@@ -105,7 +122,8 @@ def main():
                                    "fetch_bytes_x2": 2048.0 * f, "write_bytes": 1024.0 * w,
                                    "dispatches": [nf, nw],
                                    "note": f"all kernels of one bench {mode} {unit} "
-                                           "(tools/prof_steps.py markers)"}
+                                           "(tools/prof_steps.py markers)",
+                                   **provenance("step")}
     out["_note"] = (f"rocprofv3 --pmc passes (tools/gpu_pmc_{TAG}.sh over tools/prof_r02.py); "
                     "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB -> bytes")
     json.dump(out, open(os.path.join(REPO, "profiles", f"{TAG}_pmc_traffic.json"), "w"), indent=1)
@@ -123,7 +141,7 @@ def main():
         "waves": waves}
     sq["wino_pre_stats 128->128@128 B=16 (one dispatch)"] = last
     nsq = load(pdir("ns", "sq"), ns)
-    sq["ns_step launches (3 full steps)"] = nsq
+    sq["ns_step launches (3 full steps)"] = {"runs": nsq, **provenance("ns_step", nsq)}
     sq["_note"] = ("SQ_* wave counters in quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES (cycles, = 32 per "
                    "v_mfma_f32_16x16x4_f32); GRBM_GUI_ACTIVE summed over the 8 XCDs; MFMA busy "
                    "fraction = MFMA busy cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)")
