@@ -329,13 +329,6 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
     step starts with zero_grad).  Under batch sharding the averaged gradient carries any
     rank's NaN, so every rank takes the same decision."""
 
-    if graph:
-        # round 2-3: the captured step's replays stopped matching the eager step after
-        # optimizer steps / eager allocations between replays, root cause not isolated
-        # (DESIGN.md section 8); the product path is the eager step
-        raise NotImplementedError("get_pinn_step_fn(graph=True): hipGraph replay of the PINN "
-                                  "step is not supported (DESIGN.md section 8)")
-
     def loss_fn(model, operator, batch):
         f1, f2, x, y, t, target = batch
         f1 = _observe(config, operator, f1)
@@ -349,6 +342,9 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
         pinn_loss = (residual(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
                      * config.training.pinn_loss_weight)
         return pinn_loss + data_loss, pinn_loss, data_loss
+
+    if graph and train:
+        return _PinnGraphStep(loss_fn, optimize_fn, ctx)
 
     bucketer = [None]  # eager + sharded: gradient buckets all-reduced during backward
 
@@ -386,3 +382,102 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
         return loss, pinn_loss, data_loss
 
     return step_fn
+
+
+class _MaskOperator:
+    """The inpainting operator on a static device mask (keep_shape form, the one the PINN
+    observation uses): what a captured step reads, refilled before every replay."""
+
+    def __init__(self, mask):
+        self.mask = mask
+
+    def __call__(self, x, keep_shape=True, invert=False):
+        assert keep_shape
+        return (1 - self.mask) * x if invert else self.mask * x
+
+
+class _PinnGraphStep:
+    """get_pinn_step_fn(graph=True): the forward (both nets, the residual's first and second
+    derivatives) and the backward of one PINN train step as ONE hipGraph, replayed per step;
+    the NaN-gradient skip, both Adam steps and the EMA update run eagerly after it (a handful
+    of fused launches).  The eager step is ~9.4 k launches, host-bound at every batch size.
+
+    What the capture needs, and round 3's withdrawn attempt lacked:
+      * static inputs: the batch tensors and the observation mask are copied into buffers the
+        graph owns before each replay.  The eager operator moves its CPU mask to the device
+        inside the call (a host-to-device copy from a pageable tensor that the next
+        operator.next() frees), so a captured step read a dead host buffer;
+      * gradients: .grad is None when the graph is captured, so autograd allocates it from
+        the graph's pool and every replay rewrites it in place (no zero_grad while replaying:
+        setting .grad to None would detach the parameters from the graph's buffers);
+      * native kernels only inside the graph (op.conv.native_only: no MIOpen convs, no
+        library workspace state), the conv choices made eagerly during the warm-up.
+    The noise of the observation is drawn inside the graph (philox offsets advance per
+    replay).  Sharded (ctx): gradients are averaged with one all-reduce per step after the
+    replay.  Reference losses.py:332-386."""
+
+    def __init__(self, loss_fn, optimize_fn, ctx):
+        self.loss_fn, self.optimize_fn, self.ctx = loss_fn, optimize_fn, ctx
+        self.graph = None
+        self.key = None
+
+    def _capture(self, model, operator, batch):
+        from op import conv as conv_op
+        dev = batch[0].device
+        self.static = [b.detach().clone() for b in batch]
+        for i, b in enumerate(batch):
+            if b.requires_grad:
+                self.static[i].requires_grad_(True)
+        self.mask = operator.mask.to(dev).clone()
+        sop = _MaskOperator(self.mask)
+        params = list(model.parameters())
+        with conv_op.native_only():
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(2):  # kernel choices, allocator, lazy state: off the capture
+                    for p in params:
+                        p.grad = None
+                    loss, _pl, _dl = self.loss_fn(model, sop, self.static)
+                    loss.backward()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize(dev)
+            for p in params:
+                p.grad = None
+            g = torch.cuda.CUDAGraph()
+            # captured on the warm-up stream: the parameters' AccumulateGrad nodes (created
+            # in the warm-up) record that stream
+            with torch.cuda.graph(g, stream=s):
+                loss, pl, dl = self.loss_fn(model, sop, self.static)
+                loss.backward()
+        self.out = (loss, pl, dl)
+        self.graph = g
+        self.params = params
+        self.key = (id(model), tuple((b.shape, b.dtype) for b in batch))
+
+    def __call__(self, state, operator, batch):
+        model = state["model"]
+        operator.next()
+        opt_flow, opt_pres = state["optimizer"]
+        model.train()
+        key = (id(model), tuple((b.shape, b.dtype) for b in batch))
+        if self.graph is None or key != self.key:
+            self._capture(model, operator, batch)
+        with torch.no_grad():
+            for d, b in zip(self.static, batch):
+                d.copy_(b)
+            m = operator.mask
+            self.mask.copy_(m if m.device == self.mask.device else m.to(self.mask.device))
+        self.graph.replay()
+        _sync_grads(self.params, self.ctx)
+        w = model.pressurenet.end[-1].weight
+        loss, pinn_loss, data_loss = (t.detach().clone() for t in self.out)
+        if w.grad is not None and torch.isnan(w.grad).any():
+            print(">>> Nan Grad Detected <<<")
+            return loss, pinn_loss, data_loss
+        self.optimize_fn(opt_flow, model.flownet.parameters(), step=state["step"])
+        self.optimize_fn(opt_pres, model.pressurenet.parameters(), step=state["step"])
+        state["step"] += 1
+        state["ema"].update(model.parameters())
+        return loss, pinn_loss, data_loss
+

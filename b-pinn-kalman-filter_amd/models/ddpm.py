@@ -93,8 +93,8 @@ class DDPM(nn.Module):
         mods = self.all_modules
         if self.conditional:
             temb = layers.get_timestep_embedding(labels, self.nf)
-            temb = mods[0](temb)
-            temb = mods[1](self.act(temb))
+            temb = layers.dense(mods[0], temb)
+            temb = layers.dense(mods[1], self.act(temb))
         else:
             temb = None
         fused = layers._DDPM_FUSED and layers.fused_inference_ok(self, x, self.act)

@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from op import conv as conv_op
+from op import matmul as matmul_op
 from op import norm_act as norm_act_op
 from op.norm_act import ACT_NONE, ACT_SILU, group_norm_act, group_norm_affine, residual_rescale
 
@@ -27,6 +28,14 @@ def get_act(config):
     if name not in table:
         raise NotImplementedError("activation function does not exist!")
     return table[name]()
+
+
+def dense(m: nn.Linear, x):
+    """m(x) for an nn.Linear: the native GEMM on HIP tensors (op.matmul.linear, forward and
+    gradients), nn.Linear itself elsewhere."""
+    if x.is_cuda and matmul_op.supported(x, m.weight, m.bias):
+        return matmul_op.linear(x, m.weight, m.bias)
+    return m(x)
 
 
 class TembBank:
@@ -43,18 +52,20 @@ class TembBank:
             off += d.out_features
         w = torch.cat([d.weight for d in denses], 0)
         b = torch.cat([d.bias for d in denses], 0)
-        self.all = torch.addmm(b, act(temb), w.t())
+        a = act(temb)
+        self.all = (matmul_op.linear(a, w, b) if a.is_cuda and matmul_op.supported(a, w, b)
+                    else torch.addmm(b, a, w.t()))
 
     def proj(self, dense):
         off, n = self._off[id(dense)]
         return self.all[:, off:off + n]
 
 
-def temb_proj(dense: nn.Linear, act, temb):
+def temb_proj(dense_m: nn.Linear, act, temb):
     """dense(act(temb)) -- a TembBank slice when the forward built one."""
     if isinstance(temb, TembBank):
-        return temb.proj(dense)
-    return dense(act(temb))
+        return temb.proj(dense_m)
+    return dense(dense_m, act(temb))
 
 
 def gn_act(x, gn: nn.GroupNorm, act=None, bias_nc=None):
@@ -250,9 +261,12 @@ class NIN(nn.Module):
         self.b = nn.Parameter(torch.zeros(num_units), requires_grad=True)
 
     def forward(self, x):
-        # 1x1 convolution with weight W^T: one GEMM on MFMA via the BLAS library
-        w = self.W.t()[:, :, None, None]
-        return F.conv2d(x, w, self.b)
+        # 1x1 convolution with weight W^T: the MFMA GEMM kernels (forward and every
+        # derivative, op.conv.conv1x1_ad) on HIP tensors
+        w = self.W.t()
+        if _GEMM1X1 and x.is_cuda and conv_op.conv1x1_train_supported(x, w):
+            return conv_op.conv1x1_ad(x, w, self.b)
+        return F.conv2d(x, w[:, :, None, None], self.b)
 
 
 def _attention(h, nin_q, nin_k, nin_v):
@@ -261,9 +275,10 @@ def _attention(h, nin_q, nin_k, nin_v):
     q = nin_q(h).reshape(B, C, H * W)
     k = nin_k(h).reshape(B, C, H * W)
     v = nin_v(h).reshape(B, C, H * W)
-    w = torch.bmm(q.transpose(1, 2), k) * (int(C) ** (-0.5))  # [B, HW(q), HW(k)]
+    mm = matmul_op.bmm_ad if h.is_cuda and matmul_op.supported(h) else torch.bmm
+    w = mm(q.transpose(1, 2), k) * (int(C) ** (-0.5))  # [B, HW(q), HW(k)]
     w = torch.softmax(w, dim=-1)
-    out = torch.bmm(v, w.transpose(1, 2))  # [B, C, HW(q)]
+    out = mm(v, w.transpose(1, 2))  # [B, C, HW(q)]
     return out.reshape(B, C, H, W)
 
 

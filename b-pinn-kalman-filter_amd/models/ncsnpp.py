@@ -195,8 +195,8 @@ class NCSNpp(nn.Module):
             used_sigmas = None
             temb = layers.get_timestep_embedding(time_cond, self.nf)
         if self.conditional:
-            temb = mods[self._dense_idx[0]](temb)
-            temb = mods[self._dense_idx[1]](self.act(temb))
+            temb = layers.dense(mods[self._dense_idx[0]], temb)
+            temb = layers.dense(mods[self._dense_idx[1]], self.act(temb))
         else:
             temb = None
         return temb, used_sigmas

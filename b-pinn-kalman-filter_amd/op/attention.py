@@ -27,6 +27,10 @@ def attention(qkv, scale):
     qkv = qkv.detach().contiguous()
     B, _, C, P = qkv.shape
     out = torch.empty((B, C, P), dtype=torch.float32, device=qkv.device)
-    check(lib.bpk_attention_f32(qkv.data_ptr(), out.data_ptr(), B, C, P, float(scale),
-                                stream_ptr(qkv.device)), "attention")
+    # key splits (partials + a combine launch) when the batch is too small to fill the chip
+    nws = lib.bpk_attention_workspace_bytes(B, C, P)
+    ws = torch.empty(nws // 4, dtype=torch.float32, device=qkv.device) if nws > 0 else None
+    check(lib.bpk_attention_ex_f32(qkv.data_ptr(), out.data_ptr(),
+                                   None if ws is None else ws.data_ptr(), B, C, P, float(scale),
+                                   stream_ptr(qkv.device)), "attention")
     return out

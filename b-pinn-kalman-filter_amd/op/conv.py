@@ -426,6 +426,20 @@ def _save_table():
 
 
 _LOCAL_ONLY = [False]
+_NATIVE_ONLY = [False]
+
+
+@contextlib.contextmanager
+def native_only():
+    """Inside this block the igemm-vs-MIOpen choices take the implicit-GEMM kernel (the choices
+    among native kernels stay timed): a step captured in a hipGraph (the PINN step,
+    losses.get_pinn_step_fn(graph=True)) then holds only libbpk / aten kernels and no MIOpen
+    workspace or find-db state."""
+    prev, _NATIVE_ONLY[0] = _NATIVE_ONLY[0], True
+    try:
+        yield
+    finally:
+        _NATIVE_ONLY[0] = prev
 
 
 @contextlib.contextmanager
@@ -496,7 +510,7 @@ def _pick_any(key, cands):
 
 def _pick(key, run_ig, run_mi):
     """run_ig() or run_mi(), whichever the cached per-key timing says is faster (ties: igemm)."""
-    if _IG_MODE == "2":
+    if _IG_MODE == "2" or _NATIVE_ONLY[0]:
         return run_ig()
     c = _decide(key, [run_ig, run_mi])
     return run_mi() if c == 1 else run_ig()

@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--pinn-steps", type=int, default=10)
     ap.add_argument("--pinn-warmup", type=int, default=2)
     ap.add_argument("--no-pinn", action="store_true")
+    ap.add_argument("--pinn-eager", action="store_true",
+                    help="time the eager PINN step instead of its hipGraph replay")
     ap.add_argument("--dps-steps", type=int, default=2, help="accepted RK45 steps timed")
     ap.add_argument("--no-dps", action="store_true")
     ap.add_argument("--ns-steps", type=int, default=20, help="ns_step full steps timed; 0: skip")
@@ -792,14 +794,17 @@ def _pinn_run(args, ctx, dev):
     opt_f = losses.get_optimizer(c, model.flownet.parameters())
     opt_p = losses.get_optimizer(c, model.pressurenet.parameters(), 0.005)
     state = dict(optimizer=(opt_f, opt_p), model=model, ema=ema, step=c.training.n_iters)
-    step_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
-                                      ctx=ctx)
+    eager_fn = losses.get_pinn_step_fn(c, train=True, optimize_fn=losses.optimization_manager(c),
+                                       ctx=ctx)
+    step_fn = eager_fn if args.pinn_eager else losses.get_pinn_step_fn(
+        c, train=True, optimize_fn=losses.optimization_manager(c), ctx=ctx, graph=True)
     operator = get_operator(c)
     B = shard(args, ctx.world_size, c.training.batch_size)
     batch = pinn_batch(c, B, dev, seed=ctx.rank)
-    for _ in range(args.pinn_warmup):
+    # FLOPs of one step: counted on an eager step (a graph replay launches nothing from Python)
+    tally, _ = counted(lambda: eager_fn(state, operator, batch), dev)
+    for _ in range(args.pinn_warmup):  # the first graph-mode call captures the step
         step_fn(state, operator, batch)
-    tally, _ = counted(lambda: step_fn(state, operator, batch), dev)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
@@ -819,7 +824,8 @@ def bench_pinn(args, ctx, dev):
     grid_sample grad2 and the InstanceNorm+ELU double backward on HIP --, backward, two
     Adams, EMA) at pinn_pde, global batch 64 sharded over the ranks, 64x64; gradients averaged
     over ranks with RCCL.
-    Eager (the hipGraph replay of this step was withdrawn)."""
+    The step's forward + backward replayed from one hipGraph (losses.get_pinn_step_fn(
+    graph=True)); --pinn-eager times the eager step."""
     dt, losses_, tally, B = _pinn_run(args, ctx, dev)
     roof = None
     if tally is not None:
@@ -831,7 +837,7 @@ def bench_pinn(args, ctx, dev):
                               "images, ~10k kernels), so frac is low by construction")
     return {"roofline_pinn": roof, "pinn_train_steps_per_s": round(args.pinn_steps / dt, 3),
             "pinn_ms_per_step": round(dt / args.pinn_steps * 1e3, 2),
-            "pinn_mode": "eager",
+            "pinn_mode": "eager" if args.pinn_eager else "hip_graph",
             "pinn_global_batch": B * ctx.world_size,
             "pinn_losses": [round(float(v.item()), 6) for v in losses_],
             "pinn_config": "configs[3]: pinn_pde (FlowNet 2.49M + PressureNet 7.54M), 64x64"}

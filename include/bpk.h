@@ -446,6 +446,17 @@ int64_t bpk_gemm_nchw_splitk_bytes(int N, int M, int P, int K1, int K2);
 int bpk_gemm_nchw_splitk_f32(const float* W, int ldw, const float* X1, int K1, const float* X2,
                              int K2, const float* bias, float* Y, float* workspace, int N, int M,
                              int P, void* stream);
+/* Strided batched GEMM on the f32 MFMA: C(b, m, n) = alpha * sum_k A(b, m, k) B(b, k, n)
+ * (+ bias[n] for bias_mode 1, bias[m] for 2; accumulate != 0: C += instead of C =), each operand
+ * addressed by element strides (A(b, m, k) = A[b sab + m sam + k sak], ...), so transposes
+ * are strides, not copies.  Replaces the rocBLAS / hipBLASLt GEMMs behind nn.Linear (the
+ * time-embedding MLP and Dense_0 projections, reference models/ncsnpp.py:86-89,
+ * layerspp.py:232-262) and torch.bmm in the attention block under autograd (reference
+ * layerspp.py:84-88), forward and both gradients.  Deterministic. */
+int bpk_gemm_sb_f32(const float* A, int64_t sab, int64_t sam, int64_t sak, const float* B,
+                    int64_t sbb, int64_t sbk, int64_t sbn, float* C, int64_t scb, int64_t scm,
+                    int64_t scn, const float* bias, int bias_mode, float alpha, int accumulate,
+                    int batch, int M, int N, int K, void* stream);
 
 /* Channel self-attention of the score networks' attention blocks at inference, one kernel:
  *   out[b, c, i] = sum_j V[b, c, j] softmax_j(scale * sum_c' Q[b, c', i] K[b, c', j])
@@ -455,6 +466,14 @@ int bpk_gemm_nchw_splitk_f32(const float* W, int ldw, const float* X1, int K1, c
  * supported(): C % 32 == 0, P in {64, 128, 256}. */
 int bpk_attention_supported(int B, int C, int P);
 int bpk_attention_f32(const float* qkv, float* out, int B, int C, int P, float scale, void* stream);
+/* Same, with the keys split over up to 4 workgroups per query block when B x P / 64
+ * workgroups would leave most CUs idle (the per-GPU batch of a batch-sharded run: B = 8 ->
+ * 32 workgroups at 16^2): each split's unnormalised partial output and row statistics go to
+ * `workspace` (workspace_bytes(), 0 = no split: workspace may be NULL) and a combine launch
+ * merges them in a fixed order. */
+int64_t bpk_attention_workspace_bytes(int B, int C, int P);
+int bpk_attention_ex_f32(const float* qkv, float* out, float* workspace, int B, int C, int P,
+                         float scale, void* stream);
 
 /* Weight / bias gradient of that 1x1 conv (replaces the conv2d backward-weights MIOpen
  * runs for the reference's nn.Conv2d 1x1 layers -- ddpm_conv1x1 (models/layers.py:96), the

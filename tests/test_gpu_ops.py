@@ -1162,11 +1162,15 @@ def test_instance_norm_elu_residual_block_matches_aten(hip, monkeypatch):
 
 
 @pytest.mark.parametrize("B,C,P,scale", [(3, 256, 256, 1.0), (2, 64, 256, 0.125), (2, 32, 128, 0.3),
-                                         (5, 96, 64, 1.0 / 96 ** 0.5)])
+                                         (5, 96, 64, 1.0 / 96 ** 0.5), (64, 256, 256, 1 / 16),
+                                         (8, 256, 256, 1 / 16)])
 def test_fused_attention_matches_fp32_reference(hip, B, C, P, scale):
     """csrc/attention.hip (q^T k logits, row softmax and the PV product in one kernel) vs the
-    reference's bmm + softmax + bmm in float64 (1e-5 relative to max|ref|)."""
-    from op.attention import attention
+    reference's bmm + softmax + bmm in float64 (1e-5 relative to max|ref|): one workgroup per
+    64 queries (B = 64, P = 64) and the key-split form with its combine launch (the small
+    batches: 2 or 4 splits)."""
+    from op.attention import attention, lib
+    assert (lib.bpk_attention_workspace_bytes(B, C, P) > 0) == (B * P // 64 <= 128 and P >= 128)
     g = torch.Generator().manual_seed(B * C + P)
     qkv = torch.randn(B, 3, C, P, generator=g) * 0.5
     q, k, v = qkv[:, 0].double(), qkv[:, 1].double(), qkv[:, 2].double()
@@ -1357,3 +1361,80 @@ def test_upfirdn2d_fir_pad2_asymmetric_taps(hip, hw):
     ref = upfirdn2d_np(x.numpy(), k, (1, 1), (1, 1), (2, 2, 2, 2))
     assert y.shape == ref.shape == (37, 1, H + 1, W + 1)
     np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ strided batched GEMM
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("batch,M,N,K", [(3, 37, 70, 19), (2, 256, 256, 256), (1, 64, 512, 128)])
+def test_gemm_sb_strided_operands_vs_fp64(hip, ta, tb, batch, M, N, K):
+    """bpk_gemm_sb_f32 with every transpose combination read through strides (no copies),
+    ragged tiles, bias per column / per row and accumulation, vs float64 (1e-5 relative)."""
+    from op.matmul import gemm_sb
+    g = torch.Generator().manual_seed(batch * 7 + M + N + K)
+    a = torch.randn(batch, K, M, generator=g).transpose(1, 2) if ta else torch.randn(batch, M, K, generator=g)
+    b = torch.randn(batch, N, K, generator=g).transpose(1, 2) if tb else torch.randn(batch, K, N, generator=g)
+    bn, bm = torch.randn(N, generator=g), torch.randn(M, generator=g)
+    ref = torch.bmm(a.double(), b.double())
+    scale = ref.abs().max().item()
+    ad, bd = a.to(hip), b.to(hip)
+    out = gemm_sb(ad, bd).cpu()
+    assert (out.double() - ref).abs().max().item() <= 1e-5 * scale
+    out = gemm_sb(ad, bd, bn.to(hip), 1, alpha=0.5).cpu()
+    assert (out.double() - (0.5 * ref + bn.double())).abs().max().item() <= 1e-5 * scale
+    c0 = torch.randn(batch, M, N, generator=g)
+    acc = gemm_sb(ad, bd, bm.to(hip), 2, out=c0.to(hip)).cpu()
+    want = c0.double() + ref + bm.double()[:, None]
+    assert (acc.double() - want).abs().max().item() <= 1e-5 * want.abs().max().item()
+
+
+def test_linear_native_gradients_vs_fp64(hip):
+    """op.matmul.linear (nn.Linear on the native GEMM: the time-embedding MLP / Dense_0) --
+    output, first and second derivatives w.r.t. x, W, b vs float64 torch (2e-5 relative)."""
+    from op.matmul import linear
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.randn(6, 4, 96, generator=g)
+    w0 = torch.randn(160, 96, generator=g) / 10
+    b0 = torch.randn(160, generator=g)
+    go = torch.randn(6, 4, 160, generator=g)
+
+    def run(fn, dev, dt):
+        x, w, b = (t.to(dev, dt).requires_grad_() for t in (x0, w0, b0))
+        y = fn(x, w, b)
+        gx, gw, gb = torch.autograd.grad(y, (x, w, b), go.to(dev, dt), create_graph=True)
+        s = (gx ** 2).sum() + (gw * gw.detach()).sum()
+        hx, hw = torch.autograd.grad(s, (x, w))
+        return [t.detach().double().cpu() for t in (y, gx, gw, gb, hx, hw)]
+    got = run(linear, hip, torch.float32)
+    ref = run(torch.nn.functional.linear, "cpu", torch.float64)
+    for a, r in zip(got, ref):
+        assert (a - r).abs().max().item() <= 2e-5 * r.abs().max().item()
+
+
+def test_attention_block_training_on_native_gemm(hip, monkeypatch):
+    """AttnBlockpp under autograd (training / DPS): q^T k and v w^T with their gradients on
+    the native GEMM equal the torch.bmm path (output and gradients w.r.t. x and the NIN
+    weights, 1e-5 relative)."""
+    import models.layerspp as lpp
+    from op import matmul
+    g = torch.Generator().manual_seed(8)
+    blk = lpp.AttnBlockpp(128, skip_rescale=True, init_scale=0.1).to(hip).train()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn(p.shape, generator=g).to(hip) * 0.05)
+    x0 = torch.randn(3, 128, 16, 16, generator=g).to(hip)
+    go = torch.randn(3, 128, 16, 16, generator=g).to(hip)
+
+    def run():
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        grads = torch.autograd.grad(y, [x] + [blk.NIN_0.W, blk.NIN_1.W, blk.NIN_2.W], go)
+        return [y.detach()] + list(grads)
+    calls = []
+    real = matmul.gemm_sb
+    monkeypatch.setattr(matmul, "gemm_sb", lambda *a, **k: calls.append(1) or real(*a, **k))
+    got = run()
+    assert len(calls) >= 6, "the attention GEMMs did not run on the native kernel"
+    monkeypatch.setattr(matmul, "supported", lambda *t: False)
+    ref = run()
+    for a, r in zip(got, ref):
+        assert (a - r).abs().max().item() <= 1e-5 * r.abs().max().item()

@@ -270,3 +270,72 @@ def test_stencil_residual_matches_cpu_oracle(hip):
                                           pres.detach().cpu().numpy(), u_t.cpu().numpy(),
                                           v_t.cpu().numpy(), h, Re)
         assert abs(float(val) - ref) <= 1e-5 * abs(ref), (Re, float(val), ref)
+
+
+def test_pinn_step_hip_graph_replays_match_eager(hip):
+    """get_pinn_step_fn(graph=True): the forward + residual derivatives + backward captured
+    once and replayed for 8 steps (new batch and observation mask each step, optimizer steps
+    and EMA in between) == the eager step from the same state on the configs[3] 64x64
+    network: losses at every step and the final parameters / EMA (1e-5 relative; both under
+    op.conv.native_only, so the same kernels run).  Observation noise off (variance 0) so the
+    two runs draw nothing random."""
+    import copy
+
+    import losses
+    from configs.pinn import pinn_pde
+    from inverse.operators import InpaintOperator
+    from models.ema import ExponentialMovingAverage
+    from op import conv as conv_op
+    from pinn_kalman.pinn import PINN
+    c = pinn_pde.get_config()
+    c.inverse.variance = 0.0
+    c.device = hip
+    torch.manual_seed(0)
+    m0 = PINN(c)
+    B, n = 4, c.data.image_size
+    g = torch.Generator().manual_seed(1)
+    lin = torch.linspace(0.05, 1.0, n)
+    batches = []
+    for _ in range(8):
+        f1, f2 = torch.rand(B, 1, n, n, generator=g), torch.rand(B, 1, n, n, generator=g)
+        x = lin.view(1, 1, 1, n) + 0.01 * torch.rand(B, 1, n, n, generator=g)
+        y = lin.view(1, 1, n, 1) + 0.01 * torch.rand(B, 1, n, n, generator=g)
+        t = torch.randint(300, 900, (B,), generator=g).float()
+        target = torch.randn(B, 3, n, n, generator=g) * 0.5
+        batches.append([v.to(hip) for v in (f1, f2, x, y, t, target)])
+    masks = [(torch.rand(1, 1, n, n, generator=g) > 0.3).float().expand(B, 1, n, n).contiguous()
+             for _ in range(3)]  # CPU masks, as random_mask_source gives them
+
+    def run(graph):
+        m = copy.deepcopy(m0).to(hip)
+        ema = ExponentialMovingAverage(m.parameters(), decay=c.model.ema_rate)
+        state = dict(optimizer=(losses.get_optimizer(c, m.flownet.parameters()),
+                                losses.get_optimizer(c, m.pressurenet.parameters(), 0.005)),
+                     model=m, ema=ema, step=c.training.n_iters)
+        step_fn = losses.get_pinn_step_fn(c, train=True, graph=graph,
+                                          optimize_fn=losses.optimization_manager(c))
+        op = InpaintOperator(mask=masks)
+        out = []
+        with conv_op.native_only():
+            for bt in batches:
+                x, y, t = (v.clone().requires_grad_() for v in bt[2:5])
+                out.append([float(v.detach()) for v in step_fn(state, op, (bt[0], bt[1], x, y, t, bt[5]))])
+        if graph:
+            assert step_fn.graph is not None
+        return out, [p.detach().clone() for p in m.parameters()], \
+            [p.clone() for p in ema.shadow_params], state["step"]
+    lg, pg, eg, sg = run(True)
+    le, pe, ee, se = run(False)
+    assert sg == se
+    lg, le = np.array(lg), np.array(le)  # columns: loss, pinn_loss, data_loss
+    np.testing.assert_allclose(lg[:, [0, 2]], le[:, [0, 2]], rtol=1e-5, atol=0)
+    # the residual term (~1e-5, sums of products of second derivatives) at the residual
+    # tolerance of the fixtures above
+    np.testing.assert_allclose(lg[:, 1], le[:, 1], rtol=2e-3, atol=0)
+    # parameters: grid_sample's backward accumulates with atomics, so two eager runs differ
+    # in the last bits too, and Adam turns the rounding noise of (mathematically) zero
+    # gradients into O(lr) moves; bound the drift by 5e-5 absolute, <1 % of the 8 x lr
+    # (8e-3) an Adam run of 8 steps can move a parameter -- a stale input, mask or
+    # gradient buffer in the replay moves them by O(lr) and breaks the losses above
+    for a, b in zip(pg + eg, pe + ee):
+        assert (a - b).abs().max().item() <= 5e-5
