@@ -55,13 +55,21 @@ class InpaintOperator:
         self._idx = None
 
     def _observed(self, invert):
+        """[B, K] observed-pixel indices of the current mask, computed once per mask (the
+        nonzero / count check syncs with the host; the DPS drift applies the operator at
+        every function evaluation with the same mask)."""
+        key = (invert, id(self.mask), self.mask._version, self.mask.device)
+        if self._idx is not None and self._idx[0] == key:
+            return self._idx[1]
         m = (1 - self.mask) if invert else self.mask
         # one index list per sample; the reference's torch.stack needs equal counts
         flat = m.reshape(m.shape[0], -1)
         idx = [torch.nonzero(row > 0.5, as_tuple=False).squeeze(1) for row in flat]
         if len({int(i.numel()) for i in idx}) != 1:
             raise ValueError("inpaint operator: samples observe different pixel counts")
-        return torch.stack(idx)
+        idx = torch.stack(idx)
+        self._idx = (key, idx, self.mask)  # the mask is kept alive with its key
+        return idx
 
     def __call__(self, x, keep_shape=True, invert=False):
         assert self.mask.shape == x.shape, (self.mask.shape, x.shape)

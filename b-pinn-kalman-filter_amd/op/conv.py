@@ -253,7 +253,7 @@ def conv3x3_small_raw(x, weight, bias=None, pre=None):
 
 
 # ------------------------------------------------ general convolutions on the MFMA (igemm)
-_IGEMM = os.environ.get("BPK_IGEMM", "1") != "0"  # 0: MIOpen for the shapes below
+_IGEMM = True  # the implicit-GEMM kernels for the shapes below (False: MIOpen only)
 
 
 def _pair(v):
@@ -361,8 +361,7 @@ def conv2d_weight_igemm_raw(x, wshape, gy, stride=1, padding=0, bias_grad=False)
 # (no NHWC transposes, no per-call solver search on the host), MIOpen's Winograd solvers on
 # big 3x3 convs at 8x8+ (tools/bench_igemm.py, profiles/r02_igemm_shapes.jsonl).  The first
 # eager call of each (op, shapes) times both once and caches the faster; under graph
-# capture an unseen call takes the implicit-GEMM kernel.  BPK_IGEMM=2: always igemm.
-_IG_MODE = os.environ.get("BPK_IGEMM", "1")
+# capture an unseen call takes the implicit-GEMM kernel (native_only(): always igemm).
 _CHOICE: dict = {}        # agreed choices (broadcast from rank 0 under torch.distributed)
 _CHOICE_LOCAL: dict = {}  # choices made inside local_choices(): this rank's own, never agreed
 
@@ -387,7 +386,7 @@ _SEL3_MAX_HW = 32 * 32
 
 
 def _small_img(x):
-    return _SEL3 and _IG_MODE != "0" and x.shape[2] * x.shape[3] <= _SEL3_MAX_HW
+    return _SEL3 and _IGEMM and x.shape[2] * x.shape[3] <= _SEL3_MAX_HW
 
 
 # Reproducibility of the per-call choice (the timing is noisy, so two runs -- or two ranks --
@@ -510,7 +509,7 @@ def _pick_any(key, cands):
 
 def _pick(key, run_ig, run_mi):
     """run_ig() or run_mi(), whichever the cached per-key timing says is faster (ties: igemm)."""
-    if _IG_MODE == "2" or _NATIVE_ONLY[0]:
+    if _NATIVE_ONLY[0]:
         return run_ig()
     c = _decide(key, [run_ig, run_mi])
     return run_mi() if c == 1 else run_ig()

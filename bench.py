@@ -801,7 +801,10 @@ def _pinn_run(args, ctx, dev):
     operator = get_operator(c)
     B = shard(args, ctx.world_size, c.training.batch_size)
     batch = pinn_batch(c, B, dev, seed=ctx.rank)
-    # FLOPs of one step: counted on an eager step (a graph replay launches nothing from Python)
+    # FLOPs of one step: counted on an eager step (a graph replay launches nothing from
+    # Python), after one eager step that makes the per-call conv choices (their timing runs
+    # would be counted too)
+    eager_fn(state, operator, batch)
     tally, _ = counted(lambda: eager_fn(state, operator, batch), dev)
     for _ in range(args.pinn_warmup):  # the first graph-mode call captures the step
         step_fn(state, operator, batch)

@@ -334,8 +334,10 @@ def test_pinn_step_hip_graph_replays_match_eager(hip):
     np.testing.assert_allclose(lg[:, 1], le[:, 1], rtol=2e-3, atol=0)
     # parameters: grid_sample's backward accumulates with atomics, so two eager runs differ
     # in the last bits too, and Adam turns the rounding noise of (mathematically) zero
-    # gradients into O(lr) moves; bound the drift by 5e-5 absolute, <1 % of the 8 x lr
-    # (8e-3) an Adam run of 8 steps can move a parameter -- a stale input, mask or
-    # gradient buffer in the replay moves them by O(lr) and breaks the losses above
+    # gradients -- the conv biases in front of an InstanceNorm -- into sign-random moves of
+    # up to lr per step in either run; the losses above are the tight check (each depends on
+    # every earlier update), the parameters are bounded by 10 % of the 8 x 5e-3 an 8-step Adam
+    # run can move a PressureNet parameter: a stale input, mask or gradient buffer moves
+    # every parameter by O(lr) per step
     for a, b in zip(pg + eg, pe + ee):
-        assert (a - b).abs().max().item() <= 5e-5
+        assert (a - b).abs().max().item() <= 4e-3
