@@ -253,9 +253,11 @@ class GradBucketer:
             h.remove()
 
 
-def _observe(config, operator, f):
-    """inpainting measurement + Gaussian noise of variance config.inverse.variance."""
-    return operator(f, keep_shape=True) + torch.randn_like(f) * config.inverse.variance ** 0.5
+def _observe(config, operator, f, noise=None):
+    """inpainting measurement + Gaussian noise of variance config.inverse.variance (`noise`:
+    the standard-normal draw, else torch.randn_like(f))."""
+    z = torch.randn_like(f) if noise is None else noise
+    return operator(f, keep_shape=True) + z * config.inverse.variance ** 0.5
 
 
 def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
@@ -329,10 +331,10 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
     step starts with zero_grad).  Under batch sharding the averaged gradient carries any
     rank's NaN, so every rank takes the same decision."""
 
-    def loss_fn(model, operator, batch):
+    def loss_fn(model, operator, batch, noise=(None, None)):
         f1, f2, x, y, t, target = batch
-        f1 = _observe(config, operator, f1)
-        f2 = _observe(config, operator, f2)
+        f1 = _observe(config, operator, f1, noise[0])
+        f2 = _observe(config, operator, f2, noise[1])
         flow_pred, pres_pred = model(f1, f2, x, y, t)
         data_loss = (model.flownet.multiscale_data_mse(flow_pred, target)
                      + model.pressurenet.data_mse(pres_pred, target))
@@ -412,9 +414,11 @@ class _PinnGraphStep:
         setting .grad to None would detach the parameters from the graph's buffers);
       * native kernels only inside the graph (op.conv.native_only: no MIOpen convs, no
         library workspace state), the conv choices made eagerly during the warm-up.
-    The noise of the observation is drawn inside the graph (philox offsets advance per
-    replay).  Sharded (ctx): gradients are averaged with one all-reduce per step after the
-    replay.  Reference losses.py:332-386."""
+    The observation noise is drawn eagerly into static buffers before each replay (the same
+    draws, in the same order, as the eager step's two randn_like calls; a draw captured in
+    the graph returned garbage on this stack -- data loss 32.6 vs 3.5, residual NaN).
+    Sharded (ctx): gradients are averaged with one all-reduce per step after the replay.
+    Reference losses.py:332-386."""
 
     def __init__(self, loss_fn, optimize_fn, ctx):
         self.loss_fn, self.optimize_fn, self.ctx = loss_fn, optimize_fn, ctx
@@ -429,6 +433,7 @@ class _PinnGraphStep:
             if b.requires_grad:
                 self.static[i].requires_grad_(True)
         self.mask = operator.mask.to(dev).clone()
+        self.noise = (torch.zeros_like(self.static[0]), torch.zeros_like(self.static[1]))
         sop = _MaskOperator(self.mask)
         params = list(model.parameters())
         with conv_op.native_only():
@@ -438,7 +443,7 @@ class _PinnGraphStep:
                 for _ in range(2):  # kernel choices, allocator, lazy state: off the capture
                     for p in params:
                         p.grad = None
-                    loss, _pl, _dl = self.loss_fn(model, sop, self.static)
+                    loss, _pl, _dl = self.loss_fn(model, sop, self.static, self.noise)
                     loss.backward()
             torch.cuda.current_stream(dev).wait_stream(s)
             torch.cuda.synchronize(dev)
@@ -448,7 +453,7 @@ class _PinnGraphStep:
             # captured on the warm-up stream: the parameters' AccumulateGrad nodes (created
             # in the warm-up) record that stream
             with torch.cuda.graph(g, stream=s):
-                loss, pl, dl = self.loss_fn(model, sop, self.static)
+                loss, pl, dl = self.loss_fn(model, sop, self.static, self.noise)
                 loss.backward()
         self.out = (loss, pl, dl)
         self.graph = g
@@ -468,6 +473,8 @@ class _PinnGraphStep:
                 d.copy_(b)
             m = operator.mask
             self.mask.copy_(m if m.device == self.mask.device else m.to(self.mask.device))
+            for z in self.noise:
+                z.normal_()
         self.graph.replay()
         _sync_grads(self.params, self.ctx)
         w = model.pressurenet.end[-1].weight

@@ -56,6 +56,10 @@ def parse():
                     help="configs[2] global batch, sharded global/N per GPU (strong scaling)")
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling: every rank runs the whole global batch of every phase")
+    ap.add_argument("--per-rank-of", type=int, default=None, metavar="N",
+                    help="run every phase at the per-rank batch of an N-GPU strong-scaled run, "
+                         "on this process's GPU(s) (--per-rank-of 8 on one GPU: the work of each "
+                         "rank of the 8-GPU point); the line reports this process's rates")
     ap.add_argument("--batch", type=int, default=None,
                     help="explicit per-GPU batch of the sampler / DSM / PINN / nc_ddpmpp phases "
                          "(weak scaling; e.g. --batch 8 at N=1 is the per-rank work of N=8)")
@@ -99,6 +103,8 @@ def shard(args, world, global_b, explicit=True):
         return args.batch
     if args.weak:
         return global_b
+    if args.per_rank_of:
+        world = world * args.per_rank_of
     if global_b % world:
         raise SystemExit(f"[bench] global batch {global_b} does not shard over {world} ranks")
     return global_b // world
@@ -798,8 +804,9 @@ def _pinn_run(args, ctx, dev):
                                        ctx=ctx)
     step_fn = eager_fn if args.pinn_eager else losses.get_pinn_step_fn(
         c, train=True, optimize_fn=losses.optimization_manager(c), ctx=ctx, graph=True)
-    operator = get_operator(c)
     B = shard(args, ctx.world_size, c.training.batch_size)
+    c.training.batch_size = B  # the per-rank batch: the observation masks are [B, 1, H, W]
+    operator = get_operator(c)
     batch = pinn_batch(c, B, dev, seed=ctx.rank)
     # FLOPs of one step: counted on an eager step (a graph replay launches nothing from
     # Python), after one eager step that makes the per-call conv choices (their timing runs
@@ -1134,6 +1141,7 @@ def main():
                                    f"= {B}/GPU x {world}",
                        "model": "ncsnpp (62.69M params)", "global_batch": B * world,
                        "per_gpu_batch": B,
+                       "per_rank_of_n_gpus": args.per_rank_of,
                        "seq_len": None, "parallelism": f"dp{world} (batch-sharded, RCCL)",
                        "hip_graph": eng.graph is not None,
                        "dist_backend": torch.distributed.get_backend() if world > 1 else None,
