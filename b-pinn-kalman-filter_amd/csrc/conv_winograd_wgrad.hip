@@ -29,7 +29,7 @@ namespace {
 using f4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr int kCB = 32;              // cin per workgroup
-constexpr int kOB = 64;              // cout per workgroup
+constexpr int kOB = 64;              // cout per workgroup per N-block of the waves (NB)
 constexpr int kT = 8;                // tiles per K-chunk (1 tile row x 8 tile cols)
 constexpr int kXR = 4;               // input patch rows
 constexpr int kRec = 20;             // LDS stride of one 16-position record
@@ -56,11 +56,14 @@ constexpr int kXRS = 24;                     // LDS patch row: halo at 3, interi
 constexpr int kXCS = kXR * kXRS + 16;        // per-cin stride (2-way transform reads)
 constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records (644)
 
-__global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ gy,
-                                                                 float* __restrict__ part,
-                                                                 float* __restrict__ part_b,
-                                                                 WgradGeo g, int xcd_remap) {
+// NB = 16-cout blocks per wave: NB = 1 -> 64 couts per workgroup, two workgroups per CU;
+// NB = 2 (Cout % 128 == 0, round 4) -> 128 couts per workgroup, 256 accumulators per lane,
+// one workgroup per CU: the V transform, the patch staging and every A operand read serve
+// twice the couts, and each wave issues 128 MFMAs per barrier instead of 64.
+template <int NB>
+__global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
+    const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ part,
+    float* __restrict__ part_b, WgradGeo g, int xcd_remap) {
   __shared__ __attribute__((aligned(16))) float s_x[2][kCB * kXCS];   // 2 x 14.3 KB
   __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 20.6 KB
 
@@ -73,31 +76,38 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
   const int ob = (int)(b % g.cout_blocks);
   const int cbk = (int)((b / g.cout_blocks) % g.cin_blocks);
   const int split = (int)(b / ((int64_t)g.cout_blocks * g.cin_blocks));
-  const int cin0 = cbk * kCB, cout0 = ob * kOB;
+  const int cin0 = cbk * kCB, cout0 = ob * kOB * NB;
   const int64_t k_begin = g.chunks * split / g.splits;
   const int64_t k_end = g.chunks * (split + 1) / g.splits;
   const int nk = (int)(k_end - k_begin);
   const int plane = g.H * g.W;  // < 2^29 (host check)
 
-  f4 acc[16][2];
+  f4 acc[16][2][NB];
 #pragma unroll
-  for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < 16; ++p)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[p][0][nb] = acc[p][1][nb] = f4{0.f, 0.f, 0.f, 0.f};
   // bias gradient (sum of dy over n, h, w): the cin-block-0 workgroups add up the gradient
   // tiles they load anyway; per-(split, cout) partials, reduced with dw
   const bool want_b = part_b != nullptr && cbk == 0;
-  float bsum = 0.f;
+  float bsum[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) bsum[nb] = 0.f;
   if (nk <= 0) {  // empty K-range: zero partial slabs (no barrier below)
-    const int co = cout0 + 16 * wave + jj;
-    if (want_b && kq == 0) part_b[(int64_t)split * g.Cout + co] = 0.f;
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co = cout0 + 16 * NB * wave + 16 * nb + jj;
+      if (want_b && kq == 0) part_b[(int64_t)split * g.Cout + co] = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        f4* dst = reinterpret_cast<f4*>(
-            part + (((int64_t)split * g.Cin + cin0 + 16 * mb + 4 * kq + r) * g.Cout + co) * 16);
+      for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dst[q] = f4{0.f, 0.f, 0.f, 0.f};
-      }
+        for (int r = 0; r < 4; ++r) {
+          f4* dst = reinterpret_cast<f4*>(
+              part + (((int64_t)split * g.Cin + cin0 + 16 * mb + 4 * kq + r) * g.Cout + co) * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dst[q] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
     return;
   }
 
@@ -190,21 +200,24 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
       dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
   };
 
-  // ---- gradient tiles: lane (kq, jj) of wave w needs, per k-step ks, the 2 x 2 tile
-  // (4 ks + kq) of channel cout0 + 16 w + jj
-  const int gco = cout0 + 16 * wave + jj;
-  float2 gq[2][2];  // [ks][row], one chunk ahead
+  // ---- gradient tiles: lane (kq, jj) of wave w needs, per k-step ks and N-block nb, the
+  // 2 x 2 tile (4 ks + kq) of channel cout0 + 16 NB w + 16 nb + jj
+  const int gco = cout0 + 16 * NB * wave + jj;
+  float2 gq[NB][2][2];  // [nb][ks][row], one chunk ahead
   Strip gcur = strip_at(0);
-  auto load_g = [&](float2 (&dst)[2][2]) {  // gradient tiles of chunk gcur, then advance
+  auto load_g = [&](float2 (&dst)[NB][2][2]) {  // gradient tiles of chunk gcur, then advance
     const Strip s = gcur;
     advance(gcur);
-    const float* src = gy + ((int64_t)s.n * g.Cout + gco) * plane + (int64_t)(2 * s.sy) * g.W +
-                       16 * s.sx;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const float* p = src + 2 * (4 * ks + kq);
-      dst[ks][0] = *reinterpret_cast<const float2*>(p);
-      dst[ks][1] = *reinterpret_cast<const float2*>(p + g.W);
+    for (int nb = 0; nb < NB; ++nb) {
+      const float* src = gy + ((int64_t)s.n * g.Cout + gco + 16 * nb) * plane +
+                         (int64_t)(2 * s.sy) * g.W + 16 * s.sx;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const float* p = src + 2 * (4 * ks + kq);
+        dst[nb][ks][0] = *reinterpret_cast<const float2*>(p);
+        dst[nb][ks][1] = *reinterpret_cast<const float2*>(p + g.W);
+      }
     }
   };
   // Gbar = A dY A^T with A = [[1,0],[1,1],[1,-1],[0,-1]]: 16 values, position 4 i + j
@@ -258,9 +271,13 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
     const float* sv = s_v[SB];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      f4 bq[4];
-      gbar(gq[ks], bq);
-      if (want_b) bsum += (gq[ks][0].x + gq[ks][0].y) + (gq[ks][1].x + gq[ks][1].y);
+      f4 bq[NB][4];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        gbar(gq[nb][ks], bq[nb]);
+        if (want_b)
+          bsum[nb] += (gq[nb][ks][0].x + gq[nb][ks][0].y) + (gq[nb][ks][1].x + gq[nb][ks][1].y);
+      }
       if (ks == 1) load_g(gq);  // chunk j + 1 (both k-steps' tiles consumed)
       const int tile = 4 * ks + kq;
 #pragma unroll
@@ -276,9 +293,11 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
 #pragma unroll
         for (int q = 0; q < 4; ++q) a[q] = as[q];
 #pragma unroll
-        for (int p = 0; p < 16; ++p)
-          acc[p][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p >> 2][p & 3], bq[p >> 2][p & 3],
-                                                            acc[p][mb], 0, 0, 0);
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int p = 0; p < 16; ++p)
+            acc[p][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                a[p >> 2][p & 3], bq[nb][p >> 2][p & 3], acc[p][mb][nb], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -290,23 +309,27 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_pipe_kernel(const float* __
   }
   if (j < nk) step(std::integral_constant<int, 0>{});
 
-  const int co = cout0 + 16 * wave + jj;
-  if (want_b) {  // lanes jj, jj + 16, jj + 32, jj + 48 hold one channel's tiles
-    bsum += __shfl_xor(bsum, 16, 64);
-    bsum += __shfl_xor(bsum, 32, 64);
-    if (kq == 0) part_b[(int64_t)split * g.Cout + co] = bsum;
-  }
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ci = cin0 + 16 * mb + 4 * kq + r;
-      f4* dst = reinterpret_cast<f4*>(part + (((int64_t)split * g.Cin + ci) * g.Cout + co) * 16);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = f4{acc[4 * q][mb][r], acc[4 * q + 1][mb][r], acc[4 * q + 2][mb][r],
-                    acc[4 * q + 3][mb][r]};
+  for (int nb = 0; nb < NB; ++nb) {
+    const int co = gco + 16 * nb;
+    if (want_b) {  // lanes jj, jj + 16, jj + 32, jj + 48 hold one channel's tiles
+      float bs = bsum[nb];
+      bs += __shfl_xor(bs, 16, 64);
+      bs += __shfl_xor(bs, 32, 64);
+      if (kq == 0) part_b[(int64_t)split * g.Cout + co] = bs;
     }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = cin0 + 16 * mb + 4 * kq + r;
+        f4* dst = reinterpret_cast<f4*>(part + (((int64_t)split * g.Cin + ci) * g.Cout + co) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dst[q] = f4{acc[4 * q][mb][nb][r], acc[4 * q + 1][mb][nb][r], acc[4 * q + 2][mb][nb][r],
+                      acc[4 * q + 3][mb][nb][r]};
+      }
+  }
 }
 
 // dw[cout][cin] = G^T (sum_s part[s][cin][cout]) G,  G^T = [[1,.5,.5,0],[0,.5,-.5,0],[0,.5,.5,1]]
@@ -364,18 +387,29 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
   }
 }
 
+// N-blocks per wave: 2 (128 couts per workgroup) when Cout allows it (-DWGRAD_NB1: the
+// round-3 64-cout form everywhere, for A/B variant builds: tools/build_variant.sh)
+#ifdef WGRAD_NB1
+int wgrad_nb(int) { return 1; }
+#else
+int wgrad_nb(int Cout) { return Cout % (2 * kOB) == 0 ? 2 : 1; }
+#endif
+
 WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
   WgradGeo g{};
+  const int nb = wgrad_nb(Cout);
   g.N = N; g.Cin = Cin; g.Cout = Cout; g.H = H; g.W = W;
   g.strips_x = W / 16;
   g.strips_y = H / 2;
   g.cin_blocks = Cin / kCB;
-  g.cout_blocks = Cout / kOB;
+  g.cout_blocks = Cout / (kOB * nb);
   g.chunks = (int64_t)N * g.strips_y * g.strips_x;
-  // ~512 workgroups (two per CU): enough K-splits to fill the chip, no more (each split
-  // adds a [Cin][Cout][16] partial slab to write and re-read)
+  // ~512 resident workgroups' worth (two per CU at NB = 1, one at NB = 2, twice the work
+  // each): enough K-splits to fill the chip, no more (each split adds a [Cin][Cout][16]
+  // partial slab to write and re-read)
   const int64_t tiles = (int64_t)g.cin_blocks * g.cout_blocks;
-  const int64_t want = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+  const int64_t target = nb == 1 ? 512 : 256;
+  const int64_t want = std::max<int64_t>(1, (target + tiles - 1) / tiles);
   g.splits = (int)std::min<int64_t>(want, g.chunks);
   return g;
 }
@@ -414,8 +448,12 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
   float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
-  hipLaunchKernelGGL(wino_wgrad_pipe_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, gy,
-                     workspace, part_b, g, remap);
+  if (wgrad_nb(Cout) == 2)
+    hipLaunchKernelGGL(wino_wgrad_pipe_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, x,
+                       gy, workspace, part_b, g, remap);
+  else
+    hipLaunchKernelGGL(wino_wgrad_pipe_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, x,
+                       gy, workspace, part_b, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
   BPK_REQUIRE(bpk::ceil_div(pairs, 16) < (1LL << 31), "conv3x3_wino_wgrad: too many pairs");

@@ -324,11 +324,14 @@ def test_conv3x3_winograd_backward_and_filter_cache(hip, cin):
 
 
 @pytest.mark.parametrize("N,cin,cout,h,w", [(1, 32, 64, 2, 16), (2, 64, 128, 16, 32),
-                                             (3, 96, 64, 10, 48), (2, 256, 128, 32, 32)])
+                                             (3, 96, 64, 10, 48), (2, 256, 128, 32, 32),
+                                             (1, 32, 128, 2, 16), (4, 128, 256, 64, 64),
+                                             (3, 64, 384, 18, 16)])
 def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
     """Winograd split-K weight gradient vs a float64 direct computation (and MIOpen's fp32
     backward-weights held to the same bound): 2e-5 relative to max|ref|.  Shapes cover one
-    K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths."""
+    K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths, on
+    both workgroup forms (64 couts; 128 couts with two N-blocks per wave when Cout % 128 == 0)."""
     import torch.nn.functional as F
     from op import conv as conv_mod
     from op.conv import conv3x3_wgrad_raw
