@@ -1330,7 +1330,11 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
               kPreMaxCin);
   if (pipe_ok) {
     const int wg = (pre && !skip && CoutP % 128 == 0) ? 8 : 4;
+#ifdef WINO_NO_K16  // variant builds only (tools/build_variant.sh): the 8-cin forms everywhere
+    const bool k16 = false;
+#else
     const bool k16 = CoutP % 128 == 0 && Cin % 16 == 0 && C1 % 16 == 0;
+#endif
     if (k16) {
       WinoGeo gk{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / 128, div, C1, Cout};
       const int64_t items = (int64_t)N * gk.regions_x * gk.regions_y * gk.cout_blocks;
