@@ -53,3 +53,12 @@ def test_gpus_1_runs_in_process():
 def test_mismatched_world_size_is_refused():
     rc, out, err = _run(["--gpus", "1", "--plumbing"], {"WORLD_SIZE": "2", "RANK": "0"})
     assert rc == 2 and "refusing" in err and not out.strip()
+
+
+def test_per_rank_of_gives_the_n_gpu_per_rank_batch():
+    """--per-rank-of 8 on one process: every phase at the per-rank batch of the 8-GPU
+    strong-scaled run (64 / 8 = 8 for configs[2])."""
+    rc, out, err = _run(["--gpus", "1", "--plumbing", "--per-rank-of", "8"])
+    assert rc == 0, err[-2000:]
+    d = json.loads(out.strip().splitlines()[-1])
+    assert d["per_gpu_batch"] == 8 and d["scaling"] == "strong"
