@@ -393,7 +393,7 @@ int num_cus() {
   return g_num_cus;
 }
 
-constexpr int64_t kMaxWorkspace = 16ll << 20;  // split-K partials (bytes): their round trip stays small
+constexpr int64_t kMaxWorkspace = 64ll << 20;  // split-K partials (bytes): their round trip stays small
 
 // geometry, tile and split-K choice; false when the shape is out of range
 bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, int sh, int sw,

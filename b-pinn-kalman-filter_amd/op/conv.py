@@ -5,9 +5,8 @@ on the small-channel VALU kernel (csrc/conv_small.hip) when Cin <= 4 or Cout <= 
 fp32 NCHW HIP tensors whose shape the kernel supports (`supported(...)`).  Backward: the
 input gradient is the same Winograd forward kernel on the flipped, transposed filter and
 the weight gradient the Winograd split-K kernel (csrc/conv_winograd_wgrad.hip) when the
-shapes qualify, MIOpen through torch.nn.grad otherwise (and for double backward).
-BPK_WINO_WGRAD=0 falls back to MIOpen for the weight gradient (Winograd: 2.42 vs 2.83 ms on
-128->128 @128^2, B=64; 1.1-1.2x on every NCSN++ shape, profiles/r01_conv_ab.txt).  The filter
+shapes qualify, else the implicit-GEMM kernels (csrc/conv_igemm.hip); MIOpen only for what no
+native kernel takes (groups, dilation, non-fp32).  The filter
 transform U = G w G^T is cached on the weight tensor itself (keyed by its version counter, which
 every in-place update such as an optimizer step bumps), so a sampler that never changes
 its weights transforms each filter once.
@@ -356,12 +355,14 @@ def conv2d_weight_igemm_raw(x, wshape, gy, stride=1, padding=0, bias_grad=False)
     return dw, db
 
 
-# Kernel selection per distinct call: the implicit-GEMM kernels win on the small images /
-# odd channel counts / 1x1 weight gradients the PINN and the CIFAR-10 net's lowest levels run
-# (no NHWC transposes, no per-call solver search on the host), MIOpen's Winograd solvers on
-# big 3x3 convs at 8x8+ (tools/bench_igemm.py, profiles/r02_igemm_shapes.jsonl).  The first
-# eager call of each (op, shapes) times both once and caches the faster; under graph
-# capture an unseen call takes the implicit-GEMM kernel (native_only(): always igemm).
+# Kernel selection per distinct call.  Among native kernels (Winograd vs implicit GEMM on small
+# images) the first eager call of each (op, shapes) times the candidates once and caches the
+# faster; under graph capture an unseen call takes the first candidate.  MIOpen is not a
+# candidate (round 4): every conv the networks run has a native kernel, and timing MIOpen's
+# candidates cost seconds per process (immediate mode falls back to its naive kernels for
+# several backward shapes: 0.2 s per call) for, at best, 0.3 % of a sampler step (the two
+# stride-2 FIR-down shapes at B = 64, profiles/r04_stride2_igemm_vs_miopen.txt).
+# `library_candidates()` puts MIOpen back in the igemm-vs-library choices (A/B tools).
 _CHOICE: dict = {}        # agreed choices (broadcast from rank 0 under torch.distributed)
 _CHOICE_LOCAL: dict = {}  # choices made inside local_choices(): this rank's own, never agreed
 
@@ -425,16 +426,27 @@ def _save_table():
 
 
 _LOCAL_ONLY = [False]
-_NATIVE_ONLY = [False]
+_NATIVE_ONLY = [True]
 
 
 @contextlib.contextmanager
 def native_only():
     """Inside this block the igemm-vs-MIOpen choices take the implicit-GEMM kernel (the choices
-    among native kernels stay timed): a step captured in a hipGraph (the PINN step,
-    losses.get_pinn_step_fn(graph=True)) then holds only libbpk / aten kernels and no MIOpen
-    workspace or find-db state."""
+    among native kernels stay timed) even inside `library_candidates()`: a step captured in a
+    hipGraph (the PINN step, losses.get_pinn_step_fn(graph=True)) holds only libbpk / aten
+    kernels and no MIOpen workspace or find-db state."""
     prev, _NATIVE_ONLY[0] = _NATIVE_ONLY[0], True
+    try:
+        yield
+    finally:
+        _NATIVE_ONLY[0] = prev
+
+
+@contextlib.contextmanager
+def library_candidates():
+    """Inside this block MIOpen is timed against the implicit-GEMM kernel again (per call, the
+    faster kept): for A/B measurements only, the product default is native kernels."""
+    prev, _NATIVE_ONLY[0] = _NATIVE_ONLY[0], False
     try:
         yield
     finally:

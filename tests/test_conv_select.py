@@ -29,8 +29,13 @@ def test_table_replay_and_pick_first(tmp_path, monkeypatch):
     key2 = ("dgrad", (2, 8, 16, 16), (8, 8, 3, 3), (1, 1), (1, 1))
     monkeypatch.setattr(conv, "_PICK_FIRST", True)
     assert conv._decide(key2, [_never, _never]) == 0
-    assert conv._pick(key2, lambda: "ig", lambda: "mi") == "ig"
-    assert conv._pick(key, lambda: "ig", lambda: "mi") == "mi"
+    with conv.library_candidates():
+        assert conv._pick(key2, lambda: "ig", lambda: "mi") == "ig"
+        assert conv._pick(key, lambda: "ig", lambda: "mi") == "mi"
+        with conv.native_only():  # the graph-capture guard wins over the A/B block
+            assert conv._pick(key, lambda: "ig", lambda: "mi") == "ig"
+    # the product default: the native kernel, whatever the table says
+    assert conv._pick(key, lambda: "ig", _never) == "ig"
 
 
 def test_new_choice_written_back(tmp_path, monkeypatch):

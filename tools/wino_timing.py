@@ -1,4 +1,5 @@
-"""Per-workgroup phase timeline of wino_f23_pipe_kernel<1, true> (diagnostic).
+"""Per-workgroup phase timeline of the Winograd PRE conv (wino_f23_k16_kernel<true> where
+Cout % 128 == 0 and Cin % 16 == 0; diagnostic).
 
 Loads lib/libbpk_wino_timing.so (conv_winograd.hip built with -DWINO_TIMING: each workgroup
 records the 100 MHz wall clock at entry, after its prologue, after its chunk loop and after
@@ -52,16 +53,8 @@ def run(lib, B, cin, cout, hw, dev):
     torch.cuda.synchronize()
     ms = s.elapsed_time(e)
     nblk = B * (hw // 16) * (hw // 8) * ((cout + 63) // 64)
-    if os.environ.get("BPK_WINO_W8", "1") != "0" and cout % 128 == 0:
-        nblk //= 2  # 8-wave form: 128 couts per workgroup
-        # multi-item 16-cin form (conv_winograd.hip, BPK_WINO_K16_IPW): items per workgroup
-        ipw_env = int(os.environ.get("BPK_WINO_K16_IPW", "0"))
-        ipi = (hw // 16) * (hw // 8) * (cout // 128)
-        if ipw_env != 1 and cin % 32 == 0 and cin >= 64:
-            for c in range(ipi if ipw_env <= 1 else min(ipw_env, ipi), 1, -1):
-                if ipi % c == 0 and nblk // c >= (1 if ipw_env > 1 else 256):
-                    nblk //= c
-                    break
+    if cout % 128 == 0:
+        nblk //= 2  # 8-wave forms: 128 couts per workgroup (no split-K at these B = 64 shapes)
     ts6 = np.zeros((nblk, 8), dtype=np.int64)
     cu = np.zeros(nblk, dtype=np.uint32)
     n = lib.bpk_wino_timing_read(ts6.ctypes.data_as(P), cu.ctypes.data_as(P), nblk)
