@@ -352,9 +352,39 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
   }
 }
 
-// sum of the split-K partials in split order, scattered to the output layout
+// Many splits (a weight gradient over a long pixel sum into few outputs: the PINN's 1-32
+// channel convs at 64^2 x 64 images run 2048 splits into a few hundred outputs): first
+// partial sums of kRedG consecutive splits, each workgroup 64 outputs (one per lane,
+// coalesced) x kRedG splits (16 per wave, all 16 loads in flight), the four waves' sums added
+// in wave order.  The final pass then adds S / kRedG of these.  With one serial pass each
+// thread waited for 2048 dependent loads in turn (~0.5 ms for 330 outputs).
+constexpr int kRedG = 64;
+
+__global__ __launch_bounds__(256) void igemm_reduce_partial_kernel(const float* __restrict__ ws,
+                                                                   float* __restrict__ ws2,
+                                                                   int64_t total, int S) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int s0 = blockIdx.y * kRedG + wave * 16;
+  float v = 0.f;
+  if (i < total) {
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = s0 + j < S ? ws[(int64_t)(s0 + j) * total + i] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v += t[j];
+  }
+  red[wave][lane] = v;
+  __syncthreads();
+  if (wave == 0 && i < total)
+    ws2[(int64_t)blockIdx.y * total + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// sum of the S split-K partials (or partial sums) in split order, scattered to the output
+// layout
 template <int MODE>
-__global__ __launch_bounds__(256) void igemm_reduce_kernel(const float* __restrict__ ws,
+__global__ __launch_bounds__(256) void igemm_reduce_kernel(const float* __restrict__ ws, int S,
                                                            const float* __restrict__ bias,
                                                            float* __restrict__ out,
                                                            float* __restrict__ out2, IgGeo g) {
@@ -363,7 +393,8 @@ __global__ __launch_bounds__(256) void igemm_reduce_kernel(const float* __restri
        i += (int64_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / g.Ncol), col = (int)(i - (int64_t)m * g.Ncol);
     float v = ws[i];
-    for (int z = 1; z < g.splits; ++z) v += ws[(int64_t)z * total + i];
+#pragma unroll 8
+    for (int z = 1; z < S; ++z) v += ws[(int64_t)z * total + i];
     if (MODE == 0) {
       const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
       if (bias) v += bias[m];
@@ -479,8 +510,18 @@ int launch(const IgGeo& g, const float* A0, const float* B0, const float* bias, 
   BPK_LAUNCH_CHECK("conv2d_igemm");
   if (g.splits > 1) {
     const int64_t total = (int64_t)g.M * g.Ncol;
+    const float* src = ws;
+    int S = g.splits;
+    if (S > kRedG) {  // partial sums behind the partials (workspace_bytes counts them)
+      float* ws2 = ws + (int64_t)S * total;
+      const dim3 grid((unsigned)bpk::ceil_div(total, 64), (unsigned)bpk::ceil_div(S, kRedG));
+      igemm_reduce_partial_kernel<<<grid, 256, 0, st>>>(ws, ws2, total, S);
+      BPK_LAUNCH_CHECK("conv2d_igemm_reduce_partial");
+      src = ws2;
+      S = (int)bpk::ceil_div(S, kRedG);
+    }
     const unsigned blocks = (unsigned)std::min<int64_t>(bpk::ceil_div(total, 256), 4096);
-    igemm_reduce_kernel<MODE><<<blocks, 256, 0, st>>>(ws, bias, out, out2, g);
+    igemm_reduce_kernel<MODE><<<blocks, 256, 0, st>>>(src, S, bias, out, out2, g);
     BPK_LAUNCH_CHECK("conv2d_igemm_reduce");
   }
   return BPK_OK;
@@ -496,7 +537,9 @@ extern "C" int64_t bpk_conv2d_igemm_workspace_bytes(int mode, int N, int Cin, in
   if (mode < 0 || mode > 2 ||
       !make_geo(mode, N, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo, bias_grad, g))
     return -1;
-  return g.splits > 1 ? (int64_t)g.splits * g.M * g.Ncol * 4 : 0;
+  if (g.splits <= 1) return 0;
+  const int64_t S2 = g.splits > kRedG ? bpk::ceil_div(g.splits, kRedG) : 0;
+  return (g.splits + S2) * (int64_t)g.M * g.Ncol * 4;
 }
 
 extern "C" int bpk_conv2d_igemm_fwd_f32(const float* x, const float* w, const float* bias,

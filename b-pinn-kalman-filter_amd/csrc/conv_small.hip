@@ -208,7 +208,162 @@ __global__ __launch_bounds__(256) void small_cin_kernel(const float* __restrict_
   }
 }
 
+// Weight gradient of a conv with few output channels (Cout <= 4; K x K, stride 1, pad K / 2,
+// K = 1 or 3):  dw[co][c][r][s] = sum_{n, p} gy[n][co][p] x[n][c][p + (r, s) - K / 2],
+// db[co] = sum gy[n][co].  The network output convs (NCSN++ conv_out 128 -> 1 at 128^2, the
+// PINN heads into 1-4 channels) have one GEMM dimension of 1-4 against a K = pixels reduction,
+// which the implicit-GEMM kernel runs on mostly idle 64-row MFMA tiles while gathering every
+// x element 9 times (2.3 ms for B = 64, 128 -> 1 at 128^2).  Here it is a single streaming
+// pass over x (HBM-bound): one workgroup per (channel c, image n) walks the image in row bands,
+// stages each band's rows with their halo in LDS, and every thread accumulates the COUT x K^2
+// products of its pixels in registers (gy read coalesced, L2-resident across the channels);
+// the workgroup's sums (wave butterflies, then the waves in order) go to a per-image partial,
+// and small_cout_wgrad_reduce_kernel adds the images in order: deterministic.
+template <int COUT, int K>
+__global__ __launch_bounds__(256) void small_cout_wgrad_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ gy,
+                                                               float* __restrict__ part,
+                                                               float* __restrict__ partb, int Cin,
+                                                               int H, int W, int RB) {
+  extern __shared__ float s_x[];  // (RB + K - 1) x (W + K - 1)
+  constexpr int KK = K * K, P = K / 2;
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x, n = blockIdx.y;
+  const int64_t plane = (int64_t)H * W;
+  const float* xp = x + ((int64_t)n * Cin + c) * plane;
+  const float* gp = gy + (int64_t)n * COUT * plane;
+  const int Wp = W + K - 1;
+  float acc[COUT][KK], accb[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+    accb[co] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) acc[co][k] = 0.f;
+  }
+  // this thread's pixels in a band: q = tid + 256 j -> (row, col), stepped without division
+  const int dr = 256 / W, dc = 256 - dr * W;
+  const int r_first = tid / W, c_first = tid - r_first * W;
+  for (int y0 = 0; y0 < H; y0 += RB) {
+    const int rows = min(RB, H - y0);
+    __syncthreads();  // the previous band's LDS reads are done
+    for (int i = tid; i < (rows + K - 1) * Wp; i += 256) {
+      const int rr = i / Wp, cc = i - rr * Wp;
+      const int iy = y0 - P + rr, ix = cc - P;
+      s_x[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? xp[(int64_t)iy * W + ix] : 0.f;
+    }
+    __syncthreads();
+    int r = r_first, col = c_first;
+    while (r < rows) {
+      float g[COUT];
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) g[co] = gp[co * plane + (int64_t)(y0 + r) * W + col];
+#pragma unroll
+      for (int a = 0; a < K; ++a)
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+          const float xv = s_x[(r + a) * Wp + col + b];
+#pragma unroll
+          for (int co = 0; co < COUT; ++co) acc[co][a * K + b] = fmaf(g[co], xv, acc[co][a * K + b]);
+        }
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) accb[co] += g[co];
+      r += dr;
+      col += dc;
+      if (col >= W) {
+        col -= W;
+        ++r;
+      }
+    }
+  }
+  // workgroup sums: butterflies within each wave, then the four waves in order
+  __shared__ float red[4][COUT * (KK + 1)];
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int co = 0; co < COUT; ++co)
+#pragma unroll
+    for (int k = 0; k <= KK; ++k) {
+      float v = k < KK ? acc[co][k] : accb[co];
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+      if (lane == 0) red[wave][co * (KK + 1) + k] = v;
+    }
+  __syncthreads();
+  if (tid < COUT * (KK + 1)) {
+    const float v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    const int co = tid / (KK + 1), k = tid - co * (KK + 1);
+    if (k < KK)
+      part[(((int64_t)n * COUT + co) * Cin + c) * KK + k] = v;
+    else if (c == 0 && partb)
+      partb[n * COUT + co] = v;
+  }
+}
+
+// dw = sum over images of the partials, in image order (db likewise)
+__global__ __launch_bounds__(256) void small_cout_wgrad_reduce_kernel(
+    const float* __restrict__ part, const float* __restrict__ partb, float* __restrict__ dw,
+    float* __restrict__ db, int N, int Cout, int per_co) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int total = Cout * per_co;
+  if (i < total) {
+    const int co = i / per_co, rest = i - co * per_co;
+    float v = 0.f;
+#pragma unroll 8
+    for (int n = 0; n < N; ++n) v += part[((int64_t)n * Cout + co) * per_co + rest];
+    dw[i] = v;
+  } else if (db && i < total + Cout) {
+    const int co = i - total;
+    float v = 0.f;
+    for (int n = 0; n < N; ++n) v += partb[n * Cout + co];
+    db[co] = v;
+  }
+}
+
+int wgrad_rows_per_band(int H, int W) { return std::max(1, std::min(H, 1024 / W)); }
+
 }  // namespace
+
+extern "C" int bpk_conv2d_wgrad_small_cout_supported(int N, int Cin, int Cout, int H, int W,
+                                                     int K) {
+  return N > 0 && Cin > 0 && Cout >= 1 && Cout <= 4 && H > 0 && W > 0 && (K == 1 || K == 3) &&
+         (int64_t)N * Cin < (1LL << 31) && (int64_t)N * std::max(Cin, Cout) * H * W < (1LL << 40) &&
+         (int64_t)(wgrad_rows_per_band(H, W) + K - 1) * (W + K - 1) * 4 <= 64 * 1024;
+}
+
+extern "C" int64_t bpk_conv2d_wgrad_small_cout_workspace_bytes(int N, int Cin, int Cout, int K) {
+  return ((int64_t)N * Cout * Cin * K * K + (int64_t)N * Cout) * 4;
+}
+
+extern "C" int bpk_conv2d_wgrad_small_cout_f32(const float* x, const float* gy, float* dw,
+                                               float* db, void* ws, int N, int Cin, int Cout,
+                                               int H, int W, int K, void* stream) {
+  BPK_REQUIRE(bpk_conv2d_wgrad_small_cout_supported(N, Cin, Cout, H, W, K),
+              "conv2d_wgrad_small_cout: unsupported shape N=%d Cin=%d Cout=%d %dx%d K=%d", N, Cin,
+              Cout, H, W, K);
+  BPK_REQUIRE(x && gy && dw && ws, "conv2d_wgrad_small_cout: null pointer");
+  float* part = static_cast<float*>(ws);
+  float* partb = db ? part + (int64_t)N * Cout * Cin * K * K : nullptr;
+  const int RB = wgrad_rows_per_band(H, W);
+  const size_t lds = (size_t)(RB + K - 1) * (W + K - 1) * 4;
+  hipStream_t st = bpk::as_stream(stream);
+  const dim3 grid((unsigned)Cin, (unsigned)N);
+#define WG(C_, K_)                                                                                hipLaunchKernelGGL((small_cout_wgrad_kernel<C_, K_>), grid, dim3(256), lds, st, x, gy, part,                      partb, Cin, H, W, RB)
+#define WGK(C_)   do {              if (K == 3)       WG(C_, 3);     else              WG(C_, 1);   } while (0)
+  switch (Cout) {
+    case 1: WGK(1); break;
+    case 2: WGK(2); break;
+    case 3: WGK(3); break;
+    default: WGK(4); break;
+  }
+#undef WGK
+#undef WG
+  BPK_LAUNCH_CHECK("conv2d_wgrad_small_cout");
+  const int per_co = Cin * K * K;
+  const int total = Cout * per_co + (db ? Cout : 0);
+  hipLaunchKernelGGL(small_cout_wgrad_reduce_kernel, dim3((unsigned)bpk::ceil_div(total, 256)),
+                     dim3(256), 0, st, part, partb, dw, db, N, Cout, per_co);
+  BPK_LAUNCH_CHECK("conv2d_wgrad_small_cout_reduce");
+  return BPK_OK;
+}
 
 extern "C" int bpk_conv3x3_small_supported(int N, int Cin, int Cout, int H, int W) {
   return N > 0 && Cin > 0 && Cout > 0 && H > 0 && W > 0 && W % 4 == 0 &&

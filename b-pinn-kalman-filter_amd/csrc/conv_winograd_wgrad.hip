@@ -56,10 +56,13 @@ constexpr int kXRS = 24;                     // LDS patch row: halo at 3, interi
 constexpr int kXCS = kXR * kXRS + 16;        // per-cin stride (2-way transform reads)
 constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records (644)
 
-// NB = 16-cout blocks per wave: NB = 1 -> 64 couts per workgroup, two workgroups per CU;
-// NB = 2 (Cout % 128 == 0, round 4) -> 128 couts per workgroup, 256 accumulators per lane,
-// one workgroup per CU: the V transform, the patch staging and every A operand read serve
-// twice the couts, and each wave issues 128 MFMAs per barrier instead of 64.
+// NB = 16-cout blocks per wave: NB = 1 -> 64 couts per workgroup, two workgroups per CU (the
+// form that runs).  NB = 2 (128 couts per workgroup, 256 accumulators per lane, one workgroup
+// per CU: the V transform, the patch staging and every A operand read serve twice the couts)
+// was measured slower on every NCSN++ shape, round 4 (1.85 vs 1.50 ms at 128->128 @128^2,
+// 7.06 vs 5.20 at 256->256 @128^2; DSM train 2.59 vs 2.87 steps/s, same box) -- the halved
+// residency exposes the per-chunk barrier and load latency that two co-resident workgroups
+// hide -- and is not launched.
 template <int NB>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ part,
@@ -387,17 +390,11 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
   }
 }
 
-// N-blocks per wave: 2 (128 couts per workgroup) when Cout allows it (-DWGRAD_NB1: the
-// round-3 64-cout form everywhere, for A/B variant builds: tools/build_variant.sh)
-#ifdef WGRAD_NB1
-int wgrad_nb(int) { return 1; }
-#else
-int wgrad_nb(int Cout) { return Cout % (2 * kOB) == 0 ? 2 : 1; }
-#endif
+constexpr int kNB = 1;  // N-blocks per wave (see wino_wgrad_pipe_kernel)
 
 WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
   WgradGeo g{};
-  const int nb = wgrad_nb(Cout);
+  const int nb = kNB;
   g.N = N; g.Cin = Cin; g.Cout = Cout; g.H = H; g.W = W;
   g.strips_x = W / 16;
   g.strips_y = H / 2;
@@ -448,12 +445,8 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
   float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
-  if (wgrad_nb(Cout) == 2)
-    hipLaunchKernelGGL(wino_wgrad_pipe_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, st, x,
-                       gy, workspace, part_b, g, remap);
-  else
-    hipLaunchKernelGGL(wino_wgrad_pipe_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, x,
-                       gy, workspace, part_b, g, remap);
+  hipLaunchKernelGGL(wino_wgrad_pipe_kernel<kNB>, dim3((unsigned)blocks), dim3(256), 0, st, x,
+                     gy, workspace, part_b, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
   BPK_REQUIRE(bpk::ceil_div(pairs, 16) < (1LL << 31), "conv3x3_wino_wgrad: too many pairs");

@@ -355,6 +355,32 @@ def conv2d_weight_igemm_raw(x, wshape, gy, stride=1, padding=0, bias_grad=False)
     return dw, db
 
 
+def _small_cout_wgrad_ok(x, wshape, s, p):
+    Co, C, KH, KW = wshape
+    return (Co <= 4 and KH == KW and KH in (1, 3) and s == (1, 1) and p == (KH // 2, KW // 2)
+            and bool(lib.bpk_conv2d_wgrad_small_cout_supported(x.shape[0], C, Co, x.shape[2],
+                                                                x.shape[3], KH)))
+
+
+def conv2d_weight_small_cout_raw(x, wshape, gy, bias_grad=False):
+    """(dw, db or None) of a K x K / stride 1 / pad K // 2 conv into Cout <= 4 channels on the
+    streaming VALU kernel (csrc/conv_small.hip)."""
+    x = x.detach().contiguous()
+    gy = gy.detach().contiguous()
+    N, C, H, W = x.shape
+    Co, _, K, _ = (int(v) for v in wshape)
+    dw = torch.empty((Co, C, K, K), dtype=torch.float32, device=x.device)
+    db = torch.empty((Co,), dtype=torch.float32, device=x.device) if bias_grad else None
+    nb = lib.bpk_conv2d_wgrad_small_cout_workspace_bytes(N, C, Co, K)
+    ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=x.device)
+    check(lib.bpk_conv2d_wgrad_small_cout_f32(x.data_ptr(), gy.data_ptr(), dw.data_ptr(),
+                                              None if db is None else db.data_ptr(),
+                                              ws.data_ptr(), N, C, Co, H, W, K,
+                                              stream_ptr(x.device)), "conv2d_wgrad_small_cout")
+    flops.add("valu_wgrad", 2.0 * N * Co * C * K * K * H * W)
+    return dw, db
+
+
 # Kernel selection per distinct call.  Among native kernels (Winograd vs implicit GEMM on small
 # images) the first eager call of each (op, shapes) times the candidates once and caches the
 # faster; under graph capture an unseen call takes the first candidate.  MIOpen is not a
@@ -552,7 +578,14 @@ def conv2d_weight_select(x, wshape, gy, stride, padding, bias_grad):
     def mi():
         dw = torch.nn.grad.conv2d_weight(x.detach(), wshape, gy.detach(), s, p)
         return dw, (gy.detach().sum((0, 2, 3)) if bias_grad else None)
-    return _pick(key, lambda: conv2d_weight_igemm_raw(x, wshape, gy, s, p, bias_grad), mi)
+
+    def ig():
+        return conv2d_weight_igemm_raw(x, wshape, gy, s, p, bias_grad)
+    if _small_cout_wgrad_ok(x, wshape, s, p):  # few output channels: streaming kernel vs igemm
+        ig_any = ig
+        ig = lambda: _pick_any(("wsc",) + key[1:], [  # noqa: E731
+            lambda: conv2d_weight_small_cout_raw(x, wshape, gy, bias_grad), ig_any])
+    return _pick(key, ig, mi)
 
 
 def _flip_t(w):

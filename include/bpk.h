@@ -427,6 +427,17 @@ int bpk_conv3x3_small_f32(const float* x, const float* pre, const float* weight,
                           const float* bias, float* y, int N, int Cin, int Cout, int H, int W,
                           void* stream);
 
+/* Weight (+ bias) gradient of a K x K / stride 1 / pad K/2 conv (K = 1 or 3) into few output
+ * channels (Cout <= 4): dw [Cout, Cin, K, K] = sum_{n,p} gy[n][co][p] x[n][c][p + (r, s) - K/2],
+ * db [Cout] = sum gy (db may be NULL).  The networks' output convs (NCSN++ conv_out, the PINN
+ * heads; reference nn.Conv2d -> cuDNN backward-weights).  One streaming pass over x, per-image
+ * partials in `workspace` (workspace_bytes()), summed in image order: deterministic. */
+int bpk_conv2d_wgrad_small_cout_supported(int N, int Cin, int Cout, int H, int W, int K);
+int64_t bpk_conv2d_wgrad_small_cout_workspace_bytes(int N, int Cin, int Cout, int K);
+int bpk_conv2d_wgrad_small_cout_f32(const float* x, const float* gy, float* dw, float* db,
+                                    void* workspace, int N, int Cin, int Cout, int H, int W,
+                                    int K, void* stream);
+
 /* 1x1 convolution of NCHW tensors as an f32 MFMA GEMM with an optional second source
  * along K (the score networks' Conv_2 skip projections and attention NINs, which the
  * reference runs through nn.Conv2d / einsum):

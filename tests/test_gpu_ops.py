@@ -330,8 +330,7 @@ def test_conv3x3_winograd_backward_and_filter_cache(hip, cin):
 def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
     """Winograd split-K weight gradient vs a float64 direct computation (and MIOpen's fp32
     backward-weights held to the same bound): 2e-5 relative to max|ref|.  Shapes cover one
-    K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths, on
-    both workgroup forms (64 couts; 128 couts with two N-blocks per wave when Cout % 128 == 0)."""
+    K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths."""
     import torch.nn.functional as F
     from op import conv as conv_mod
     from op.conv import conv3x3_wgrad_raw
@@ -1001,6 +1000,7 @@ _IG_CASES = [
     (2, 6, 9, 9, 4, 4, 2, 1),        # flow_upsample k4 s2 p1
     (3, 33, 5, 5, 17, 1, 1, 0),      # 1x1, non-multiple-of-16 channels
     (2, 7, 11, 13, 5, 5, 1, 2),      # generic-kernel template (5x5)
+    (64, 6, 64, 64, 6, 3, 1, 1),     # PINN 6-channel conv at 64^2: >64 wgrad splits (two-level sum)
 ]
 
 
@@ -1035,6 +1035,37 @@ def test_conv2d_igemm_fwd_dgrad_wgrad_vs_fp64(hip, case):
     close(dw, gw_ref, "wgrad")
     close(db, gb_ref, "bias grad")
     dw2, none = conv2d_weight_igemm_raw(x.to(hip), w.shape, gy.to(hip), s, p, bias_grad=False)
+    assert none is None and torch.equal(dw2, dw)
+
+
+@pytest.mark.parametrize("case", [
+    # N, Cin, H, W, Cout, K
+    (2, 5, 9, 13, 1, 3),       # odd sizes, bands ragged
+    (3, 16, 64, 64, 4, 3),     # PINN head shape
+    (2, 7, 8, 300, 2, 3),      # W > 256: one pixel per thread per row step
+    (2, 3, 5, 7, 3, 1),        # 1x1
+    (1, 4, 1, 1, 2, 3),        # 1 x 1 image: every tap but the centre reads padding
+    (4, 128, 32, 32, 1, 3),    # NCSN++ conv_out shape class (128 -> 1)
+])
+def test_conv2d_wgrad_small_cout_vs_fp64(hip, case):
+    """Weight + bias gradient of a conv into Cout <= 4 channels (csrc/conv_small.hip streaming
+    kernel) vs float64 autograd on the CPU: within 2e-5 of the gradient's magnitude;
+    deterministic (two calls bit-identical)."""
+    from op.conv import conv2d_weight_small_cout_raw
+    N, C, H, W, Co, K = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(Co, C, K, K, generator=g)
+    gy = torch.randn(N, Co, H, W, generator=g)
+    xd, wd, bd = x.double(), w.double().requires_grad_(), torch.zeros(Co, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(xd, wd, bd, 1, K // 2)
+    gw_ref, gb_ref = torch.autograd.grad(y, (wd, bd), gy.double())
+    dw, db = conv2d_weight_small_cout_raw(x.to(hip), w.shape, gy.to(hip), bias_grad=True)
+    for got, ref, what in ((dw, gw_ref, "dw"), (db, gb_ref, "db")):
+        tol = 2e-5 * max(1.0, float(ref.abs().max()))
+        err = float((got.double().cpu() - ref).abs().max())
+        assert err <= tol, f"{what}: {err} > {tol}"
+    dw2, none = conv2d_weight_small_cout_raw(x.to(hip), w.shape, gy.to(hip), bias_grad=False)
     assert none is None and torch.equal(dw2, dw)
 
 
