@@ -16,6 +16,11 @@
 //                          conv transpose; also ConvTranspose2d's forward)
 //   MODE 2  weight grad    C[co][(ci,r,s)] = sum_p gy[n][co][oy][ox] x[n][ci][iy][ix], plus
 //                          one extra column of ones: the bias gradient sum_p gy[co][p]
+//   MODE 3  backward-data of a strided conv, one input-pixel class per launch: the pixels
+//                          (iy, ix) = (cy + s_h iyc, cx + s_w ixc) only receive the taps
+//                          r = rc0 + s_h i, s = sc0 + s_w j (r = (cy + p_h) mod s_h ...), so
+//                          each class is a dense GEMM over Cout * KHc * KWc instead of MODE 1's
+//                          K = Cout * KH * KW of which 3/4 are structural zeros at stride 2
 //
 // Tile: 64 x 64 (or, when those alone fill the chip, 128 x 128) outputs per workgroup (4
 // waves, 2 x 2 of 32 x 32 / 64 x 64, each 2 x 2 / 4 x 4 MFMA blocks),
@@ -58,7 +63,27 @@ struct IgGeo {
   int nchunk, chunks_per_split, splits, tile;  // tile: 0 = 64x64, 1 = 128x128, 2 = 16x256
   int wcols;  // MODE 2: Cin * KH * KW (the column Ncol - 1 == wcols is the bias column)
   FDiv f_howo, f_wo, f_hw, f_w, f_khw, f_kw, f_sh, f_sw;
+  // MODE 3: the input-pixel class (cy, cx), its grid Hc x Wc and sub-filter KHc x KWc whose
+  // taps start at (rc0, sc0) and step by the stride
+  int cy, cx, Hc, Wc, KHc, KWc, rc0, sc0;
+  FDiv f_hwc, f_wc, f_khwc, f_kwc;
 };
+
+// k -> (co, r, s) of a MODE 3 class sub-filter tap
+__device__ inline void split_tap_class(int k, const IgGeo& g, int& co, int& r, int& s) {
+  co = fdiv(k, g.f_khwc);
+  const int t = k - co * (g.KHc * g.KWc);
+  const int ri = fdiv(t, g.f_kwc);
+  r = g.rc0 + ri * g.sh;
+  s = g.sc0 + (t - ri * g.KWc) * g.sw;
+}
+
+// MODE 3 column -> output offset of its input pixel (n, cy + sh iyc, cx + sw ixc)
+__device__ inline int64_t class_pixel_offset(int col, const IgGeo& g) {
+  const int n = fdiv(col, g.f_hwc), pix = col - n * (g.Hc * g.Wc);
+  const int iyc = fdiv(pix, g.f_wc), ixc = pix - iyc * g.Wc;
+  return (int64_t)n * g.Cin * g.HW + (int64_t)(g.cy + iyc * g.sh) * g.W + g.cx + ixc * g.sw;
+}
 
 // k -> (c, r, s) of a filter tap index k = (c * KH + r) * KW + s; compile-time KH, KW turn
 // the divisions into multiplies
@@ -121,6 +146,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
       py = oy * g.sh - g.ph;
       px = ox * g.sw - g.pw;
       bbase = (int64_t)n * g.Cin * g.HW;
+    } else if (MODE == 3) {
+      const int n = fdiv(pp, g.f_hwc), pix = pp - n * (g.Hc * g.Wc);
+      const int iyc = fdiv(pix, g.f_wc), ixc = pix - iyc * g.Wc;
+      py = g.cy + iyc * g.sh + g.ph;
+      px = g.cx + ixc * g.sw + g.pw;
+      bbase = (int64_t)n * g.Cout * g.HoWo;
     } else {
       const int n = fdiv(pp, g.f_hw), pix = pp - n * g.HW;
       const int iy = fdiv(pix, g.f_w), ix = pix - iy * g.W;
@@ -153,6 +184,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
         const int khw = KH_ ? KH_ * KW_ : g.KHW;
         a_co = KH_ ? k / khw : fdiv(k, g.f_khw);
         a_rs = k - a_co * khw;
+      } else if (MODE == 3) {
+        int r, s;
+        split_tap_class(k < g.K ? k : 0, g, a_co, r, s);
+        a_rs = r * g.KW + s;
       } else if (MODE == 2) {
         a_n = fdiv(k < g.K ? k : 0, g.f_howo);
         a_pix = k - a_n * g.HoWo;
@@ -167,6 +202,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
           } else if (MODE == 1) {  // m = ci, k = (co, r, s)
             const int khw = KH_ ? KH_ * KW_ : g.KHW;
             v = A0[((int64_t)a_co * g.Cin + m) * khw + a_rs];
+          } else if (MODE == 3) {  // m = ci, k = (co, class tap)
+            v = A0[((int64_t)a_co * g.Cin + m) * g.KHW + a_rs];
           } else {  // m = co, k = pixel
             v = A0[((int64_t)a_n * g.Cout + m) * g.HoWo + a_pix];
           }
@@ -181,16 +218,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
         const int k = kb + bk + kBStep * j;
         float v = 0.f;
         int c, r, s;
-        split_tap<KH_, KW_>(k < g.K ? k : 0, g, c, r, s);
+        if (MODE == 3)
+          split_tap_class(k < g.K ? k : 0, g, c, r, s);
+        else
+          split_tap<KH_, KW_>(k < g.K ? k : 0, g, c, r, s);
         if (MODE == 0) {
           const int iy = py + r, ix = px + s;
           if (pvalid && k < g.K && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
             v = B0[bbase + ((int64_t)c * g.H + iy) * g.W + ix];
         } else {
-          const int ty = py - r, tx = px - s;
+          const int ty = py - r, tx = px - s;  // MODE 3: multiples of the stride by construction
           if (pvalid && k < g.K && ty >= 0 && tx >= 0) {
             const int oy = fdiv(ty, g.f_sh), ox = fdiv(tx, g.f_sw);
-            if (oy * g.sh == ty && ox * g.sw == tx && oy < g.Ho && ox < g.Wo)
+            if ((MODE == 3 || (oy * g.sh == ty && ox * g.sw == tx)) && oy < g.Ho && ox < g.Wo)
               v = B0[bbase + ((int64_t)c * g.Ho + oy) * g.Wo + ox];
           }
         }
@@ -293,6 +333,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
         const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
         obase = (int64_t)n * g.Cout * g.HoWo + pix;
         ostride = g.HoWo;
+      } else if (MODE == 3) {
+        obase = class_pixel_offset(col, g);
+        ostride = g.HW;
       } else {
         const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
         obase = (int64_t)n * g.Cin * g.HW + pix;
@@ -325,6 +368,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
     } else if (MODE == 1) {
       const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
       obase = (int64_t)n * g.Cin * g.HW + pix;
+      ostride = g.HW;
+    } else if (MODE == 3) {
+      obase = class_pixel_offset(col, g);
       ostride = g.HW;
     } else {
       obase = col;
@@ -402,6 +448,8 @@ __global__ __launch_bounds__(256) void igemm_reduce_kernel(const float* __restri
     } else if (MODE == 1) {
       const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
       out[((int64_t)n * g.Cin + m) * g.HW + pix] = v;
+    } else if (MODE == 3) {
+      out[class_pixel_offset(col, g) + (int64_t)m * g.HW] = v;
     } else {
       if (col == g.wcols)
         out2[m] = v;
@@ -425,6 +473,8 @@ int num_cus() {
 }
 
 constexpr int64_t kMaxWorkspace = 64ll << 20;  // split-K partials (bytes): their round trip stays small
+
+void choose_tiling(IgGeo& g, int mode);
 
 // geometry, tile and split-K choice; false when the shape is out of range
 bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, int sh, int sw,
@@ -451,6 +501,55 @@ bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, 
   } else {
     g.M = Cout; g.Ncol = g.wcols + (bias_col ? 1 : 0); g.K = N * Ho * Wo;
   }
+  choose_tiling(g, mode);
+  return true;
+}
+
+// MODE 3 geometry of input-pixel class (cy, cx) of a strided backward-data; false when the
+// class holds no pixel
+bool make_geo_class(const IgGeo& base, int cy, int cx, IgGeo& g) {
+  g = base;
+  g.cy = cy; g.cx = cx;
+  g.Hc = (int)bpk::ceil_div(base.H - cy, base.sh);
+  g.Wc = (int)bpk::ceil_div(base.W - cx, base.sw);
+  if (g.Hc <= 0 || g.Wc <= 0) return false;
+  g.rc0 = (cy + base.ph) % base.sh;
+  g.sc0 = (cx + base.pw) % base.sw;
+  g.KHc = (int)bpk::ceil_div(base.KH - g.rc0, base.sh);  // >= 1: KH >= sh (class_dgrad_ok)
+  g.KWc = (int)bpk::ceil_div(base.KW - g.sc0, base.sw);
+  g.f_hwc = make_fdiv(g.Hc * g.Wc); g.f_wc = make_fdiv(g.Wc);
+  g.f_khwc = make_fdiv(g.KHc * g.KWc); g.f_kwc = make_fdiv(g.KWc);
+  g.M = base.Cin; g.Ncol = base.N * g.Hc * g.Wc; g.K = base.Cout * g.KHc * g.KWc;
+  choose_tiling(g, 3);
+  return true;
+}
+
+int64_t grid_size(const IgGeo& g) {
+  const int tm = g.tile == 1 ? 128 : g.tile == 2 ? 16 : 64;
+  const int tn = g.tile == 1 ? 128 : g.tile == 2 ? 256 : 64;
+  return bpk::ceil_div(g.M, tm) * bpk::ceil_div(g.Ncol, tn) * g.splits;
+}
+
+// strided backward-data runs class by class (MODE 3) when every class has a tap and every
+// class launch still fills the chip (small images: the classes' launches of a few dozen
+// workgroups each ran longer than the one MODE 1 launch with its structural zeros, e.g. the
+// PINN's 32^2 stride-2 convs, 73 vs 45 us)
+bool class_dgrad_ok(const IgGeo& g) {
+  if (!((g.sh > 1 || g.sw > 1) && g.KH >= g.sh && g.KW >= g.sw)) return false;
+  IgGeo gc;
+  for (int cy = 0; cy < g.sh; ++cy)
+    for (int cx = 0; cx < g.sw; ++cx)
+      if (make_geo_class(g, cy, cx, gc) && grid_size(gc) < num_cus()) return false;
+  return true;
+}
+
+int64_t ws_bytes(const IgGeo& g) {
+  if (g.splits <= 1) return 0;
+  const int64_t S2 = g.splits > kRedG ? bpk::ceil_div(g.splits, kRedG) : 0;
+  return (g.splits + S2) * (int64_t)g.M * g.Ncol * 4;
+}
+
+void choose_tiling(IgGeo& g, int mode) {
   g.nchunk = (g.K + BK - 1) / BK;
   const int64_t cus = num_cus();
   // 16 x 256 tiles for M <= 16 (a forward / backward-data conv into 1-16 channels: no
@@ -474,7 +573,6 @@ bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, 
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::min<int64_t>(cap, 4096)));
   g.chunks_per_split = (int)bpk::ceil_div(g.nchunk, splits);
   g.splits = (int)bpk::ceil_div(g.nchunk, g.chunks_per_split);
-  return true;
 }
 
 template <int MODE, int TM, int TN, int WMW>
@@ -484,7 +582,9 @@ void launch_tile(const IgGeo& g, const float* A0, const float* B0, const float* 
                   (unsigned)g.splits);
 #define BPK_IG(KH_, KW_) \
   igemm_kernel<MODE, KH_, KW_, TM, TN, WMW><<<grid, 256, 0, st>>>(A0, B0, bias, out, out2, wsp, g)
-  if (g.KH == 3 && g.KW == 3)
+  if (MODE == 3)  // class sub-filters: runtime tap arithmetic (split_tap_class)
+    BPK_IG(0, 0);
+  else if (g.KH == 3 && g.KW == 3)
     BPK_IG(3, 3);
   else if (g.KH == 1 && g.KW == 1)
     BPK_IG(1, 1);
@@ -537,9 +637,15 @@ extern "C" int64_t bpk_conv2d_igemm_workspace_bytes(int mode, int N, int Cin, in
   if (mode < 0 || mode > 2 ||
       !make_geo(mode, N, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo, bias_grad, g))
     return -1;
-  if (g.splits <= 1) return 0;
-  const int64_t S2 = g.splits > kRedG ? bpk::ceil_div(g.splits, kRedG) : 0;
-  return (g.splits + S2) * (int64_t)g.M * g.Ncol * 4;
+  if (mode == 1 && class_dgrad_ok(g)) {  // the largest class's partials (classes run in turn)
+    int64_t b = 0;
+    IgGeo gc;
+    for (int cy = 0; cy < sh; ++cy)
+      for (int cx = 0; cx < sw; ++cx)
+        if (make_geo_class(g, cy, cx, gc)) b = std::max(b, ws_bytes(gc));
+    return b;
+  }
+  return ws_bytes(g);
 }
 
 extern "C" int bpk_conv2d_igemm_fwd_f32(const float* x, const float* w, const float* bias,
@@ -568,8 +674,21 @@ extern "C" int bpk_conv2d_igemm_dgrad_f32(const float* gy, const float* w, float
               Cout, KH, KW);
   BPK_REQUIRE((H + 2 * ph - KH) / sh + 1 == Ho && (W + 2 * pw - KW) / sw + 1 == Wo,
               "conv2d_igemm_dgrad: output %dx%d inconsistent with input %dx%d", Ho, Wo, H, W);
+  hipStream_t st = bpk::as_stream(stream);
+  if (class_dgrad_ok(g)) {
+    BPK_REQUIRE(gy && w && gx, "conv2d_igemm_dgrad: null pointer");
+    IgGeo gc;
+    for (int cy = 0; cy < sh; ++cy)
+      for (int cx = 0; cx < sw; ++cx) {
+        if (!make_geo_class(g, cy, cx, gc)) continue;
+        BPK_REQUIRE(gc.splits == 1 || ws, "conv2d_igemm_dgrad: null workspace");
+        const int rc = launch<3>(gc, w, gy, nullptr, gx, nullptr, ws, st);
+        if (rc != BPK_OK) return rc;
+      }
+    return BPK_OK;
+  }
   BPK_REQUIRE(gy && w && gx && (g.splits == 1 || ws), "conv2d_igemm_dgrad: null pointer");
-  return launch<1>(g, w, gy, nullptr, gx, nullptr, ws, bpk::as_stream(stream));
+  return launch<1>(g, w, gy, nullptr, gx, nullptr, ws, st);
 }
 
 extern "C" int bpk_conv2d_igemm_wgrad_f32(const float* x, const float* gy, float* dw, float* db,

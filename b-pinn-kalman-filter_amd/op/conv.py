@@ -566,7 +566,19 @@ def conv2d_input_select(xshape, w, gy, stride, padding):
     s, p = _pair(stride), _pair(padding)
     xshape = tuple(int(v) for v in xshape)
     key = ("dgrad", xshape, tuple(w.shape), s, p)
-    return _pick(key, lambda: conv2d_input_igemm_raw(xshape, w, gy, s, p),
+
+    def ig():
+        return conv2d_input_igemm_raw(xshape, w, gy, s, p)
+    N, C, H, W = xshape
+    if (C <= 4 and tuple(w.shape[2:]) == (3, 3) and s == (1, 1) and p == (1, 1)
+            and bool(lib.bpk_conv3x3_small_supported(N, w.shape[0], C, H, W))):
+        # into <= 4 channels: the conv of gy with the flipped, transposed filter on the
+        # small-Cout streaming kernel (the PINN heads' input gradients), timed against igemm
+        ig_any = ig
+        ig = lambda: _pick_any(("dsc",) + key[1:], [  # noqa: E731
+            lambda: conv3x3_small_raw(gy.detach().contiguous(), _flip_t(w.detach()).contiguous()),
+            ig_any])
+    return _pick(key, ig,
                  lambda: torch.nn.grad.conv2d_input(xshape, w.detach(), gy.detach(), s, p))
 
 

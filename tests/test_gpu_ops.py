@@ -1001,6 +1001,8 @@ _IG_CASES = [
     (3, 33, 5, 5, 17, 1, 1, 0),      # 1x1, non-multiple-of-16 channels
     (2, 7, 11, 13, 5, 5, 1, 2),      # generic-kernel template (5x5)
     (64, 6, 64, 64, 6, 3, 1, 1),     # PINN 6-channel conv at 64^2: >64 wgrad splits (two-level sum)
+    (2, 5, 10, 11, 7, 3, 3, 1),      # stride 3, small: backward-data as one launch (MODE 1)
+    (16, 128, 65, 65, 256, 3, 2, 0),  # NCSN++ FIR-down conv: backward-data by pixel class (MODE 3)
 ]
 
 
@@ -1067,6 +1069,23 @@ def test_conv2d_wgrad_small_cout_vs_fp64(hip, case):
         assert err <= tol, f"{what}: {err} > {tol}"
     dw2, none = conv2d_weight_small_cout_raw(x.to(hip), w.shape, gy.to(hip), bias_grad=False)
     assert none is None and torch.equal(dw2, dw)
+
+
+@pytest.mark.parametrize("cin", [1, 4])
+def test_conv2d_input_select_small_cin_candidates(hip, cin, monkeypatch):
+    """Backward-data into <= 4 channels: both candidates of the timed choice (the small-Cout
+    kernel on the flipped / transposed filter, and igemm) vs float64 conv2d_input."""
+    from op import conv
+    g = torch.Generator().manual_seed(cin)
+    xshape = (3, cin, 16, 20)
+    w = torch.randn(64, cin, 3, 3, generator=g) / 24
+    gy = torch.randn(3, 64, 16, 20, generator=g)
+    ref = torch.nn.grad.conv2d_input(xshape, w.double(), gy.double(), 1, 1)
+    for c in (0, 1):
+        monkeypatch.setattr(conv, "_CHOICE", {("dsc", xshape, tuple(w.shape), (1, 1), (1, 1)): c})
+        got = conv.conv2d_input_select(xshape, w.to(hip), gy.to(hip), 1, 1)
+        err = float((got.double().cpu() - ref).abs().max())
+        assert err <= 2e-5 * max(1.0, float(ref.abs().max())), (c, err)
 
 
 @pytest.mark.parametrize("k,stride,pad,cin,cout,hw", [(3, 2, 1, 3, 16, 12), (3, 1, 1, 49, 32, 4),
