@@ -555,21 +555,24 @@ void choose_tiling(IgGeo& g, int mode) {
   // 16 x 256 tiles for M <= 16 (a forward / backward-data conv into 1-16 channels: no
   // 64-row tile mostly idle; the weight gradient's columns are gathers, kept at 64); 128 x 128 (4x the MFMA work per staged chunk) when M, N are large;
   // else 64 x 64
+  // the weight gradient decides on its filter columns alone (the bias column would change
+  // the split count, and with it the summation order: dw must not depend on bias_grad)
+  const int ncol = mode == 2 ? g.wcols : g.Ncol;
   int tm, tn;
   if (g.M <= 16 && mode != 2) {
     g.tile = 2; tm = 16; tn = 256;
-  } else if (g.M >= 128 && (int64_t)g.M * g.Ncol >= 128ll * 128 * cus / 2) {
+  } else if (g.M >= 128 && (int64_t)g.M * ncol >= 128ll * 128 * cus / 2) {
     g.tile = 1; tm = tn = 128;
   } else {
     g.tile = 0; tm = tn = 64;
   }
-  const int64_t tiles = bpk::ceil_div(g.M, tm) * bpk::ceil_div(g.Ncol, tn);
+  const int64_t tiles = bpk::ceil_div(g.M, tm) * bpk::ceil_div(ncol, tn);
   // split K until ~4 (64 x 64: 8) workgroups per CU for latency hiding, >= 8 chunks (128
   // of K) per split, partials within the workspace cap
   const int64_t want = (g.tile == 0 ? 8 : 4) * cus;
   int64_t splits = 1;
   if (tiles < want) splits = std::min<int64_t>(bpk::ceil_div(want, tiles), g.nchunk / 8);
-  const int64_t cap = kMaxWorkspace / ((int64_t)g.M * g.Ncol * 4);
+  const int64_t cap = kMaxWorkspace / ((int64_t)g.M * (mode == 2 ? g.wcols + 1 : g.Ncol) * 4);
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::min<int64_t>(cap, 4096)));
   g.chunks_per_split = (int)bpk::ceil_div(g.nchunk, splits);
   g.splits = (int)bpk::ceil_div(g.nchunk, g.chunks_per_split);
