@@ -67,6 +67,11 @@ struct IgGeo {
   // taps start at (rc0, sc0) and step by the stride
   int cy, cx, Hc, Wc, KHc, KWc, rc0, sc0;
   FDiv f_hwc, f_wc, f_khwc, f_kwc;
+  // tap-major K order (forward, stride-1 backward-data of 3x3 filters with Cc % 16 == 0):
+  // k = (r * KW + s) * Cc + c, Cc = Cin (forward) or Cout (backward-data), so a 16-wide
+  // K-chunk is 16 channels of ONE tap
+  int tap, Cc;
+  FDiv f_cc;
 };
 
 // k -> (co, r, s) of a MODE 3 class sub-filter tap
@@ -99,7 +104,7 @@ __device__ inline void split_tap(int k, const IgGeo& g, int& c, int& r, int& s) 
 
 // TM x TN outputs per workgroup of 4 waves (WMW along M x 4 / WMW along N; each wave
 // NBM x NBN MFMA blocks of 16 x 16), K chunks of 16 through double-buffered LDS
-template <int MODE, int KH_, int KW_, int TM, int TN, int WMW>
+template <int MODE, int KH_, int KW_, int TM, int TN, int WMW, bool TAP>
 __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0,
                                                     const float* __restrict__ B0,
                                                     const float* __restrict__ bias,
@@ -176,8 +181,30 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
   float ra[NLA], rb[NLB];
   auto gload = [&](int kc) {
     const int kb = kc * BK;
+    // tap-major chunk: one tap (r, s) for channels c0 .. c0 + 15 -- the gathers below need
+    // one bounds test and one address per chunk instead of a (c, r, s) split per element
+    int tap_rs = 0, tap_c0 = 0, tap_r = 0, tap_s = 0;
+    if (TAP) {
+      tap_rs = fdiv(kb, g.f_cc);
+      tap_c0 = kb - tap_rs * g.Cc;
+      tap_r = tap_rs / KW_;
+      tap_s = tap_rs - tap_r * KW_;
+    }
     // A
-    {
+    if (TAP) {
+#pragma unroll
+      for (int j = 0; j < NLA; ++j) {
+        const int m = m0 + am + 16 * j;
+        float v = 0.f;
+        if (m < g.M) {
+          if (MODE == 0)  // w[m][c][r][s]
+            v = A0[((int64_t)m * g.Cin + tap_c0 + ak) * (KH_ * KW_) + tap_rs];
+          else            // w[co][m][r][s]
+            v = A0[((int64_t)(tap_c0 + ak) * g.Cin + m) * (KH_ * KW_) + tap_rs];
+        }
+        ra[j] = v;
+      }
+    } else {
       const int k = kb + ak;
       int a_co = 0, a_rs = 0, a_n = 0, a_pix = 0;
       if (MODE == 1) {
@@ -212,7 +239,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
       }
     }
     // B
-    if (MODE != 2) {
+    if (TAP) {
+      int ty, tx, hh, ww;
+      if (MODE == 0) {
+        ty = py + tap_r; tx = px + tap_s; hh = g.H; ww = g.W;
+      } else {  // stride 1: the output pixel is the input pixel shifted back by the tap
+        ty = py - tap_r; tx = px - tap_s; hh = g.Ho; ww = g.Wo;
+      }
+      const bool ok = pvalid && ty >= 0 && ty < hh && tx >= 0 && tx < ww;
+      const int64_t cstride = (int64_t)hh * ww;
+      const float* bp = B0 + bbase + (int64_t)ty * ww + tx + (int64_t)(tap_c0 + bk) * cstride;
+#pragma unroll
+      for (int j = 0; j < NLB; ++j) rb[j] = ok ? bp[(int64_t)(kBStep * j) * cstride] : 0.f;
+    } else if (MODE != 2) {
 #pragma unroll
       for (int j = 0; j < NLB; ++j) {
         const int k = kb + bk + kBStep * j;
@@ -501,6 +540,10 @@ bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, 
   } else {
     g.M = Cout; g.Ncol = g.wcols + (bias_col ? 1 : 0); g.K = N * Ho * Wo;
   }
+  g.Cc = mode == 0 ? Cin : Cout;
+  g.tap = (mode == 0 || (mode == 1 && sh == 1 && sw == 1)) && KH == 3 && KW == 3 &&
+          g.Cc % BK == 0;
+  g.f_cc = make_fdiv(g.Cc);
   choose_tiling(g, mode);
   return true;
 }
@@ -509,6 +552,7 @@ bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, 
 // class holds no pixel
 bool make_geo_class(const IgGeo& base, int cy, int cx, IgGeo& g) {
   g = base;
+  g.tap = 0;
   g.cy = cy; g.cx = cx;
   g.Hc = (int)bpk::ceil_div(base.H - cy, base.sh);
   g.Wc = (int)bpk::ceil_div(base.W - cx, base.sw);
@@ -584,9 +628,12 @@ void launch_tile(const IgGeo& g, const float* A0, const float* B0, const float* 
   const dim3 grid((unsigned)bpk::ceil_div(g.Ncol, TN), (unsigned)bpk::ceil_div(g.M, TM),
                   (unsigned)g.splits);
 #define BPK_IG(KH_, KW_) \
-  igemm_kernel<MODE, KH_, KW_, TM, TN, WMW><<<grid, 256, 0, st>>>(A0, B0, bias, out, out2, wsp, g)
+  igemm_kernel<MODE, KH_, KW_, TM, TN, WMW, false><<<grid, 256, 0, st>>>(A0, B0, bias, out, out2, wsp, g)
   if (MODE == 3)  // class sub-filters: runtime tap arithmetic (split_tap_class)
     BPK_IG(0, 0);
+  else if ((MODE == 0 || MODE == 1) && g.tap)
+    igemm_kernel<(MODE == 0 ? 0 : 1), 3, 3, TM, TN, WMW, true><<<grid, 256, 0, st>>>(
+        A0, B0, bias, out, out2, wsp, g);
   else if (g.KH == 3 && g.KW == 3)
     BPK_IG(3, 3);
   else if (g.KH == 1 && g.KW == 1)
