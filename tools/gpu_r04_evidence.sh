@@ -10,3 +10,5 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r04_b8 -o 
 echo PROF_B8_OK
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r04_train -o train --output-format csv -- python tools/prof_train.py > gpurun_out/prof_r04_train.log 2>&1 || { tail gpurun_out/prof_r04_train.log; exit 1; }
 echo PROF_TRAIN_OK
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r04_pinn -o pinn --output-format csv -- python tools/prof_pinn.py > gpurun_out/prof_r04_pinn.log 2>&1 || { tail gpurun_out/prof_r04_pinn.log; exit 1; }
+echo PROF_PINN_OK
