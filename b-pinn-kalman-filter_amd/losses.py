@@ -346,7 +346,7 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
         return pinn_loss + data_loss, pinn_loss, data_loss
 
     if graph and train:
-        return _PinnGraphStep(loss_fn, optimize_fn, ctx)
+        return _PinnGraphStep(loss_fn, optimize_fn, ctx, config.optim.grad_clip)
 
     bucketer = [None]  # eager + sharded: gradient buckets all-reduced during backward
 
@@ -362,6 +362,11 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
             opt_pres.zero_grad()
             loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
             loss.backward()
+            # the values only: a returned loss that still carries the spent autograd graph
+            # keeps the parameters' AccumulateGrad nodes alive, and a hipGraph captured later
+            # on another stream (get_pinn_step_fn(graph=True)) then accumulates through them
+            # (stream mismatch: corrupted gradients, or a crash inside the capture)
+            loss, pinn_loss, data_loss = loss.detach(), pinn_loss.detach(), data_loss.detach()
             if bucketer[0] is not None:
                 bucketer[0].finish()  # buckets all-reduced while backward ran
             else:
@@ -420,8 +425,9 @@ class _PinnGraphStep:
     Sharded (ctx): gradients are averaged with one all-reduce per step after the replay.
     Reference losses.py:332-386."""
 
-    def __init__(self, loss_fn, optimize_fn, ctx):
+    def __init__(self, loss_fn, optimize_fn, ctx, grad_clip=-1.0):
         self.loss_fn, self.optimize_fn, self.ctx = loss_fn, optimize_fn, ctx
+        self.grad_clip = float(grad_clip)
         self.graph = None
         self.key = None
 
@@ -444,19 +450,62 @@ class _PinnGraphStep:
                     for p in params:
                         p.grad = None
                     loss, _pl, _dl = self.loss_fn(model, sop, self.static, self.noise)
-                    loss.backward()
+                    loss.backward(inputs=params)
+            # nothing of the warm-up may be freed while the capture runs: a block released
+            # mid-capture went back to the general pool and could be handed to the graph, which
+            # then shared it with eager allocations after the capture (replays read garbage a
+            # few steps later)
+            del loss, _pl, _dl
             torch.cuda.current_stream(dev).wait_stream(s)
             torch.cuda.synchronize(dev)
             for p in params:
                 p.grad = None
+            for b in self.static:
+                b.grad = None
+            # the host side reads eager-owned copies the graph writes (gradients, losses), and
+            # every reduction of the step -- the NaN probe, the clipping norms -- runs inside a
+            # captured graph: on this stack eager reduction kernels between replays (the
+            # gradient-norm clip, isnan().any(), a p.grad.abs().sum()) made later replays read
+            # garbage (fixed-parameter replays: identical losses without eager reductions, NaN
+            # from the third replay with them; elementwise eager work -- fills, copies, the
+            # fused Adam, the EMA lerp -- is harmless; tools/diag_pinn_graph_iso.py)
+            gbufs = [torch.zeros_like(p) for p in params]
+            obuf = torch.zeros(4, device=dev, dtype=torch.float32)
             g = torch.cuda.CUDAGraph()
             # captured on the warm-up stream: the parameters' AccumulateGrad nodes (created
-            # in the warm-up) record that stream
+            # in the warm-up) record that stream.  backward(inputs=params): the coordinate
+            # inputs' .grad (unused; the eager step accumulates them as the reference does)
+            # is neither computed nor accumulated by the replays
             with torch.cuda.graph(g, stream=s):
                 loss, pl, dl = self.loss_fn(model, sop, self.static, self.noise)
-                loss.backward()
-        self.out = (loss, pl, dl)
+                loss.backward(inputs=params)
+                live = [(gb, p.grad) for gb, p in zip(gbufs, params) if p.grad is not None]
+                torch._foreach_copy_([a for a, _ in live], [b for _, b in live])
+                obuf[:3].copy_(torch.stack([loss.detach(), pl.detach(), dl.detach()]))
+            # the graph's own gradient tensors stay referenced (their memory is the graph's);
+            # the parameters' .grad become the eager-owned copies from here on
+            self.graph_grads = [p.grad for p in params]
+            for p, gb in zip(params, gbufs):
+                p.grad = gb if p.grad is not None else None
+            # graph B, replayed after the (sharded: all-reduced) gradients are final: the
+            # reference's NaN probe on the pressure net's last weight, then clip_grad_norm_ of
+            # each optimizer's parameters (optimization_manager; torch's formula)
+            w = model.pressurenet.end[-1].weight
+            groups = [[p.grad for p in m.parameters() if p.grad is not None]
+                      for m in (model.flownet, model.pressurenet)]
+            gb_ = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb_, stream=s):
+                obuf[3:].copy_(torch.isnan(w.grad).any().float().reshape(1))
+                if self.grad_clip >= 0:
+                    for grads in groups:
+                        norms = torch._foreach_norm(grads, 2.0)
+                        total = torch.linalg.vector_norm(torch.stack(norms), 2.0)
+                        coef = torch.clamp(self.grad_clip / (total + 1e-6), max=1.0)
+                        torch._foreach_mul_(grads, coef)
+        self.out = (obuf[0], obuf[1], obuf[2])
+        self.obuf = obuf
         self.graph = g
+        self.graph_b = gb_
         self.params = params
         self.key = (id(model), tuple((b.shape, b.dtype) for b in batch))
 
@@ -477,13 +526,15 @@ class _PinnGraphStep:
                 z.normal_()
         self.graph.replay()
         _sync_grads(self.params, self.ctx)
-        w = model.pressurenet.end[-1].weight
+        self.graph_b.replay()
         loss, pinn_loss, data_loss = (t.detach().clone() for t in self.out)
-        if w.grad is not None and torch.isnan(w.grad).any():
+        if bool(self.obuf[3].item()):
             print(">>> Nan Grad Detected <<<")
             return loss, pinn_loss, data_loss
-        self.optimize_fn(opt_flow, model.flownet.parameters(), step=state["step"])
-        self.optimize_fn(opt_pres, model.pressurenet.parameters(), step=state["step"])
+        # clipped inside graph B already
+        self.optimize_fn(opt_flow, model.flownet.parameters(), step=state["step"], grad_clip=-1.0)
+        self.optimize_fn(opt_pres, model.pressurenet.parameters(), step=state["step"],
+                         grad_clip=-1.0)
         state["step"] += 1
         state["ema"].update(model.parameters())
         return loss, pinn_loss, data_loss

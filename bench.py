@@ -808,11 +808,8 @@ def _pinn_run(args, ctx, dev):
     c.training.batch_size = B  # the per-rank batch: the observation masks are [B, 1, H, W]
     operator = get_operator(c)
     batch = pinn_batch(c, B, dev, seed=ctx.rank)
-    # FLOPs of one step: counted on an eager step (a graph replay launches nothing from
-    # Python), after one eager step that makes the per-call conv choices (their timing runs
-    # would be counted too)
-    eager_fn(state, operator, batch)
-    tally, _ = counted(lambda: eager_fn(state, operator, batch), dev)
+    if args.pinn_eager:  # the eager step's conv choices (their timing runs) before the count
+        eager_fn(state, operator, batch)
     for _ in range(args.pinn_warmup):  # the first graph-mode call captures the step
         step_fn(state, operator, batch)
     torch.cuda.synchronize(dev)
@@ -825,7 +822,13 @@ def _pinn_run(args, ctx, dev):
     ctx.barrier()
     torch.cuda.synchronize(dev)
     dt = ctx.all_reduce_max(time.perf_counter() - t0, dev)
-    return dt, (loss, pinn_loss, data_loss), tally, B
+    losses_ = tuple(float(v) for v in (loss, pinn_loss, data_loss))
+    # FLOPs of one step: counted on an eager step (a graph replay launches nothing from
+    # Python), after the timed region -- an eager step before the capture left later replays
+    # reading garbage on this stack (tools/diag_pinn_bench.py), and the graph's warm-up made
+    # the conv choices already
+    tally, _ = counted(lambda: eager_fn(state, operator, batch), dev)
+    return dt, losses_, tally, B
 
 
 def bench_pinn(args, ctx, dev):
@@ -849,7 +852,7 @@ def bench_pinn(args, ctx, dev):
             "pinn_ms_per_step": round(dt / args.pinn_steps * 1e3, 2),
             "pinn_mode": "eager" if args.pinn_eager else "hip_graph",
             "pinn_global_batch": B * ctx.world_size,
-            "pinn_losses": [round(float(v.item()), 6) for v in losses_],
+            "pinn_losses": [round(v, 6) for v in losses_],
             "pinn_config": "configs[3]: pinn_pde (FlowNet 2.49M + PressureNet 7.54M), 64x64"}
 
 
