@@ -2,7 +2,9 @@
 (MODE = train | cifar | pinn | dps) through bench.main with one timed step, and brackets the
 phase's single counted step (bench.counted: after the warm-up, outside the timed loop) with a
 marker dispatch of fused_bias_act_kernel on 256 floats (a kernel no bench phase launches).
-tools/pmc_summary.py sums FETCH_SIZE / WRITE_SIZE over the dispatches between the markers."""
+tools/pmc_summary.py sums FETCH_SIZE / WRITE_SIZE over the dispatches between the markers.
+The PINN phase runs its eager step (--pinn-eager): the counted step is eager in either mode,
+and the hipGraph capture of the timed step segfaulted under rocprofv3 --pmc (round 4)."""
 import os
 import sys
 
@@ -37,7 +39,7 @@ common = ["--steps", "1", "--warmup", "1", "--no-roofline", "--no-cpu-baseline",
 argv = {"train": ["--train-steps", "1", "--cifar-steps", "0", "--no-pinn", "--no-dps"],
         "cifar": ["--train-steps", "1", "--train-warmup", "0", "--cifar-steps", "1", "--no-pinn",
                   "--no-dps"],
-        "pinn": ["--no-train", "--pinn-steps", "1", "--pinn-warmup", "1", "--no-dps"],
+        "pinn": ["--no-train", "--pinn-steps", "1", "--pinn-warmup", "1", "--no-dps", "--pinn-eager"],
         "dps": ["--no-train", "--no-pinn", "--dps-steps", "1"]}[MODE]
 sys.argv = ["bench.py"] + common + argv
 bench.main()
