@@ -423,6 +423,10 @@ class _PinnGraphStep:
     draws, in the same order, as the eager step's two randn_like calls; a draw captured in
     the graph returned garbage on this stack -- data loss 32.6 vs 3.5, residual NaN).
     Sharded (ctx): gradients are averaged with one all-reduce per step after the replay.
+    Caveat (measured on this ROCm stack): aten reduction kernels run
+    eagerly between replays -- of any tensor -- corrupt later replays, so the NaN probe and the
+    gradient clipping are a second captured graph and the caller must not reduce on the device
+    between steps (float() of the returned losses is fine).
     Reference losses.py:332-386."""
 
     def __init__(self, loss_fn, optimize_fn, ctx, grad_clip=-1.0):

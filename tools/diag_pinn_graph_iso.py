@@ -43,6 +43,9 @@ for i in range(16):
     gsum = 0.0 if "nogsum" in mode else float(sum(
         p.grad.double().abs().sum() for p in model.parameters() if p.grad is not None))
     print(mode.split("-")[0], i, [round(v, 6) for v in vals], "gradsum", round(gsum, 6), flush=True)
+    if mode.startswith("redunrel"):  # eager reductions of tensors the graph never sees
+        for k in range(1, 40):
+            float(torch.randn((k * 7919) % 300000 + 1, device=dev).double().abs().sum())
     if mode.startswith("churn"):
         for k in range(1, 40):
             keep.append(torch.randn((k * 7919) % 300000 + 1, device=dev))
