@@ -113,42 +113,6 @@ constexpr int kPreMaxCin = 1024;        // pipelined kernel: GroupNorm affine ta
 // pre[n][cin] = (s, t) (bpk_group_norm_affine_f32): the patch load applies silu(x s + t)
 // (zero padding stays zero), so the normalized tensor is never written to HBM.
 // fast exp / reciprocal: a few ulp, far inside the network tolerance (1e-4)
-// Pipelined kernel's instruction schedule (A/B switch): 0 = side work fenced off between
-// the MFMA groups, 1 = free (compiler), 2 = interleaved, WINO_VPM VALU per MFMA
-#ifndef WINO_SCHED
-#define WINO_SCHED 0
-#endif
-#ifndef WINO_STAGGER
-#define WINO_STAGGER 0
-#endif
-#ifndef WINO_STAGGER_MODE
-#define WINO_STAGGER_MODE 0
-#endif
-#ifndef WINO_VPM
-#define WINO_VPM 4
-#endif
-#ifndef WINO_W8SPLIT
-#define WINO_W8SPLIT 0
-#endif
-// 8-wave form: waves 4-7 run their side work two MFMA groups after waves 0-3 (A/B)
-#ifndef WINO_W8ROT
-#define WINO_W8ROT 0
-#endif
-// prologue load order (A/B): 0 = patches 0-2, U(0), GroupNorm table; 1 = in consumption order
-#ifndef WINO_PRO
-#define WINO_PRO 0
-#endif
-// wave priority (A/B): 1 = s_setprio 2 through the prologue and the epilogue, 0 in the chunk
-// loop, so a starting / finishing workgroup's VALU is not starved by its co-resident
-// partner's loop (MI355X_MICROARCH.md: VALU issue is arbitrated by priority, then age)
-#ifndef WINO_PRIO
-#define WINO_PRIO 0
-#endif
-// 8-wave form (A/B): static s_setprio 1 for the second-dispatched half (waves 4-7) through the
-// chunk loop (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
-#ifndef WINO_PRIO8
-#define WINO_PRIO8 0
-#endif
 
 __device__ inline float silu_f(float z) { return z * __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 
@@ -532,22 +496,11 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
   __shared__ float2 s_ss[PRE ? kPreMaxCin : 1];  // PRE: (s, t) of every input channel
 
   WINO_TS(0);
-#if WINO_PRIO
-  __builtin_amdgcn_s_setprio(2);
-#endif
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   // grid < 2^31 blocks (host check): 32-bit block arithmetic
   const unsigned nblk = gridDim.x;
   unsigned b = blockIdx.x;
-#if WINO_STAGGER > 0
-  // first-round stagger (A/B): the two workgroups resident on a CU otherwise start, and
-  // keep running, in phase -- both in prologue / epilogue at once
-  if (nblk >= 1024 && (WINO_STAGGER_MODE == 0 ? (b >= 256u && b < 512u)
-                                               : (b < 512u && ((b >> 3) & 1u)))) {
-    for (int i = 0; i < WINO_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
   unsigned cb, rx, ry;
   unsigned r = udivmod(b, (unsigned)g.cout_blocks, cb);
@@ -557,18 +510,11 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
   const int cout_w = (int)cb * (WG * kWN) + wave * kWN;
   static_assert(WG == 4 || (WG == 8 && NB == 1), "8-wave form: NB = 1");
   // 8 waves: waves 0-3 stage channels 0-3 of a chunk and transform V, waves 4-7 stage
-  // channels 4-7 (wave-uniform, in SGPRs)
-  // WINO_W8SPLIT (A/B): waves 0-3 only transform V and waves 4-7 only stage the patches (all 8
-  // channels per thread) inside the chunk loop, so the two waves of a SIMD do different side
-  // work -- as written the role branches make the compiler spill (118 VGPRs), so it is off
-  constexpr bool kSplit = WG == 8 && WINO_W8SPLIT;
-  constexpr int kCT = kSplit ? kCK : kCK * 4 / WG;  // channels staged per thread
-  const int ph = WG == 8 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
-  const int phc = kSplit ? 0 : ph;  // channel half staged by this thread
-  // every wave transforms (waves w and w + 4 write the same V records, identical values): a
-  // wave-uniform branch around the transform made the compiler spill
-  const bool xf = !kSplit || ph == 0;
-  const bool pw = !kSplit || ph != 0;
+  // channels 4-7 (wave-uniform, in SGPRs).  Every wave transforms (waves w and w + 4 write the
+  // same V records, identical values): a wave-uniform branch around the transform, or waves
+  // with split roles, made the compiler spill
+  constexpr int kCT = kCK * 4 / WG;  // channels staged per thread
+  const int phc = WG == 8 ? __builtin_amdgcn_readfirstlane(tid >> 8) : 0;
 
   // accumulators: the first chunk's k-step 0 MFMAs take an inline-constant zero C operand
   // (no 128 register clears in the prologue)
@@ -682,31 +628,6 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
   // global loads of patches 0-2, U(0) and the GroupNorm table are all issued before the
   // first wait, so a workgroup pays one memory latency here, not four.
   float pv0[kCT], pv1[kCT];
-#if WINO_PRO == 1
-  // loads in the order they are consumed (vmcnt is in order): GroupNorm table, patches 0 / 1,
-  // U(0), patch 2 -- the patch stores and the first transform wait only for what they read
-  float2 ssv[PRE ? kPreMaxCin / 256 : 1];
-  if (PRE) {
-#pragma unroll
-    for (int i = 0; i < kPreMaxCin / 256; ++i)
-      if (tid + 256 * i < g.Cin) ssv[i] = pre_n[tid + 256 * i];  // (WG = 4 only)
-  }
-  load_patch(0);
-#pragma unroll
-  for (int c = 0; c < kCT; ++c) pv0[c] = pv[c];
-  load_patch(1);
-#pragma unroll
-  for (int c = 0; c < kCT; ++c) pv1[c] = pv[c];
-  load_u(0, 0);
-  load_u(1, 0);
-  load_patch(2);
-  if (PRE) {
-#pragma unroll
-    for (int i = 0; i < kPreMaxCin / 256; ++i)
-      if (tid + 256 * i < g.Cin) s_ss[tid + 256 * i] = ssv[i];
-    __syncthreads();
-  }
-#else
   load_patch(0);
 #pragma unroll
   for (int c = 0; c < kCT; ++c) pv0[c] = pv[c];
@@ -720,16 +641,13 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
     for (int c = tid; c < g.Cin; c += 64 * WG) s_ss[c] = pre_n[c];
     __syncthreads();
   }
-#endif
   WINO_TS(1);
   store_patch_from(pv0, s_patch_raw[0], 0);
   store_patch_from(pv1, s_patch_raw[1], 1);
   __syncthreads();
   WINO_TS(2);
-  if (xf) {
-    read_d(s_patch_raw[0]);
-    write_v(s_v[0]);
-  }
+  read_d(s_patch_raw[0]);
+  write_v(s_v[0]);
   __syncthreads();
 
   // A operands a[q] = V[pos 4q..4q+3] of (ks, mb) = this lane's tile row of one LDS record;
@@ -746,34 +664,24 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
 #pragma unroll
     for (int q = 0; q < 4; ++q) a[q] = src[q];
   }
-  // ROT: the side work of the 8-wave form's waves 4-7 runs two MFMA groups later than that of
-  // waves 0-3 (store + load of the patches first, then the V transform), so the two waves of a
-  // SIMD -- one from each half, in step through the same barriers -- never run their
-  // GroupNorm+SiLU patch stores at the same time
   // TM: 0 = full side work, 1 = no patch load (chunk nch - 3), 2 = no patch load / store
   // (nch - 2), 3 = the last chunk: no side work, no filter prefetch, no barrier
-  auto step = [&](int k, auto sb_c, auto first_c, auto rot_c,
-                  auto tm_c) __attribute__((always_inline)) {
+  auto step = [&](int k, auto sb_c, auto first_c, auto tm_c) __attribute__((always_inline)) {
     constexpr int SB = decltype(sb_c)::value;
     constexpr bool FIRST = decltype(first_c)::value;
-    constexpr int ROT = decltype(rot_c)::value;
     constexpr int TM = decltype(tm_c)::value;
     const float* sv = s_v[SB];
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
       const int ks = grp >> 1, mb = grp & 1;
-      const int sw = (grp + ROT) & 3;
-      // side work of the next chunks, spread over the four MFMA groups
-#if WINO_SCHED == 0 || WINO_SCHED == 4
+      // side work of the next chunks, spread over the four MFMA groups and fenced off from
+      // the MFMAs (free / interleaved schedules measured slower, round 2)
       __builtin_amdgcn_sched_barrier(0);
-#endif
-      if (TM < 3 && sw == 0 && xf) read_d(s_patch_raw[SB ^ 1]);  // patch(k+1)
-      if (TM < 3 && sw == 1 && xf) write_v(s_v[SB ^ 1]);         // V(k+1)
-      if (TM < 2 && sw == 2 && pw) store_patch(s_patch_raw[SB], k + 2);  // patch(k+2)
-      if (TM < 1 && sw == 3 && pw) load_patch(k + 3);
-#if WINO_SCHED == 0
+      if (TM < 3 && grp == 0) read_d(s_patch_raw[SB ^ 1]);  // patch(k+1)
+      if (TM < 3 && grp == 1) write_v(s_v[SB ^ 1]);         // V(k+1)
+      if (TM < 2 && grp == 2) store_patch(s_patch_raw[SB], k + 2);  // patch(k+2)
+      if (TM < 1 && grp == 3) load_patch(k + 3);
       __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -796,19 +704,6 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
           }
         }
       }
-#if WINO_SCHED >= 2
-      // the group's side work interleaved into its MFMA stream: each MFMA's 32-cycle
-      // issue shadow covers a few of the wave's own VALU / LDS instructions
-#pragma unroll
-      for (int i = 0; i < 16 * NB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, WINO_VPM, 0);  // VALU
-#if WINO_SCHED == 2
-        __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);  // DS
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM
-#endif
-      }
-#endif
     }
     if constexpr (TM < 3) {
       __syncthreads();
@@ -821,46 +716,30 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
   using C1 = std::integral_constant<int, 1>;
   using F = std::false_type;
   WINO_TS(3);
-#if WINO_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
-#if WINO_PRIO8
-  if (WG == 8 && ph) __builtin_amdgcn_s_setprio(1);
-#endif
   using T0 = std::integral_constant<int, 0>;
-  auto run = [&](auto rot_c) __attribute__((always_inline)) {
-    step(0, C0{}, std::true_type{}, rot_c, T0{});
+  auto run = [&]() __attribute__((always_inline)) {
+    step(0, C0{}, std::true_type{}, T0{});
     int k = 1;
     if constexpr (TAIL) {  // nch even, >= 4: chunks nch - 3, nch - 2, nch - 1 have SB 1, 0, 1
       for (; k + 1 <= nch - 4; k += 2) {
-        step(k, C1{}, F{}, rot_c, T0{});
-        step(k + 1, C0{}, F{}, rot_c, T0{});
+        step(k, C1{}, F{}, T0{});
+        step(k + 1, C0{}, F{}, T0{});
       }
-      step(k, C1{}, F{}, rot_c, std::integral_constant<int, 1>{});
-      step(k + 1, C0{}, F{}, rot_c, std::integral_constant<int, 2>{});
-      step(k + 2, C1{}, F{}, rot_c, std::integral_constant<int, 3>{});
+      step(k, C1{}, F{}, std::integral_constant<int, 1>{});
+      step(k + 1, C0{}, F{}, std::integral_constant<int, 2>{});
+      step(k + 2, C1{}, F{}, std::integral_constant<int, 3>{});
     } else {
       for (; k + 1 < nch; k += 2) {
-        step(k, C1{}, F{}, rot_c, T0{});
-        step(k + 1, C0{}, F{}, rot_c, T0{});
+        step(k, C1{}, F{}, T0{});
+        step(k + 1, C0{}, F{}, T0{});
       }
-      if (k < nch) step(k, C1{}, F{}, rot_c, T0{});
+      if (k < nch) step(k, C1{}, F{}, T0{});
     }
   };
   // (one call site per instantiation: a second, dead one stopped the inliner and put the
   // accumulators in scratch)
-  if constexpr (WG == 8 && WINO_W8ROT) {
-    if (ph)
-      run(std::integral_constant<int, 2>{});
-    else
-      run(std::integral_constant<int, 0>{});
-  } else {
-    run(std::integral_constant<int, 0>{});
-  }
+  run();
   WINO_TS(4);
-#if WINO_PRIO
-  __builtin_amdgcn_s_setprio(2);
-#endif
 
   // output transform straight from registers to global memory (no LDS staging, no
   // barrier).  Per M-block a lane holds tiles m = 16 mb + 4 kq + rg, rg = 0..3: tile row

@@ -508,6 +508,7 @@ class _PinnGraphStep:
                         torch._foreach_mul_(grads, coef)
         self.out = (obuf[0], obuf[1], obuf[2])
         self.obuf = obuf
+        self.gbufs = [p.grad for p in params]
         self.graph = g
         self.graph_b = gb_
         self.params = params
@@ -521,6 +522,12 @@ class _PinnGraphStep:
         key = (id(model), tuple((b.shape, b.dtype) for b in batch))
         if self.graph is None or key != self.key:
             self._capture(model, operator, batch)
+        # the optimizers read p.grad: point it back at the buffers the graphs write, in case a
+        # caller's zero_grad(set_to_none=True) or an eager step replaced it since the last call
+        #  -- else Adam would apply stale gradients, or skip every parameter
+        for p, gb in zip(self.params, self.gbufs):
+            if p.grad is not gb:
+                p.grad = gb
         with torch.no_grad():
             for d, b in zip(self.static, batch):
                 d.copy_(b)

@@ -28,17 +28,31 @@ def gemm_sb(a, b, bias=None, bias_mode=0, alpha=1.0, out=None):
     two = a.dim() == 2 and b.dim() == 2
     a3 = a if a.dim() == 3 else a.unsqueeze(0)
     b3 = b if b.dim() == 3 else b.unsqueeze(0)
-    batch = max(a3.shape[0], b3.shape[0])
+    ba, bb = a3.shape[0], b3.shape[0]
+    if a3.dim() != 3 or b3.dim() != 3 or not (ba == bb or ba == 1 or bb == 1):
+        raise RuntimeError(f"gemm_sb: batch sizes {tuple(a.shape)} x {tuple(b.shape)} "
+                           "(equal, or one of them 1 and broadcast)")
+    batch = max(ba, bb)
     M, K = a3.shape[1], a3.shape[2]
     if b3.shape[1] != K:
         raise RuntimeError(f"gemm_sb: inner sizes {tuple(a.shape)} x {tuple(b.shape)}")
     N = b3.shape[2]
-    sa = (0 if a3.shape[0] == 1 else a3.stride(0),) + tuple(a3.stride()[1:])
-    sb = (0 if b3.shape[0] == 1 else b3.stride(0),) + tuple(b3.stride()[1:])
+    sa = (0 if ba == 1 else a3.stride(0),) + tuple(a3.stride()[1:])
+    sb = (0 if bb == 1 else b3.stride(0),) + tuple(b3.stride()[1:])
     acc = out is not None
+    if acc:
+        want = (M, N) if (two and out.dim() == 2) else (batch, M, N)
+        if (tuple(out.shape) != want or out.dtype != torch.float32 or not out.is_cuda
+                or out.device != a.device):
+            raise RuntimeError(f"gemm_sb: out {tuple(out.shape)} {out.dtype} on {out.device}, "
+                               f"expected float32 {want} on {a.device}")
     c = out if acc else torch.empty((batch, M, N), dtype=torch.float32, device=a.device)
     c3 = c if c.dim() == 3 else c.unsqueeze(0)
     bias_c = None if bias is None else bias.detach().contiguous()
+    if (bias_c is not None and bias_mode in (1, 2)
+            and bias_c.numel() != (N if bias_mode == 1 else M)):
+        raise RuntimeError(f"gemm_sb: bias of {bias_c.numel()} values for bias_mode {bias_mode} "
+                           f"(M {M}, N {N})")
     check(lib.bpk_gemm_sb_f32(a3.data_ptr(), *sa, b3.data_ptr(), *sb, c3.data_ptr(),
                               *_strides3(c3), None if bias_c is None else bias_c.data_ptr(),
                               bias_mode if bias_c is not None else 0, float(alpha), int(acc),

@@ -1440,6 +1440,20 @@ def test_gemm_sb_strided_operands_vs_fp64(hip, ta, tb, batch, M, N, K):
     assert (acc.double() - want).abs().max().item() <= 1e-5 * want.abs().max().item()
 
 
+def test_gemm_sb_rejects_mismatched_shapes(hip):
+    """Batch sizes that are neither equal nor 1, a wrong `out` and a bias of the wrong length
+    raise before any launch (mismatched batches read past the smaller operand)."""
+    from op.matmul import gemm_sb
+    a, b = torch.randn(2, 8, 4, device=hip), torch.randn(3, 4, 5, device=hip)
+    with pytest.raises(RuntimeError, match="batch"):
+        gemm_sb(a, b)
+    with pytest.raises(RuntimeError, match="out"):
+        gemm_sb(a, b[:2], out=torch.zeros(2, 8, 6, device=hip))
+    with pytest.raises(RuntimeError, match="bias"):
+        gemm_sb(a, b[:2], torch.zeros(4, device=hip), 1)
+    assert gemm_sb(a, b[:1]).shape == (2, 8, 5)  # batch 1 broadcasts
+
+
 def test_linear_native_gradients_vs_fp64(hip):
     """op.matmul.linear (nn.Linear on the native GEMM: the time-embedding MLP / Dense_0) --
     output, first and second derivatives w.r.t. x, W, b vs float64 torch (2e-5 relative)."""
