@@ -36,7 +36,7 @@ constexpr int kRec = 20;             // LDS stride of one 16-position record
 
 struct WgradGeo {
   int N, Cin, Cout, H, W;
-  int strips_x, strips_y;  // W / 16, H / 2
+  int strips_x, strips_y;  // W / 16, H / 2 (PAIR: 1, H / 2; a strip = 2 rows of two images)
   int cin_blocks, cout_blocks, splits;
   int64_t chunks;          // N * strips_y * strips_x
 };
@@ -63,7 +63,11 @@ constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records
 // 7.06 vs 5.20 at 256->256 @128^2; DSM train 2.59 vs 2.87 steps/s, same box) -- the halved
 // residency exposes the per-chunk barrier and load latency that two co-resident workgroups
 // hide -- and is not launched.
-template <int NB>
+// PAIR (8-pixel-wide images, CIFAR-10's 8 x 8 level): a chunk's 2 x 16 strip is the same two
+// rows of images 2p (tiles 0-3) and 2p + 1 (tiles 4-7); each image's halo columns are padding
+// (always zero), so a patch row is [0 | A x0..7 | 0 0 | B x0..7 | 0] and the gradient tiles of
+// k-step ks come from image 2p + ks.  Strip cursor: n = pair, strips_x = 1.
+template <int NB, bool PAIR = false>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ part,
     float* __restrict__ part_b, WgradGeo g, int xcd_remap) {
@@ -149,8 +153,8 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   auto load_x = [&]() {  // patch of chunk xcur, then advance
     const Strip s = xcur;
     advance(xcur);
-    const int oy0 = 2 * s.sy, ox0 = 16 * s.sx;
-    const float* base = x + ((int64_t)s.n * g.Cin + cin0) * plane;
+    const int oy0 = 2 * s.sy, ox0 = PAIR ? -8 * xh : 16 * s.sx;  // PAIR: half xh = image 2n + xh
+    const float* base = x + ((int64_t)(PAIR ? 2 * s.n + xh : s.n) * g.Cin + cin0) * plane;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(base), 0, kCB * plane * 4, 0x00020000);
     const int iy = oy0 - 1 + xpy;
@@ -174,6 +178,12 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   auto store_x = [&](float* sx) {
     float* row = sx + xc * kXCS + xpy * kXRS;
     const float z = xrow_ok ? 1.f : 0.f;
+    if (PAIR) {  // image xh's 8 pixels at columns 4 + 10 xh (8-byte aligned for xh = 1)
+      float2* r2 = reinterpret_cast<float2*>(row + 4 + 10 * xh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r2[e] = make_float2(xv[2 * e] * z, xv[2 * e + 1] * z);
+      return;
+    }
     *reinterpret_cast<f4*>(row + 4 + 8 * xh) = f4{xv[0] * z, xv[1] * z, xv[2] * z, xv[3] * z};
     *reinterpret_cast<f4*>(row + 8 + 8 * xh) = f4{xv[4] * z, xv[5] * z, xv[6] * z, xv[7] * z};
     row[xh ? 20 : 3] = (xrow_ok && xhalo_ok) ? xv[8] : 0.f;
@@ -181,12 +191,13 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
 
   // ---- V = B^T d B of one (tile, cin) per thread: c = tid >> 3, tile = tid & 7
   const int vc = tid >> 3, vt = tid & 7;
+  const int vcol = 3 + 2 * vt + (PAIR && vt >= 4 ? 2 : 0);  // PAIR: past image A's right halo
   float d[4][4];
   auto read_d = [&](const float* sx) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[i][j] = sx[vc * kXCS + i * kXRS + 3 + 2 * vt + j];
+      for (int j = 0; j < 4; ++j) d[i][j] = sx[vc * kXCS + i * kXRS + vcol + j];
   };
   auto write_v = [&](float* sv) {
     float t[4][4];
@@ -213,11 +224,12 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     advance(gcur);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
-      const float* src = gy + ((int64_t)s.n * g.Cout + gco + 16 * nb) * plane +
-                         (int64_t)(2 * s.sy) * g.W + 16 * s.sx;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const float* p = src + 2 * (4 * ks + kq);
+        // tile 4 ks + kq; PAIR: k-step ks is image 2n + ks, tile column kq
+        const float* src = gy + ((int64_t)(PAIR ? 2 * s.n + ks : s.n) * g.Cout + gco + 16 * nb) * plane +
+                           (int64_t)(2 * s.sy) * g.W + (PAIR ? 0 : 16 * s.sx);
+        const float* p = src + 2 * (PAIR ? kq : 4 * ks + kq);
         dst[nb][ks][0] = *reinterpret_cast<const float2*>(p);
         dst[nb][ks][1] = *reinterpret_cast<const float2*>(p + g.W);
       }
@@ -235,6 +247,12 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   };
 
   // ---- prologue
+  if (PAIR) {  // the padding columns 3, 12, 13, 22 of every patch row, both buffers: zero once
+    for (int i = tid; i < 2 * kCB * kXR; i += 256) {
+      float* row = s_x[i / (kCB * kXR)] + ((i % (kCB * kXR)) / kXR) * kXCS + (i % kXR) * kXRS;
+      row[3] = row[12] = row[13] = row[22] = 0.f;
+    }
+  }
   float xv0[9], xv1[9];
   bool ok0r, ok0h, ok1r, ok1h;
   load_x();
@@ -392,15 +410,18 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
 
 constexpr int kNB = 1;  // N-blocks per wave (see wino_wgrad_pipe_kernel)
 
+static bool wgrad_pair(int N, int W) { return W == 8 && N % 2 == 0; }
+
 WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
   WgradGeo g{};
   const int nb = kNB;
   g.N = N; g.Cin = Cin; g.Cout = Cout; g.H = H; g.W = W;
-  g.strips_x = W / 16;
+  const bool pair = wgrad_pair(N, W);
+  g.strips_x = pair ? 1 : W / 16;
   g.strips_y = H / 2;
   g.cin_blocks = Cin / kCB;
   g.cout_blocks = Cout / (kOB * nb);
-  g.chunks = (int64_t)N * g.strips_y * g.strips_x;
+  g.chunks = (int64_t)(pair ? N / 2 : N) * g.strips_y * g.strips_x;
   // ~512 resident workgroups' worth (two per CU at NB = 1, one at NB = 2, twice the work
   // each): enough K-splits to fill the chip, no more (each split adds a [Cin][Cout][16]
   // partial slab to write and re-read)
@@ -415,7 +436,7 @@ WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
 
 extern "C" int bpk_conv3x3_wino_wgrad_supported(int N, int Cin, int Cout, int H, int W) {
   return N > 0 && Cin > 0 && Cout > 0 && Cin % kCB == 0 && Cout % kOB == 0 && H % 2 == 0 &&
-         W % 16 == 0 && (int64_t)H * W * kCB * 4 < (1LL << 31);
+         (W % 16 == 0 || wgrad_pair(N, W)) && (int64_t)H * W * kCB * 4 < (1LL << 31);
 }
 
 extern "C" int64_t bpk_conv3x3_wino_wgrad_workspace_bytes(int N, int Cin, int Cout, int H,
@@ -437,7 +458,8 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
                                                int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_wgrad_supported(N, Cin, Cout, H, W),
               "conv3x3_wino_wgrad: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin "
-              "%% 32, Cout %% 64, H %% 2, W %% 16 == 0)", N, Cin, Cout, H, W);
+              "%% 32, Cout %% 64, H %% 2, W %% 16 == 0 or W == 8 with N even)", N, Cin, Cout,
+              H, W);
   BPK_REQUIRE(workspace != nullptr, "conv3x3_wino_wgrad: workspace is NULL");
   const WgradGeo g = make_geo(N, Cin, Cout, H, W);
   const int64_t blocks = (int64_t)g.splits * g.cin_blocks * g.cout_blocks;
@@ -445,8 +467,12 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
   float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
-  hipLaunchKernelGGL(wino_wgrad_pipe_kernel<kNB>, dim3((unsigned)blocks), dim3(256), 0, st, x,
-                     gy, workspace, part_b, g, remap);
+  if (wgrad_pair(N, W))
+    hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, true>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, x, gy, workspace, part_b, g, remap);
+  else
+    hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, false>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, x, gy, workspace, part_b, g, remap);
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
   BPK_REQUIRE(bpk::ceil_div(pairs, 16) < (1LL << 31), "conv3x3_wino_wgrad: too many pairs");

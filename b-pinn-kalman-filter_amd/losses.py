@@ -420,13 +420,12 @@ class _PinnGraphStep:
       * native kernels only inside the graph (op.conv.native_only: no MIOpen convs, no
         library workspace state), the conv choices made eagerly during the warm-up.
     The observation noise is drawn eagerly into static buffers before each replay (the same
-    draws, in the same order, as the eager step's two randn_like calls; a draw captured in
-    the graph returned garbage on this stack -- data loss 32.6 vs 3.5, residual NaN).
+    draws, in the same order, as the eager step's two randn_like calls).
     Sharded (ctx): gradients are averaged with one all-reduce per step after the replay.
-    Caveat (measured on this ROCm stack): aten reduction kernels run
-    eagerly between replays -- of any tensor -- corrupt later replays, so the NaN probe and the
-    gradient clipping are a second captured graph and the caller must not reduce on the device
-    between steps (float() of the returned losses is fine).
+    Replays are safe against any eager work between steps (an eval step, metrics, reductions,
+    RCCL calls) with the HIP runtime setting of op/_hipenv.py in effect: round 4's "eager
+    reductions corrupt later replays" was the runtime's graph packet capture reading kernel
+    arguments from the eager launch ring (root cause and measurements in op/_hipenv.py).
     Reference losses.py:332-386."""
 
     def __init__(self, loss_fn, optimize_fn, ctx, grad_clip=-1.0):
@@ -436,7 +435,9 @@ class _PinnGraphStep:
         self.key = None
 
     def _capture(self, model, operator, batch):
+        from op import _hipenv
         from op import conv as conv_op
+        _hipenv.warn_if_unsafe("get_pinn_step_fn(graph=True)")
         dev = batch[0].device
         self.static = [b.detach().clone() for b in batch]
         for i, b in enumerate(batch):
@@ -466,13 +467,8 @@ class _PinnGraphStep:
                 p.grad = None
             for b in self.static:
                 b.grad = None
-            # the host side reads eager-owned copies the graph writes (gradients, losses), and
-            # every reduction of the step -- the NaN probe, the clipping norms -- runs inside a
-            # captured graph: on this stack eager reduction kernels between replays (the
-            # gradient-norm clip, isnan().any(), a p.grad.abs().sum()) made later replays read
-            # garbage (fixed-parameter replays: identical losses without eager reductions, NaN
-            # from the third replay with them; elementwise eager work -- fills, copies, the
-            # fused Adam, the EMA lerp -- is harmless; tools/diag_pinn_graph_iso.py)
+            # the host side reads eager-owned copies the graph writes (gradients, losses); the
+            # NaN probe and the clipping norms run in a second captured graph (fewer launches)
             gbufs = [torch.zeros_like(p) for p in params]
             obuf = torch.zeros(4, device=dev, dtype=torch.float32)
             g = torch.cuda.CUDAGraph()

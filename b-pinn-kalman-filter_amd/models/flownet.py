@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from op import correlation, grid_sample
+from op.fused_act import LeakyReLU, leaky_relu
 
 from . import layers
 
@@ -58,7 +59,8 @@ def project(f, u, dt):
 
 
 def _lrelu():
-    return nn.LeakyReLU(negative_slope=0.1, inplace=False)
+    # nn.LeakyReLU(0.1) of the reference, on the native kernel (op.fused_act.LeakyReLU)
+    return LeakyReLU(negative_slope=0.1)
 
 
 def _conv3(cin, cout, stride=1):
@@ -140,7 +142,7 @@ class Matching(nn.Module):
         else:
             base = self.flow_upsample(flow)
             feature2 = project(feature2, base, -self.dt)
-        cost = F.leaky_relu(correlation.FunctionCorrelation(feature1, feature2, stride=1))
+        cost = leaky_relu(correlation.FunctionCorrelation(feature1, feature2, stride=1))
         return base + self.corr_conv(cost)
 
 

@@ -6,6 +6,7 @@ Mirrors the reference package `op/` (op/__init__.py:1-2): `upfirdn2d`,
 (`sde_kernels`).  All of them call libbpk.so through the C ABI of include/bpk.h; the
 reference's extension entry points are also registered with the dispatcher (`torch_ops`).
 """
+from . import _hipenv  # noqa: F401  (HIP runtime settings: before any device call)
 from .fused_act import FusedLeakyReLU, fused_leaky_relu
 from .upfirdn2d import upfirdn2d
 from . import correlation, grid_sample, ns_step, norm_act, sde_kernels

@@ -17,7 +17,8 @@ import os
 import re
 import threading
 
-import torch
+from . import _hipenv  # noqa: F401  (HIP runtime settings: before torch touches the device)
+import torch  # noqa: E402
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _REPO_ROOT = os.path.dirname(_PKG_ROOT)

@@ -36,6 +36,15 @@ def wino_supported(x, weight):
     return bool(lib.bpk_conv3x3_wino_supported(N, C, weight.shape[0], H, W))
 
 
+def wino_pair_supported(x, weight):
+    """The 16-cin Winograd kernel's two-images-per-region form (8-pixel-wide images: CIFAR-10's
+    8 x 8 level): one source, no GroupNorm statistics."""
+    if not _shape_ok(x, weight):
+        return False
+    N, C, H, W = x.shape
+    return bool(lib.bpk_conv3x3_wino_pair_supported(N, C, weight.shape[0], H, W))
+
+
 def small_supported(x, weight):
     """The VALU small-channel kernel (csrc/conv_small.hip): Cin <= 4 or Cout <= 4."""
     if not _shape_ok(x, weight):
@@ -610,7 +619,7 @@ def _fwd_impl(x, w, bias=None, skip=None, div=1.0):
     """conv(x, w) + bias [-> (skip + .) / div] without autograd: Winograd MFMA kernel,
     small-channel kernel, or MIOpen for the other shapes."""
     w = w.detach().contiguous()
-    if wino_supported(x, w):
+    if wino_supported(x, w) or wino_pair_supported(x, w):
         if _small_img(x) and igemm_supported(x, w, 1, 1):
             def ig():
                 y = conv2d_igemm_raw(x, w, None if bias is None else bias.detach(), 1, 1)
@@ -661,7 +670,8 @@ def _fwd_ft_impl(x, w):
     w = w.detach()
     N, C, H, W = x.shape
     if (C == w.shape[0] and x.is_cuda and x.dtype == torch.float32
-            and bool(lib.bpk_conv3x3_wino_supported(N, C, w.shape[1], H, W))):
+            and (bool(lib.bpk_conv3x3_wino_supported(N, C, w.shape[1], H, W))
+                 or bool(lib.bpk_conv3x3_wino_pair_supported(N, C, w.shape[1], H, W)))):
         if (_small_img(x) and _IGEMM and w.dtype == torch.float32
                 and _igemm_shape_ok((N, w.shape[1], H, W), tuple(w.shape), (1, 1), (1, 1))):
             key = ("d3", tuple(x.shape), tuple(w.shape))
@@ -822,7 +832,7 @@ def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
                 from .norm_act import residual_rescale
                 y = residual_rescale(skip, y, None, div)
             return y
-        if not wino_supported(x, weight):
+        if not (wino_supported(x, weight) or (not stats and wino_pair_supported(x, weight))):
             raise RuntimeError(f"conv3x3(pre=...): unsupported shape {tuple(x.shape)} x "
                                f"{tuple(weight.shape)}")
         return conv3x3_fwd_raw(x, weight, bias, skip, div, pre, stats)

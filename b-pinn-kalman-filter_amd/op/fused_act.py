@@ -9,6 +9,14 @@ and the double backward re-applies the same mask with the incoming bias grad
 Note: the reference's CPU branch hard-codes slope 0.2 (op/fused_act.py:91); this
 build has no CPU branch and always honours `negative_slope`, matching the
 reference's GPU semantics.
+
+`leaky_relu` / `LeakyReLU`: the plain activation (no bias, scale 1) of FlowNet (reference
+models/flownet.py: nn.LeakyReLU(0.1) after every conv, F.leaky_relu of the cost volume) on the
+same kernel, bit-identical to aten's (out > 0 selects the same branch as x > 0 for a positive
+slope).  Its backward is a Function of the output gradient only: the mask is piecewise constant,
+so its derivative w.r.t. the activation is zero -- which aten's leaky_relu_backward
+materializes (zeros_like + an accumulating add per node) on every pass of the PINN residual's
+double backward.
 """
 from __future__ import annotations
 
@@ -75,6 +83,58 @@ class _FusedLeakyReLUFn(Function):
         gi, gb = _FusedLeakyReLUGrad.apply(grad_output.contiguous(), out, ctx.negative_slope,
                                            ctx.scale)
         return gi, gb, None, None
+
+
+class _LeakyReLUGrad(Function):
+    """g * (out > 0 ? 1 : slope): the backward of leaky_relu, linear in g (its own backward is
+    itself), no gradient w.r.t. the mask source `out`."""
+
+    @staticmethod
+    def forward(ctx, g, out, negative_slope):
+        ctx.save_for_backward(out)
+        ctx.negative_slope = negative_slope
+        return fused_bias_act_raw(g, None, out, 3, 1, negative_slope, 1.0)
+
+    @staticmethod
+    def backward(ctx, gg):
+        out, = ctx.saved_tensors
+        return _LeakyReLUGrad.apply(gg.contiguous(), out, ctx.negative_slope), None, None
+
+
+class _LeakyReLU(Function):
+    @staticmethod
+    def forward(ctx, x, negative_slope):
+        out = fused_bias_act_raw(x, None, None, 3, 0, negative_slope, 1.0)
+        ctx.save_for_backward(out)
+        ctx.negative_slope = negative_slope
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out, = ctx.saved_tensors
+        return _LeakyReLUGrad.apply(g.contiguous(), out, ctx.negative_slope), None
+
+
+def leaky_relu(input, negative_slope=0.01):
+    """F.leaky_relu(input, negative_slope) on the native kernel, differentiable to any order."""
+    require_hip(input, what="leaky_relu")
+    if negative_slope <= 0:
+        raise RuntimeError("leaky_relu: the output-sign mask needs negative_slope > 0")
+    return _LeakyReLU.apply(input, float(negative_slope))
+
+
+class LeakyReLU(nn.Module):
+    """nn.LeakyReLU(negative_slope) on the native kernel (no parameters, no state-dict keys)."""
+
+    def __init__(self, negative_slope=0.01, inplace=False):
+        super().__init__()
+        self.negative_slope = negative_slope
+
+    def forward(self, input):
+        return leaky_relu(input, self.negative_slope)
+
+    def extra_repr(self):
+        return f"negative_slope={self.negative_slope}"
 
 
 def fused_leaky_relu(input, bias, negative_slope=0.2, scale=2 ** 0.5):

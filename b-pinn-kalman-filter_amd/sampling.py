@@ -589,6 +589,8 @@ class PCEngine:
             self._capture_graphs(model, x, x_mean)
 
     def _capture_graphs(self, model, x, x_mean):
+        from op import _hipenv
+        _hipenv.warn_if_unsafe("PCEngine(use_graph=True)")
         # static buffers owned by the graph
         self._gx = x.clone()
         self._gxm = x_mean.clone()

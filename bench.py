@@ -37,6 +37,7 @@ sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
 _MIOPEN_CACHE = os.path.join(REPO, "b-pinn-kalman-filter_amd", "miopen_cache")
 os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_MIOPEN_CACHE, "kernels"))
 os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_MIOPEN_CACHE, "db"))
+from op import _hipenv  # noqa: E402,F401  (HIP graph-replay setting, before torch)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -363,10 +364,14 @@ def upfirdn_rooflines(dev, batch):
 
 
 def cpu_upfirdn_baseline():
-    """The oracle's torch-CPU upfirdn2d (the reference's upfirdn2d_native algorithm: zero
-    insertion, pad, conv2d with the flipped kernel, stride) on bounded samples of the four
-    8(d) shapes (batch 4 instead of 64), best of 5, algorithmic GB/s."""
-    from oracle.upfirdn2d_ref import upfirdn2d_torch
+    """The reference CPU path's own op sequence (oracle.upfirdn2d_ref.upfirdn2d_native_seq:
+    zero insertion by padding, crop, a single-channel conv2d at full resolution, then the
+    [::down] slice -- reference op/upfirdn2d.py:159-200) on bounded samples of the four 8(d)
+    shapes (batch 4 instead of 64), best of 5, algorithmic GB/s.  (Round 4 timed a strided-conv
+    restatement instead: oneDNN ran the 1-channel down2 conv of [1024, 1, 66, 66] planes on a
+    direct kernel and the other shapes on its generic path, one shape at 40 GB/s and the rest at
+    0.4-1.5.)"""
+    from oracle.upfirdn2d_ref import upfirdn2d_native_seq as upfirdn2d_torch
     k = torch.tensor(np.outer([1, 3, 3, 1], [1, 3, 3, 1]) / 64.0, dtype=torch.float32)
     res = {}
     for name, (c, hw), kw, gain in UPFIRDN_SHAPES:
@@ -378,7 +383,8 @@ def cpu_upfirdn_baseline():
             best = min(best, time.perf_counter() - t0)
         res[name] = round(4.0 * (x.numel() + y.numel()) / best / 1e9, 3)
     return {"value": res, "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": "oracle.upfirdn2d_ref.upfirdn2d_torch on the 8(d) shapes at batch 4, best of 5"}
+            "sample": "oracle.upfirdn2d_ref.upfirdn2d_native_seq (the reference's CPU op sequence) "
+                      "on the 8(d) shapes at batch 4, best of 5"}
 
 
 def _cpu_model():

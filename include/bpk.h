@@ -355,6 +355,11 @@ int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout
 int bpk_conv3x3_wino_filter_ft_f32(const float* weight, float* U, int Cin, int Cout,
                                    void* stream);
 int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W);
+/* The 16-cin kernel's pair form, used by bpk_conv3x3_wino_ex_f32 / _splitk_f32 when W == 8 (and
+ * the W % 16 form does not apply): two 8 x 8 images side by side per 8 x 16 region -- N even,
+ * H % 8, Cin % 16, Cout % 128 == 0, one source, no statistics (CIFAR-10's 8 x 8 level,
+ * reference configs/vp/cifar10_ncsnpp_continuous.py:41-64 ch_mult (1, 2, 2, 2)). */
+int bpk_conv3x3_wino_pair_supported(int N, int Cin, int Cout, int H, int W);
 int bpk_conv3x3_wino_f32(const float* x, const float* U, const float* bias, float* y, int N,
                          int Cin, int Cout, int H, int W, void* stream);
 /* Same conv with the residual-block tail fused into the epilogue (layerspp.py:272-274,

@@ -4,7 +4,10 @@ Follows `upfirdn2d_native` (reference op/upfirdn2d.py:159-200): zero-insert
 upsample, pad (negative = crop), convolve with the 180-degree-rotated kernel,
 keep every `down`-th sample.  Two forms:
   * `upfirdn2d_np`   : numpy tap loop (any dtype), the independent checker;
-  * `upfirdn2d_torch`: torch-CPU conv2d form (fast; used by nets_ref / cpu baseline).
+  * `upfirdn2d_torch`: torch-CPU conv2d form (fast; used by nets_ref);
+  * `upfirdn2d_native_seq`: the reference's own CPU op sequence, step for step (pad-based zero
+    insertion, crop, 1-channel F.conv2d at full resolution, then the `[::down]` slice) -- the
+    upfirdn2d CPU baseline of bench.py times this one.
 """
 from __future__ import annotations
 
@@ -61,3 +64,27 @@ def upfirdn2d_torch(x, k, up=1, down=1, pad=(0, 0)):
     w = torch.flip(k, [0, 1]).to(x.dtype).reshape(1, 1, kh, kw)
     out = F.conv2d(U.reshape(N * C, 1, U.shape[2], U.shape[3]), w, stride=down)
     return out.reshape(N, C, out.shape[2], out.shape[3])
+
+
+def upfirdn2d_native_seq(x, k, up=1, down=1, pad=(0, 0)):
+    """The reference CPU path's op sequence (op/upfirdn2d.py:159-200, `upfirdn2d_native` with
+    the symmetric (up, down, pad) of `upfirdn2d`, op/upfirdn2d.py:145-156): the view/pad zero
+    insertion, the pad + crop, one single-channel conv2d over every plane at the upsampled
+    resolution, and the stride taken afterwards by slicing (so a down-2 op convolves 4x the
+    output pixels, as the reference does)."""
+    _, channel, in_h, in_w = x.shape
+    kh, kw = k.shape
+    p0, p1 = pad
+    out = x.reshape(-1, in_h, 1, in_w, 1, 1)
+    out = F.pad(out, [0, 0, 0, up - 1, 0, 0, 0, up - 1])
+    out = out.view(-1, in_h * up, in_w * up, 1)
+    out = F.pad(out, [0, 0, max(p0, 0), max(p1, 0), max(p0, 0), max(p1, 0)])
+    out = out[:, max(-p0, 0):out.shape[1] - max(-p1, 0), max(-p0, 0):out.shape[2] - max(-p1, 0), :]
+    out = out.permute(0, 3, 1, 2).reshape(-1, 1, in_h * up + p0 + p1, in_w * up + p0 + p1)
+    w = torch.flip(k, [0, 1]).view(1, 1, kh, kw).to(x.dtype)
+    out = F.conv2d(out, w)
+    out = out.reshape(-1, 1, in_h * up + p0 + p1 - kh + 1, in_w * up + p0 + p1 - kw + 1)
+    out = out.permute(0, 2, 3, 1)[:, ::down, ::down, :]
+    oh = (in_h * up + p0 + p1 - kh) // down + 1
+    ow = (in_w * up + p0 + p1 - kw) // down + 1
+    return out.reshape(-1, channel, oh, ow)

@@ -11,6 +11,7 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 for p in (PKG, REPO):
     if p not in sys.path:
         sys.path.insert(0, p)
+from op import _hipenv  # noqa: E402,F401  (HIP graph-replay setting, before any device call)
 
 
 def pytest_configure(config):

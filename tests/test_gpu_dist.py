@@ -253,6 +253,69 @@ def test_nan_on_one_rank_makes_every_rank_skip():
         np.testing.assert_array_equal(p1, p0)
 
 
+def _pinn_graph_worker(rank, world, port, q):
+    """4 PINN train steps of the sharded graph step and of the sharded eager step (same model,
+    batch shard and noise) on this rank; returns both runs' losses and final parameters."""
+    try:
+        ctx = _setup(rank, world, port)
+        import copy
+
+        import losses
+        from configs.pinn import pinn_pde
+        from conftest import build_pinn_weights, load_golden, small_config
+        from inverse.operators import InpaintOperator
+        from models.ema import ExponentialMovingAverage
+        from op import conv as conv_op
+        from pinn_kalman.pinn import PINN
+        dev = torch.device("cuda:0")
+        c = small_config(pinn_pde.get_config)
+        m0 = build_pinn_weights(PINN, c).to(dev)
+        c.device = dev
+        d = load_golden("pinn_step.npz")
+        B = 2 // world
+        sl = slice(rank * B, (rank + 1) * B)
+        T = lambda k: torch.tensor(d[k][sl].copy(), device=dev)
+        out = {}
+        for graph in (True, False):
+            m = copy.deepcopy(m0)
+            em = ExponentialMovingAverage(m.parameters(), decay=c.model.ema_rate)
+            state = dict(optimizer=(losses.get_optimizer(c, m.flownet.parameters()),
+                                    losses.get_optimizer(c, m.pressurenet.parameters(), 0.001)),
+                         model=m, ema=em, step=50)
+            op = InpaintOperator(mask=[torch.tensor(d["mask"][sl].copy(), device=dev)])
+            step_fn = losses.get_pinn_step_fn(c, train=True, ctx=ctx, graph=graph,
+                                              optimize_fn=losses.optimization_manager(c))
+            ls = []
+            torch.manual_seed(11 + rank)
+            with conv_op.native_only():
+                for _ in range(4):
+                    batch = (T("f1"), T("f2"), T("x").requires_grad_(), T("y").requires_grad_(),
+                             T("t").requires_grad_(), T("target"))
+                    ls.append([float(v) for v in step_fn(state, op, batch)])
+            out[graph] = (ls, torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy())
+        q.put((rank, out, None))
+        torch.distributed.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_sharded_pinn_graph_step_matches_sharded_eager_step():
+    """get_pinn_step_fn(graph=True, ctx=...) on 2 ranks (the gradient all-reduce runs eagerly
+    between the two graph replays of a step): losses of 4 steps and the final parameters ==
+    the sharded eager step's on each rank, and the two ranks' replicas stay identical
+    (the multi-rank graph path compared with the eager one)."""
+    two = _run(_pinn_graph_worker, 2, )
+    for _, out, _ in two:
+        lg, pg = out[True]
+        le, pe = out[False]
+        lg, le = np.array(lg), np.array(le)
+        np.testing.assert_allclose(lg[:, [0, 2]], le[:, [0, 2]], rtol=1e-5, atol=0)
+        np.testing.assert_allclose(lg[:, 1], le[:, 1], rtol=2e-3, atol=1e-9)
+        assert np.abs(pg - pe).max() <= 4e-3
+    np.testing.assert_array_equal(two[0][1][True][1], two[1][1][True][1])
+
+
 def _rccl_capture_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",

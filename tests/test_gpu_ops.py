@@ -111,6 +111,33 @@ def test_fused_leaky_relu_grads_f64(hip):
     assert torch.autograd.gradgradcheck(f, (x, b))
 
 
+@pytest.mark.parametrize("slope", [0.1, 0.01])
+def test_native_leaky_relu_bit_identical_to_aten_to_third_order(hip, slope):
+    """op.fused_act.leaky_relu (FlowNet's activation on the native kernel): forward, first,
+    second and third derivatives bit-identical to F.leaky_relu under autograd, and f64
+    gradcheck / gradgradcheck.  (The mask's derivative is not materialized: a derivative whose
+    only path is through it has no graph here, where aten builds one of zeros.)"""
+    import torch.nn.functional as F
+    from op.fused_act import leaky_relu
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.randn(3, 5, 7, 9, generator=g)
+    x0[0, 0, 0, :3] = 0.0  # the x == 0 boundary takes the slope branch in both
+    w = torch.randn(3, 5, 7, 9, generator=g).to(hip)
+
+    def derivs(fn):
+        x = x0.to(hip).requires_grad_()
+        y = fn(x)
+        (d1,) = torch.autograd.grad((y * w).sum(), x, create_graph=True)
+        (d2,) = torch.autograd.grad((d1 * y * y).sum(), x, create_graph=True)
+        (d3,) = torch.autograd.grad((d2 * y).sum(), x)
+        return [t.detach() for t in (y, d1, d2, d3)]
+    for a, b in zip(derivs(lambda v: leaky_relu(v, slope)), derivs(lambda v: F.leaky_relu(v, slope))):
+        assert torch.equal(a, b)
+    x = torch.randn(2, 3, 4, 4, dtype=torch.float64, device=hip, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda v: leaky_relu(v, slope), (x,))
+    assert torch.autograd.gradgradcheck(lambda v: leaky_relu(v, slope), (x,))
+
+
 # ------------------------------------------------------------------ GroupNorm + SiLU
 @pytest.mark.parametrize("N,C,H,G", [(2, 64, 16, 16), (3, 128, 32, 32), (2, 256, 64, 32),
                                       (2, 384, 64, 32), (1, 8, 5, 2), (2, 32, 128, 8),
@@ -326,11 +353,13 @@ def test_conv3x3_winograd_backward_and_filter_cache(hip, cin):
 @pytest.mark.parametrize("N,cin,cout,h,w", [(1, 32, 64, 2, 16), (2, 64, 128, 16, 32),
                                              (3, 96, 64, 10, 48), (2, 256, 128, 32, 32),
                                              (1, 32, 128, 2, 16), (4, 128, 256, 64, 64),
-                                             (3, 64, 384, 18, 16)])
+                                             (3, 64, 384, 18, 16), (128, 256, 256, 8, 8),
+                                             (2, 32, 64, 8, 8), (16, 512, 256, 8, 8)])
 def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
     """Winograd split-K weight gradient vs a float64 direct computation (and MIOpen's fp32
     backward-weights held to the same bound): 2e-5 relative to max|ref|.  Shapes cover one
-    K-chunk, several chunks per split, odd strip counts and the NCSN++ channel widths."""
+    K-chunk, several chunks per split, odd strip counts, the NCSN++ channel widths, and the
+    pair form for 8-pixel-wide images (two images per strip: CIFAR-10's 8 x 8 level)."""
     import torch.nn.functional as F
     from op import conv as conv_mod
     from op.conv import conv3x3_wgrad_raw
@@ -1349,6 +1378,94 @@ def test_conv3x3_winograd_split_k(hip, mode, N, cin, cout, hw):
         v = out.reshape(N, cout, hw // 8, 8, hw // 16, 16).var((3, 5), unbiased=False).reshape(N, cout, R)
         assert (part[..., 0] - m).abs().max().item() <= 1e-5 * scale
         assert (part[..., 1] / cnt - v).abs().max().item() <= 1e-4 * v.abs().max().item()
+
+
+@pytest.mark.parametrize("cin,cout,hw,two", [(128, 128, 128, False), (256, 256, 64, False),
+                                             (512, 256, 32, False), (256, 128, 128, True),
+                                             (512, 256, 64, True)])
+@pytest.mark.parametrize("mode", ["pre_stats", "pre_skip_stats", "plain_bias"])
+def test_conv3x3_winograd_persistent_form_bit_identical(hip, cin, cout, hw, two, mode):
+    """The persistent 16-cin form (one workgroup per CU walking a run of regions; taken when a
+    launch has at least two items per CU) == the per-item grid bit for bit: the batch is run
+    whole (1024 items: persistent) and in four slices of 256 items (per-item grid, no split-K),
+    outputs and GroupNorm partial statistics compared exactly; and vs F.conv2d (1e-5)."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3, conv3x3_fwd_raw, gn_partials
+    rpi, cb = (hw // 8) * (hw // 16), cout // 128
+    bs = 256 // (rpi * cb)  # images per slice: 256 items
+    N = 4 * bs
+    g = torch.Generator(device=hip).manual_seed(cin + hw)
+    x = torch.randn(N, cin, hw, hw, device=hip, generator=g)
+    w = torch.randn(cout, cin, 3, 3, device=hip, generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(cout, device=hip, generator=g)
+    pre = torch.stack([torch.rand(N, cin, device=hip, generator=g) + 0.5,
+                       torch.randn(N, cin, device=hip, generator=g) * 0.1], -1).contiguous()
+    skip = torch.randn(N, cout, hw, hw, device=hip, generator=g)
+    c1 = cin // 2
+
+    def run(sl):
+        xs = x[sl].contiguous()
+        kw = dict(x2=xs[:, c1:].contiguous()) if two else {}
+        xa = xs[:, :c1].contiguous() if two else xs
+        with torch.no_grad():
+            if mode == "pre_stats":
+                y = conv3x3_fwd_raw(xa, w, b, pre=pre[sl].contiguous(), stats=True, **kw)
+            elif mode == "pre_skip_stats":
+                y = conv3x3_fwd_raw(xa, w, b, skip=skip[sl].contiguous(), div=2 ** 0.5,
+                                    pre=pre[sl].contiguous(), stats=True, **kw)
+            else:
+                y = conv3x3_fwd_raw(xa, w, b, **kw)
+        part = gn_partials(y)
+        return y, (part[0] if part is not None else None)
+    y, p = run(slice(0, N))
+    for i in range(4):
+        ys, ps = run(slice(i * bs, (i + 1) * bs))
+        assert torch.equal(y[i * bs:(i + 1) * bs], ys)
+        if p is not None:
+            assert torch.equal(p[i * bs:(i + 1) * bs], ps)
+    a = x if mode == "plain_bias" else F.silu(x * pre[..., 0, None, None] + pre[..., 1, None, None])
+    ref = F.conv2d(a, w, b, padding=1)
+    if mode == "pre_skip_stats":
+        ref = (skip + ref) / 2 ** 0.5
+    assert (y - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    del conv3x3
+
+
+@pytest.mark.parametrize("N,cin,cout,h", [(128, 256, 256, 8), (16, 256, 256, 8), (2, 512, 256, 8),
+                                          (6, 32, 128, 16)])
+@pytest.mark.parametrize("mode", ["plain", "skip", "pre", "dgrad"])
+def test_conv3x3_winograd_pair_form_8_wide(hip, mode, N, cin, cout, h):
+    """The 16-cin kernel's pair form for 8-pixel-wide images (two images per 8 x 16 region:
+    CIFAR-10's 8 x 8 level) -- plain, residual tail, GroupNorm+SiLU prologue and backward-data,
+    with and without split-K (N = 16, 2 take the split), vs F.conv2d (1e-5 of max|ref|)."""
+    import torch.nn.functional as F
+    from op.conv import conv3x3, conv3x3_fwd_raw, lib, wino_pair_supported, wino_supported
+    g = torch.Generator().manual_seed(N * 7 + cin + h)
+    x = torch.randn(N, cin, h, 8, generator=g).to(hip)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(hip)
+    b = torch.randn(cout, generator=g).to(hip)
+    assert wino_pair_supported(x, w) and not wino_supported(x, w)
+    assert not lib.bpk_conv3x3_wino_pair_supported(N + 1, cin, cout, h, 8)  # odd N: igemm
+    with torch.no_grad():
+        if mode == "plain":
+            out, ref = conv3x3_fwd_raw(x, w, b), F.conv2d(x, w, b, padding=1)
+        elif mode == "skip":
+            skip = torch.randn(N, cout, h, 8, generator=g).to(hip)
+            out = conv3x3_fwd_raw(x, w, b, skip=skip, div=2 ** 0.5)
+            ref = (skip + F.conv2d(x, w, b, padding=1)) / 2 ** 0.5
+        elif mode == "pre":
+            st = torch.stack([torch.rand(N, cin, generator=g) + 0.5,
+                              torch.randn(N, cin, generator=g) * 0.3], -1).to(hip)
+            out = conv3x3(x, w, b, pre=st)
+            ref = F.conv2d(F.silu(x * st[..., 0, None, None] + st[..., 1, None, None]), w, b,
+                           padding=1)
+        else:
+            wt = (torch.randn(cin, cout, 3, 3, generator=g) / (3 * cout ** 0.5)).to(hip)
+            gy = torch.randn(N, cin, h, 8, generator=g).to(hip)  # conv(gy, flip_t(wt)): cin -> cout
+            out = conv3x3_fwd_raw(gy, wt, ft=True)
+            ref = torch.nn.grad.conv2d_input((N, cout, h, 8), wt, gy, padding=1)
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() <= 1e-5 * scale
 
 
 @pytest.mark.parametrize("N,cin,cout,h,w", [(2, 128, 128, 8, 16), (3, 256, 256, 16, 8),

@@ -6,6 +6,9 @@
 # $1 = kernels (single-kernel passes) | steps (whole-step traffic; $2 = modes)
 TAG=${TAG:-r04}
 D=gpurun_out/pmc_$TAG
+# the kernel-argument pool at 64 MB: with the default pool rocprofv3 --pmc died with SIGSEGV
+# inside a launch at a pool boundary on the PINN and DPS steps (rounds 4-5)
+export HSA_KERNARG_POOL_SIZE=${HSA_KERNARG_POOL_SIZE:-67108864}
 mkdir -p $D; export TMPDIR=/tmp
 run() {  # script mode group counters...
   local script=$1 mode=$2 grp=$3; shift 3

@@ -6,6 +6,8 @@
 # with a larger kernel-argument pool (its SIGSEGV was inside a launch, at a pool-sized boundary).
 mkdir -p gpurun_out/r05b; export TMPDIR=/tmp
 O=gpurun_out/r05b
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q --timeout 120 --timeout-method thread -k "pair_form or split_k or winograd" > $O/pytest_pair.log 2>&1 || { tail -30 $O/pytest_pair.log; exit 1; }
+tail -2 $O/pytest_pair.log
 run() {  # name, env..., -- args
   local name=$1; shift
   env "$@" timeout -k 10 240 python -u tools/audit_pinn_graph.py $ARGS > $O/$name.log 2>&1 || { tail -5 $O/$name.log; exit 1; }

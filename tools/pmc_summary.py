@@ -47,7 +47,7 @@ def step_bytes(mode, counter):
         if r["Counter_Name"] == counter:
             d["v"] += float(r["Counter_Value"])
     ids = list(per)
-    marks = [i for i, d in enumerate(per.values()) if "fused_bias_act" in d["name"]]
+    marks = [i for i, d in enumerate(per.values()) if "fused_bias_act_kernel<double>" in d["name"]]
     assert len(marks) >= 2, (mode, counter, len(marks))
     a, b = marks[-2], marks[-1]
     inside = [per[ids[i]]["v"] for i in range(a + 1, b)]

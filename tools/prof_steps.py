@@ -1,10 +1,13 @@
 """rocprofv3 --pmc driver for the whole-step rooflines' HBM traffic: runs one bench phase
 (MODE = train | cifar | pinn | dps) through bench.main with one timed step, and brackets the
 phase's single counted step (bench.counted: after the warm-up, outside the timed loop) with a
-marker dispatch of fused_bias_act_kernel on 256 floats (a kernel no bench phase launches).
+marker dispatch of fused_bias_act_kernel<double> on 256 values (an instance no bench phase
+launches: FlowNet's LeakyReLU runs the float one).
 tools/pmc_summary.py sums FETCH_SIZE / WRITE_SIZE over the dispatches between the markers.
-The PINN phase runs its eager step (--pinn-eager): the counted step is eager in either mode,
-and the hipGraph capture of the timed step segfaulted under rocprofv3 --pmc (round 4)."""
+The PINN phase runs its eager step (--pinn-eager): the counted step is eager in either mode.
+Run the passes with HSA_KERNARG_POOL_SIZE=67108864: round 4's PINN / DPS passes died with
+SIGSEGV inside a kernel launch at a kernel-argument-pool boundary (rocprofv3 copying a launch's
+arguments; the 64 MB pool moved past it in round 5)."""
 import os
 import sys
 
@@ -20,7 +23,7 @@ _orig = bench.counted
 
 def _marker(dev):
     from op.fused_act import fused_bias_act_raw
-    t = torch.zeros(256, device=dev)
+    t = torch.zeros(256, device=dev, dtype=torch.float64)  # the f64 instance: no phase runs it
     fused_bias_act_raw(t, None, None, 1, 0, 0.2, 1.0)
     torch.cuda.synchronize(dev)
 
@@ -34,6 +37,17 @@ def counted(fn, dev):
 
 
 bench.counted = counted
+if MODE == "dps":
+    # the counted NFE is all the PMC pass needs: the warm-up and the timed RK45 solves become
+    # one function evaluation each (every dispatch is serialized under --pmc: the real solves
+    # took minutes)
+    import inverse.conditional_sampling as _cs
+
+    def _one_eval(config, ode_func, x0, t1, shape, eps, ctx=None):
+        _cs.get_solver.last_nfe = 1
+        return ode_func(t1, x0).reshape(shape).to(torch.float32)
+    _one_eval.last_nfe = 1
+    _cs.get_solver = _one_eval
 common = ["--steps", "1", "--warmup", "1", "--no-roofline", "--no-cpu-baseline", "--ns-steps", "0",
           "--ncddpmpp-steps", "0"]
 argv = {"train": ["--train-steps", "1", "--cifar-steps", "0", "--no-pinn", "--no-dps"],
