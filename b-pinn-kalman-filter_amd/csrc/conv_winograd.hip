@@ -1119,399 +1119,6 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   WINO_TS(5);
 }
 
-// Persistent form of the 16-cin kernel (one workgroup per CU walking a contiguous run of
-// regions for one 128-cout block).  Per item the non-persistent kernel spends ~19 % of a
-// 128-input-channel item outside its chunk loop: the first patch loads landing (2.5 us), the
-// staging of two patches and the first transform, and ~1 us until the next workgroup starts
-// (round-4 timeline).  Here the chunk pipeline runs across item boundaries: chunk K of the
-// workgroup's stream (item K / nch, input-channel chunk K % nch) is loaded at step K - 3, staged
-// (GroupNorm affine + SiLU, halo mask) at K - 2 and transformed at K - 1 whichever item those
-// steps belong to, so the next item's first chunks are ready when the current item's last MFMAs
-// end; only the epilogue separates two items.  The patch loads go straight into LDS (buffer_load
-// ... lds, 32 KB of raw patches in thread order: no registers -- the register form of the
-// pipeline left no room for the persistent loop), and so do the per-item GroupNorm tables
-// (double-buffered, 2 x 8 KB); both are read back with inline-asm LDS reads behind explicit
-// vmcnt waits (a compiler-visible read of a DMA target waits for every outstanding load).  The B
-// operands wrap around: the last chunk prefetches chunk 0's U for the next item (same couts).
-// Every item runs the non-persistent kernel's arithmetic in the same order: results are
-// bit-identical.  LDS: 30 + 80 KB (patches, V) + 32 KB (raw) + 16 KB (tables) = 158 KB.
-// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only: vmcnt[3:0] in bits 3:0,
-// vmcnt[5:4] in bits 15:14, expcnt 7 and lgkmcnt 15 (= no wait) in bits 6:4 and 11:8
-constexpr int kVmcntOnly(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
-
-template <bool PRE>
-__global__ __launch_bounds__(512, 1) void wino_f23_k16p_kernel(
-    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
-    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2) {
-  constexpr int CK = 16;
-  constexpr int kPatch = CK * kPR * kPCp;
-  constexpr int kTab = PRE ? 2 * kPreMaxCin : 1;  // (s, t) per channel, flat
-  __shared__ __attribute__((aligned(16))) float s_patch_raw[2][kPatch];
-  constexpr int kVBuf = CK * kM * kVS;
-  __shared__ __attribute__((aligned(16))) float s_v[2][kVBuf];
-  __shared__ __attribute__((aligned(16))) float s_tab[2][kTab];       // DMA target
-  __shared__ __attribute__((aligned(16))) float s_raw[2][CK][256];    // DMA target
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const unsigned nblk = gridDim.x;
-  unsigned L = blockIdx.x;
-  if (xcd_remap) L = (L & 7u) * (nblk >> 3) + (L >> 3);
-  unsigned cb;
-  const unsigned grp_id = udivmod(L, (unsigned)g.cout_blocks, cb);
-  const unsigned ngrp = nblk / (unsigned)g.cout_blocks;
-  const unsigned rpi = (unsigned)(g.regions_x * g.regions_y);  // regions per image
-  const unsigned total = (unsigned)g.N * rpi;
-  const unsigned f_begin = (unsigned)(((unsigned long long)total * grp_id) / ngrp);
-  const int nitems = (int)((((unsigned long long)total * (grp_id + 1)) / ngrp) - f_begin);
-  const int cout_w = (int)cb * 128 + wave * 16;
-  const int ph = __builtin_amdgcn_readfirstlane(tid >> 8);  // channels 8 ph .. 8 ph + 7
-  const int64_t plane = (int64_t)g.H * g.W;
-  const int C2 = g.Cin - g.C1;
-  const int kq = lane >> 4, jj = lane & 15;
-  const int nch = g.Cin / CK;                       // even, >= 4 (host)
-  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(U), 0, (int)((int64_t)g.Cin * g.Cout * 64), 0x00020000);
-  // whole-tensor descriptors (host: every byte offset < 2^31); the image and channel offsets go
-  // into soffset, so no per-item descriptor is built (a descriptor computed in the loop ended
-  // up in VGPRs, and every load in a readfirstlane loop)
-  const unsigned long long xa = reinterpret_cast<unsigned long long>(x);
-  const unsigned long long x2a = reinterpret_cast<unsigned long long>(C2 > 0 ? x2 : x);
-  const int xbytes = (int)((int64_t)g.N * g.C1 * plane * 4);
-  const int x2bytes = (int)((int64_t)g.N * (C2 > 0 ? C2 : g.C1) * plane * 4);
-  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float2*>(PRE ? pre : nullptr), 0, PRE ? 8 * g.N * g.Cin : 0, 0x00020000);
-
-  // the thread's patch position (fixed for every item)
-  const int t8 = tid & 255;
-  const int tpos = t8 < kPR * kPC ? t8 : 0;
-  const int tpy = tpos / kPC, tpx = tpos - tpy * kPC;
-  const int pdst = tpy * kPCp + tpx + ph * 8 * (kPR * kPCp);
-  // an item = (image, region) -> (n, oy0, ox0), as three scalars (a struct selected between two
-  // items went to scratch memory)
-  auto item_at = [&](int i, int& n, int& oy0, int& ox0) {
-    unsigned rr, rx;
-    const unsigned nn = udivmod(f_begin + (unsigned)i, rpi, rr);
-    const unsigned ry = udivmod(rr, (unsigned)g.regions_x, rx);
-    n = __builtin_amdgcn_readfirstlane((int)nn);
-    oy0 = __builtin_amdgcn_readfirstlane((int)ry * kOutRows);
-    ox0 = __builtin_amdgcn_readfirstlane((int)rx * kOutCols);
-  };
-  auto pos_of = [&](int oy0, int ox0, bool& in) {  // byte offset of the (clamped) position
-    const int iy = oy0 - 1 + tpy, ix = ox0 - 1 + tpx;
-    in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-    const int cy = min(max(iy, 0), g.H - 1), cx = min(max(ix, 0), g.W - 1);
-    return (cy * g.W + cx) * 4;
-  };
-  using lds_ptr = __attribute__((address_space(3))) void*;
-  auto lds_addr = [](const float* p) {
-    return (unsigned)(size_t)(__attribute__((address_space(3))) const float*)p;
-  };
-  // the items whose chunks the current step stages / loads: `cur` (chunk kk < nch) or `nxt`
-  // (chunk kk - nch), kept in scalars per item
-  int cur_n = 0, cur_oy = 0, cur_ox = 0, nxt_n = 0, nxt_oy = 0, nxt_ox = 0;
-  bool has_next = false;
-  // chunk kk of the current item (kk >= nch: of the next) -> raw channels ph * 8 + c0 .. + 3
-  // into s_raw[buf], slot t8
-  auto dma_patch = [&](int kk, int buf, int c0) {
-    if (kk >= nch && !has_next) return;
-    const bool nx = kk >= nch;
-    const int itn = nx ? nxt_n : cur_n;
-    const int k = nx ? kk - nch : kk;
-    bool in;
-    const int poff = pos_of(nx ? nxt_oy : cur_oy, nx ? nxt_ox : cur_ox, in);
-    const int cc = k * CK;
-    const bool second = cc >= g.C1;
-    const int soff = (second ? itn * C2 + cc - g.C1 : itn * g.C1 + cc) * (int)plane * 4 +
-                     ph * 8 * (int)plane * 4;
-    // the descriptor is built here from a scalar select of the base address (a select of two
-    // whole descriptors went through scratch memory)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(second ? x2a : xa), 0, second ? x2bytes : xbytes, 0x00020000);
-#pragma unroll
-    for (int c = c0; c < c0 + 4; ++c)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (lds_ptr)&s_raw[buf][ph * 8 + c][64 * (wave & 3)], 4, poff,
-          soff + c * (int)plane * 4, 0, 0);
-  };
-  // the GroupNorm table of item `it` (index i) into s_tab[i & 1] (flat floats, 2 Cin of them)
-  auto dma_table = [&](int itn, int tb) {
-    if (!PRE) return;
-#pragma unroll
-    for (int r = 0; r < kTab / 512; ++r)
-      if (512 * r < 2 * g.Cin)  // wave-uniform; entries past 2 Cin land past the table: unread
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            prs, (lds_ptr)&s_tab[tb][512 * r + 64 * wave], 4, (512 * r + tid) * 4,
-            itn * g.Cin * 8, 0, 0);
-  };
-  // stage channels ph * 8 + c0 .. + 3 of chunk kk (as dma_patch) from s_raw[buf]: affine +
-  // SiLU, halo mask -> s_patch_raw[buf].  The caller has waited (vmcnt) for the chunk's loads;
-  // each thread reads the slots its own loads wrote, the table after a barrier behind its loads'
-  // completion.  tb = the table buffer of the chunk's item.
-  auto stage = [&](int kk, int buf, int tb, int c0) {
-    if (kk >= nch && !has_next) return;
-    const bool nx = kk >= nch;
-    const int k = nx ? kk - nch : kk;
-    bool pin;
-    (void)pos_of(nx ? nxt_oy : cur_oy, nx ? nxt_ox : cur_ox, pin);
-    float v[4];
-    const unsigned ra = lds_addr(&s_raw[buf][ph * 8 + c0][t8]);
-    asm volatile(
-        "ds_read_b32 %0, %4\n\t"
-        "ds_read_b32 %1, %4 offset:1024\n\t"
-        "ds_read_b32 %2, %4 offset:2048\n\t"
-        "ds_read_b32 %3, %4 offset:3072\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3])
-        : "v"(ra)
-        : "memory");
-    if (PRE) {
-      float2 st[4];
-      const unsigned ta = lds_addr(&s_tab[tb][2 * (k * CK + ph * 8 + c0)]);
-      asm volatile(
-          "ds_read_b64 %0, %4\n\t"
-          "ds_read_b64 %1, %4 offset:8\n\t"
-          "ds_read_b64 %2, %4 offset:16\n\t"
-          "ds_read_b64 %3, %4 offset:24\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=v"(st[0]), "=v"(st[1]), "=v"(st[2]), "=v"(st[3])
-          : "v"(ta)
-          : "memory");
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] = silu_f(v[c] * st[c].x + st[c].y);
-    }
-    float* sp = &s_patch_raw[buf][pdst + c0 * (kPR * kPCp)];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) sp[c * (kPR * kPCp)] = pin ? v[c] : 0.f;
-  };
-
-  f4 acc[16][2];
-  f4 uo[2][4];
-  const int uoff = ((kq * g.Cout + cout_w + jj) * 16) * 4;
-  auto u_soff = [&](int k, int ks) { return ((((k == nch) ? 0 : k) * CK + 4 * ks) * g.Cout) * 64; };
-  auto load_u = [&](int slot, int k, int ks) {
-    const int soff = u_soff(k, ks);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      using u4 = __attribute__((ext_vector_type(4))) unsigned;
-      const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff, 0);
-      uo[slot][q] = __builtin_bit_cast(f4, w);
-    }
-  };
-  const int tc = tid >> 5, tm = tid & 31;
-  const int tty = tm / kTC, ttx = tm - tty * kTC;
-  float d[4][4];
-  auto read_d = [&](const float* sp) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; j += 2) {
-        const float2 v2 =
-            *reinterpret_cast<const float2*>(&sp[(tc * kPR + 2 * tty + i) * kPCp + 2 * ttx + j]);
-        d[i][j] = v2.x;
-        d[i][j + 1] = v2.y;
-      }
-  };
-  auto write_v = [&](float* sv) {
-    float t[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      t[0][j] = d[0][j] - d[2][j];
-      t[1][j] = d[1][j] + d[2][j];
-      t[2][j] = d[2][j] - d[1][j];
-      t[3][j] = d[1][j] - d[3][j];
-    }
-    f4* dst = reinterpret_cast<f4*>(&sv[(tc * kM + tm) * kVS]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dst[i] = f4{t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1], t[i][1] - t[i][3]};
-  };
-  f4 a[4];
-  auto a_src = [&](const float* sv, int grp) {  // grp = 2 ks + mb
-    const int ks = grp >> 1, mb = grp & 1;
-    return reinterpret_cast<const f4*>(&sv[((4 * ks + kq) * kM + mb * 16 + jj) * kVS]);
-  };
-
-  if (nitems <= 0) return;
-  // ---- stream prologue: table(0), chunks 0 / 1 staged, chunk 2 in flight, V(0), U(0)
-  item_at(0, cur_n, cur_oy, cur_ox);
-  dma_table(cur_n, 0);
-  dma_patch(0, 0, 0);
-  dma_patch(0, 0, 4);
-  dma_patch(1, 1, 0);
-  dma_patch(1, 1, 4);
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  stage(0, 0, 0, 0);
-  stage(0, 0, 0, 4);
-  stage(1, 1, 0, 0);
-  stage(1, 1, 0, 4);
-  dma_patch(2, 0, 0);
-  dma_patch(2, 0, 4);
-  load_u(0, 0, 0);
-  load_u(1, 0, 1);
-  __syncthreads();
-  read_d(s_patch_raw[0]);
-  write_v(s_v[0]);
-  __syncthreads();
-  {
-    const f4* src = a_src(s_v[0], 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a[q] = src[q];
-  }
-
-  // step k of item i (stream chunk K = i nch + k; SB = K & 1 = k & 1, nch even); chunk k + 2
-  // (staged) and k + 3 (loaded) may be the next item's; tabs = the table buffers (cur, nxt)
-  // LAST (the item's last chunk): the next item's A operands are read after the epilogue (they
-  // would be live through it)
-  auto step = [&](int k, int tcur, auto sb_c, auto first_c,
-                  auto last_c) __attribute__((always_inline)) {
-    constexpr int SB = decltype(sb_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value;
-    constexpr bool LAST = decltype(last_c)::value;
-    const float* sv = s_v[SB];
-#pragma unroll
-    for (int grp = 0; grp < 8; ++grp) {
-      const int ks = grp >> 1, mb = grp & 1;
-      __builtin_amdgcn_sched_barrier(0);
-      if (grp == 0) read_d(s_patch_raw[SB ^ 1]);  // patch(K+1)
-      if (grp == 1) write_v(s_v[SB ^ 1]);         // V(K+1)
-      if (grp == 2) {  // stage(k+2): its loads (step k-1) are older than the 16 newest
-        __builtin_amdgcn_s_waitcnt(kVmcntOnly(16));  // expcnt / lgkmcnt not waited
-        stage(k + 2, SB, k + 2 >= nch ? tcur ^ 1 : tcur, 0);
-      }
-      if (grp == 3) {
-        __builtin_amdgcn_s_waitcnt(kVmcntOnly(12));
-        stage(k + 2, SB, k + 2 >= nch ? tcur ^ 1 : tcur, 4);
-      }
-      if (grp == 4) dma_patch(k + 3, SB ^ 1, 0);
-      if (grp == 5) dma_patch(k + 3, SB ^ 1, 4);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp)
-          acc[4 * q + pp][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[q][pp], uo[ks & 1][q][pp],
-              (FIRST && ks == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[4 * q + pp][mb], 0, 0, 0);
-        if (grp < 7) a[q] = a_src(sv, grp + 1)[q];
-        if (mb == 1) {  // k-step ks + 2 of this chunk, or ks - 2 of the next (the next item's
-                        // chunk 0 after the last)
-          const int soff = ks < 2 ? u_soff(k, ks + 2) : u_soff(k + 1, ks - 2);
-          using u4 = __attribute__((ext_vector_type(4))) unsigned;
-          const u4 w = __builtin_amdgcn_raw_buffer_load_b128(urs, uoff + q * 16, soff, 0);
-          uo[ks & 1][q] = __builtin_bit_cast(f4, w);
-        }
-      }
-    }
-    __syncthreads();
-    if (!LAST) {
-      const f4* src = a_src(s_v[SB ^ 1], 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = src[q];
-    }
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  const float rdiv = 1.f / g.div;
-  for (int i = 0; i < nitems; ++i) {
-    has_next = i + 1 < nitems;
-    if (has_next) {
-      item_at(i + 1, nxt_n, nxt_oy, nxt_ox);
-      // s_tab[(i + 1) & 1]: item i - 1's table, last read during its chunk nch - 3
-      dma_table(nxt_n, (i + 1) & 1);
-    }
-    const int tcur = i & 1;
-    using T = std::true_type;
-    using F = std::false_type;
-    step(0, tcur, C0{}, T{}, F{});
-    for (int k = 1; k + 1 < nch; k += 2) {
-      step(k, tcur, C1{}, F{}, F{});
-      step(k + 1, tcur, C0{}, F{}, F{});
-    }
-    step(nch - 1, tcur, C1{}, F{}, T{});
-
-    // ---- epilogue of item i (the non-persistent kernel's)
-    if (cout_w < g.CoutS) {
-      const int n = cur_n, oy0 = cur_oy, ox0 = cur_ox;
-      const int co = cout_w + jj;
-      const float bv = bias ? bias[co] : 0.f;
-      const int oxl = ox0 + 8 * (kq & 1);
-      const int64_t obase = ((int64_t)n * g.CoutS + co) * plane;
-      float lm = 0.f, lm2 = 0.f;
-      f4 skv[2][2][2];
-      if (skip) {
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-              skv[mb][h][e] = *reinterpret_cast<const f4*>(
-                  &skip[obase + (int64_t)(oy0 + 2 * (2 * mb + (kq >> 1)) + h) * g.W + oxl + 4 * e]);
-      }
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb) {
-        const int oy = oy0 + 2 * (2 * mb + (kq >> 1));
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            f4 v;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const int rg = 2 * e + u;
-              float t[4];
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                t[j] = h == 0 ? acc[j][mb][rg] + acc[4 + j][mb][rg] + acc[8 + j][mb][rg]
-                              : acc[4 + j][mb][rg] - acc[8 + j][mb][rg] - acc[12 + j][mb][rg];
-              v[2 * u] = t[0] + t[1] + t[2] + bv;
-              v[2 * u + 1] = t[1] - t[2] - t[3] + bv;
-            }
-            const int64_t o = obase + (int64_t)(oy + h) * g.W + oxl + 4 * e;
-            if (skip) {
-              const f4 sk = skv[mb][h][e];
-#pragma unroll
-              for (int c = 0; c < 4; ++c) v[c] = div_rn(sk[c] + v[c], g.div, rdiv);
-            }
-            *reinterpret_cast<f4*>(&y[o]) = v;
-            if (stats) {
-              const float sm = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
-              float sm2 = 0.f;
-#pragma unroll
-              for (int c = 0; c < 4; ++c) sm2 = fmaf(v[c] - sm, v[c] - sm, sm2);
-              constexpr float kW[8] = {1.f, 1.f / 2, 1.f / 3, 1.f / 4, 1.f / 5, 1.f / 6, 1.f / 7, 1.f / 8};
-              const int st = 4 * mb + 2 * h + e;
-              const float dd = sm - lm;
-              lm = lm + dd * kW[st];
-              lm2 = (lm2 + sm2) + dd * dd * (4.f * st * kW[st]);
-            }
-          }
-        }
-      }
-      if (stats) {
-        merge_stats(lm, lm2, __shfl_xor(lm, 16, 64), __shfl_xor(lm2, 16, 64), 32.f);
-        merge_stats(lm, lm2, __shfl_xor(lm, 32, 64), __shfl_xor(lm2, 32, 64), 64.f);
-        if (kq == 0) {
-          const int region = (oy0 / kOutRows) * g.regions_x + ox0 / kOutCols;
-          stats[((int64_t)n * g.CoutS + co) * (int)rpi + region] = make_float2(lm, lm2);
-        }
-      }
-    }
-    cur_n = nxt_n;
-    cur_oy = nxt_oy;
-    cur_ox = nxt_ox;
-    {  // the next item's chunk-0 A operands (V(0) in s_v[0], written during the last chunk)
-      const f4* src = a_src(s_v[0], 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = src[q];
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // no LDS DMA in flight at exit
-}
-
 // Split-K epilogue: y = sum_s part[s] + bias, or (skip + that) / div, and the GroupNorm partial
 // statistics of the stored values, as the 16-cin kernel's own epilogue (the partial slabs are
 // summed in a fixed order: deterministic).  One workgroup = 8 channels x one 8 x 16 region of
@@ -1565,25 +1172,6 @@ __global__ __launch_bounds__(256) void wino_splitk_reduce_kernel(
 }  // namespace
 
 static int cout_padded(int Cout) { return (Cout + 63) / 64 * 64; }
-
-static int wino_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
-
-// A/B of the persistent 16-cin form during round 5 (BPK_WINO_PERSIST=0: the per-item grid)
-static bool wino_persist() {
-  static const bool on = [] {
-    const char* e = std::getenv("BPK_WINO_PERSIST");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 
 extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
   return (int64_t)16 * Cin * cout_padded(Cout) * (int64_t)sizeof(float);
@@ -1671,8 +1259,8 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
               "Cout %% 16, H %% 8, W %% 16 == 0)", N, Cin, Cout, H, W);
   const int CoutP = cout_padded(Cout);
   // Kernel choice (each form measured against the others on the NCSN++ / DDPM++ shapes;
-  // the rejected variants -- a persistent form, 128-cout NB = 2 blocks, the 4-wave residual
-  // tail -- are gone, numbers in DESIGN.md section 4):
+  // the rejected variants -- two persistent forms (register- and LDS-DMA-staged), 128-cout
+  // NB = 2 blocks, the 4-wave residual tail -- are gone, numbers in DESIGN.md section 4):
   //   * wino_f23_k16_kernel: CoutP % 128 == 0 and 16-cin chunks (every NCSN++ conv);
   //   * wino_f23_pipe_kernel: the other shapes (8-wave / 128-cout form for the GroupNorm
   //     prologue convs without a residual tail, 4 waves / 64 couts otherwise);
@@ -1696,21 +1284,6 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
       BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino: grid too large");
       const float2* kpre = reinterpret_cast<const float2*>(pre);
       hipStream_t kst = bpk::as_stream(stream);
-      // persistent form: one workgroup per CU, at least two items each, 4+ chunks per item
-      const int cus = wino_cus();
-      if (wino_persist() && Cin / 16 >= 4 && (Cin / 16) % 2 == 0 && C1 % 16 == 0 &&
-          cus % 8 == 0 && cus % gk.cout_blocks == 0 && items >= 2LL * cus &&
-          (int64_t)N * std::max(C1, Cin - C1) * H * W * 4 < (1LL << 31) &&
-          (!pre || Cin <= kPreMaxCin)) {
-        if (pre)
-          hipLaunchKernelGGL((wino_f23_k16p_kernel<true>), dim3((unsigned)cus), dim3(512), 0, kst,
-                             x, U, bias, skip, kpre, y, stats2, gk, 1, x2);
-        else
-          hipLaunchKernelGGL((wino_f23_k16p_kernel<false>), dim3((unsigned)cus), dim3(512), 0,
-                             kst, x, U, bias, skip, kpre, y, stats2, gk, 1, x2);
-        BPK_LAUNCH_CHECK("conv3x3_wino_k16p");
-        return BPK_OK;
-      }
       const int64_t kblocks = items;
       const int kremap = (kblocks % 8 == 0) ? 1 : 0;
       if (pre)

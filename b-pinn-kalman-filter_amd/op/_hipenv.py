@@ -18,6 +18,9 @@ is bit-stable with this variable at 0 (the packets are rebuilt per replay,
 the PINN replay time unchanged: 84.4 vs 84.0 ms) or with a 64 MB pool (HSA_KERNARG_POOL_SIZE:
 only delays the wrap).  The audit of every pointer the captured step reads found no aliasing:
 all of them lie in the graph's private pool or in live tensors (profiles/r05_pinn_graph_audit.json).
+The PC sampler's step graph (B = 8, 24 steps, the same large-argument launches between steps)
+stayed bit-identical to the run without them with the setting at 1 and at 0 (round 5) -- not
+shown vulnerable, covered by the setting all the same.
 """
 from __future__ import annotations
 

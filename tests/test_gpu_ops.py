@@ -1380,57 +1380,6 @@ def test_conv3x3_winograd_split_k(hip, mode, N, cin, cout, hw):
         assert (part[..., 1] / cnt - v).abs().max().item() <= 1e-4 * v.abs().max().item()
 
 
-@pytest.mark.parametrize("cin,cout,hw,two", [(128, 128, 128, False), (256, 256, 64, False),
-                                             (512, 256, 32, False), (256, 128, 128, True),
-                                             (512, 256, 64, True)])
-@pytest.mark.parametrize("mode", ["pre_stats", "pre_skip_stats", "plain_bias"])
-def test_conv3x3_winograd_persistent_form_bit_identical(hip, cin, cout, hw, two, mode):
-    """The persistent 16-cin form (one workgroup per CU walking a run of regions; taken when a
-    launch has at least two items per CU) == the per-item grid bit for bit: the batch is run
-    whole (1024 items: persistent) and in four slices of 256 items (per-item grid, no split-K),
-    outputs and GroupNorm partial statistics compared exactly; and vs F.conv2d (1e-5)."""
-    import torch.nn.functional as F
-    from op.conv import conv3x3, conv3x3_fwd_raw, gn_partials
-    rpi, cb = (hw // 8) * (hw // 16), cout // 128
-    bs = 256 // (rpi * cb)  # images per slice: 256 items
-    N = 4 * bs
-    g = torch.Generator(device=hip).manual_seed(cin + hw)
-    x = torch.randn(N, cin, hw, hw, device=hip, generator=g)
-    w = torch.randn(cout, cin, 3, 3, device=hip, generator=g) / (3 * cin ** 0.5)
-    b = torch.randn(cout, device=hip, generator=g)
-    pre = torch.stack([torch.rand(N, cin, device=hip, generator=g) + 0.5,
-                       torch.randn(N, cin, device=hip, generator=g) * 0.1], -1).contiguous()
-    skip = torch.randn(N, cout, hw, hw, device=hip, generator=g)
-    c1 = cin // 2
-
-    def run(sl):
-        xs = x[sl].contiguous()
-        kw = dict(x2=xs[:, c1:].contiguous()) if two else {}
-        xa = xs[:, :c1].contiguous() if two else xs
-        with torch.no_grad():
-            if mode == "pre_stats":
-                y = conv3x3_fwd_raw(xa, w, b, pre=pre[sl].contiguous(), stats=True, **kw)
-            elif mode == "pre_skip_stats":
-                y = conv3x3_fwd_raw(xa, w, b, skip=skip[sl].contiguous(), div=2 ** 0.5,
-                                    pre=pre[sl].contiguous(), stats=True, **kw)
-            else:
-                y = conv3x3_fwd_raw(xa, w, b, **kw)
-        part = gn_partials(y)
-        return y, (part[0] if part is not None else None)
-    y, p = run(slice(0, N))
-    for i in range(4):
-        ys, ps = run(slice(i * bs, (i + 1) * bs))
-        assert torch.equal(y[i * bs:(i + 1) * bs], ys)
-        if p is not None:
-            assert torch.equal(p[i * bs:(i + 1) * bs], ps)
-    a = x if mode == "plain_bias" else F.silu(x * pre[..., 0, None, None] + pre[..., 1, None, None])
-    ref = F.conv2d(a, w, b, padding=1)
-    if mode == "pre_skip_stats":
-        ref = (skip + ref) / 2 ** 0.5
-    assert (y - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-    del conv3x3
-
-
 @pytest.mark.parametrize("N,cin,cout,h", [(128, 256, 256, 8), (16, 256, 256, 8), (2, 512, 256, 8),
                                           (6, 32, 128, 16)])
 @pytest.mark.parametrize("mode", ["plain", "skip", "pre", "dgrad"])
