@@ -596,14 +596,14 @@ int64_t ws_bytes(const IgGeo& g) {
 void choose_tiling(IgGeo& g, int mode) {
   g.nchunk = (g.K + BK - 1) / BK;
   const int64_t cus = num_cus();
-  // 16 x 256 tiles for M <= 16 (a forward / backward-data conv into 1-16 channels: no
-  // 64-row tile mostly idle; the weight gradient's columns are gathers, kept at 64); 128 x 128 (4x the MFMA work per staged chunk) when M, N are large;
-  // else 64 x 64
+  // 16 x 256 tiles for M <= 16 (a conv into 1-16 channels, or the weight gradient of one:
+  // no 64-row tile three-quarters idle -- the PINN's 16-channel weight gradients over 64^2 x 64
+  // pixels); 128 x 128 (4x the MFMA work per staged chunk) when M, N are large; else 64 x 64
   // the weight gradient decides on its filter columns alone (the bias column would change
   // the split count, and with it the summation order: dw must not depend on bias_grad)
   const int ncol = mode == 2 ? g.wcols : g.Ncol;
   int tm, tn;
-  if (g.M <= 16 && mode != 2) {
+  if (g.M <= 16) {
     g.tile = 2; tm = 16; tn = 256;
   } else if (g.M >= 128 && (int64_t)g.M * ncol >= 128ll * 128 * cus / 2) {
     g.tile = 1; tm = tn = 128;

@@ -67,10 +67,13 @@ constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records
 // rows of images 2p (tiles 0-3) and 2p + 1 (tiles 4-7); each image's halo columns are padding
 // (always zero), so a patch row is [0 | A x0..7 | 0 0 | B x0..7 | 0] and the gradient tiles of
 // k-step ks come from image 2p + ks.  Strip cursor: n = pair, strips_x = 1.
-template <int NB, bool PAIR = false>
+// PRE: the convolved input is silu(x * s + t) with pre[n][cin] = (s, t) -- the GroupNorm+SiLU
+// the forward conv applied in its input load (op.conv.gn_silu_conv3x3_ad) -- applied here in
+// the patch store with the forward prologue's arithmetic; the zero padding stays zero.
+template <int NB, bool PAIR = false, bool PRE = false>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ part,
-    float* __restrict__ part_b, WgradGeo g, int xcd_remap) {
+    float* __restrict__ part_b, WgradGeo g, int xcd_remap, const float2* __restrict__ pre) {
   __shared__ __attribute__((aligned(16))) float s_x[2][kCB * kXCS];   // 2 x 14.3 KB
   __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 20.6 KB
 
@@ -148,13 +151,16 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   const int xp = tid >> 1, xh = tid & 1;
   const int xc = xp >> 2, xpy = xp & 3;
   float xv[9];
+  float2 xst = make_float2(1.f, 0.f);  // PRE: the patch channel's (s, t)
   bool xrow_ok, xhalo_ok;
   Strip xcur = strip_at(0);
   auto load_x = [&]() {  // patch of chunk xcur, then advance
     const Strip s = xcur;
     advance(xcur);
     const int oy0 = 2 * s.sy, ox0 = PAIR ? -8 * xh : 16 * s.sx;  // PAIR: half xh = image 2n + xh
-    const float* base = x + ((int64_t)(PAIR ? 2 * s.n + xh : s.n) * g.Cin + cin0) * plane;
+    const int img = PAIR ? 2 * s.n + xh : s.n;
+    const float* base = x + ((int64_t)img * g.Cin + cin0) * plane;
+    if (PRE) xst = pre[(int64_t)img * g.Cin + cin0 + xc];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(base), 0, kCB * plane * 4, 0x00020000);
     const int iy = oy0 - 1 + xpy;
@@ -178,6 +184,13 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   auto store_x = [&](float* sx) {
     float* row = sx + xc * kXCS + xpy * kXRS;
     const float z = xrow_ok ? 1.f : 0.f;
+    if (PRE) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) {
+        const float u = xv[e] * xst.x + xst.y;
+        xv[e] = u * __builtin_amdgcn_rcpf(1.f + __expf(-u));
+      }
+    }
     if (PAIR) {  // image xh's 8 pixels at columns 4 + 10 xh (8-byte aligned for xh = 1)
       float2* r2 = reinterpret_cast<float2*>(row + 4 + 10 * xh);
 #pragma unroll
@@ -254,31 +267,33 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     }
   }
   float xv0[9], xv1[9];
+  float2 st0, st1;
   bool ok0r, ok0h, ok1r, ok1h;
   load_x();
 #pragma unroll
   for (int e = 0; e < 9; ++e) xv0[e] = xv[e];
-  ok0r = xrow_ok; ok0h = xhalo_ok;
+  ok0r = xrow_ok; ok0h = xhalo_ok; st0 = xst;
   load_x();
 #pragma unroll
   for (int e = 0; e < 9; ++e) xv1[e] = xv[e];
-  ok1r = xrow_ok; ok1h = xhalo_ok;
+  ok1r = xrow_ok; ok1h = xhalo_ok; st1 = xst;
   load_x();
   load_g(gq);
   {
     float keep[9];
     bool kr = xrow_ok, kh = xhalo_ok;
+    const float2 kst = xst;
 #pragma unroll
     for (int e = 0; e < 9; ++e) { keep[e] = xv[e]; xv[e] = xv0[e]; }
-    xrow_ok = ok0r; xhalo_ok = ok0h;
+    xrow_ok = ok0r; xhalo_ok = ok0h; xst = st0;
     store_x(s_x[0]);
 #pragma unroll
     for (int e = 0; e < 9; ++e) xv[e] = xv1[e];
-    xrow_ok = ok1r; xhalo_ok = ok1h;
+    xrow_ok = ok1r; xhalo_ok = ok1h; xst = st1;
     store_x(s_x[1]);
 #pragma unroll
     for (int e = 0; e < 9; ++e) xv[e] = keep[e];
-    xrow_ok = kr; xhalo_ok = kh;
+    xrow_ok = kr; xhalo_ok = kh; xst = kst;
   }
   __syncthreads();
   read_d(s_x[0]);
@@ -456,6 +471,13 @@ extern "C" int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float
 extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, float* dw,
                                                float* db, float* workspace, int N, int Cin,
                                                int Cout, int H, int W, void* stream) {
+  return bpk_conv3x3_wino_wgrad_pre_f32(x, nullptr, gy, dw, db, workspace, N, Cin, Cout, H, W,
+                                        stream);
+}
+
+extern "C" int bpk_conv3x3_wino_wgrad_pre_f32(const float* x, const float* pre, const float* gy,
+                                              float* dw, float* db, float* workspace, int N,
+                                              int Cin, int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_wgrad_supported(N, Cin, Cout, H, W),
               "conv3x3_wino_wgrad: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin "
               "%% 32, Cout %% 64, H %% 2, W %% 16 == 0 or W == 8 with N even)", N, Cin, Cout,
@@ -467,12 +489,16 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
   float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
-  if (wgrad_pair(N, W))
-    hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, true>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, x, gy, workspace, part_b, g, remap);
-  else
-    hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, false>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, x, gy, workspace, part_b, g, remap);
+  const float2* kp = reinterpret_cast<const float2*>(pre);
+#define BPK_WG(PAIR_, PRE_)                                                                      \
+  hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, PAIR_, PRE_>), dim3((unsigned)blocks),        \
+                     dim3(256), 0, st, x, gy, workspace, part_b, g, remap, kp)
+  if (wgrad_pair(N, W)) {
+    if (pre) BPK_WG(true, true); else BPK_WG(true, false);
+  } else {
+    if (pre) BPK_WG(false, true); else BPK_WG(false, false);
+  }
+#undef BPK_WG
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
   const int64_t pairs = (int64_t)Cin * Cout;
   BPK_REQUIRE(bpk::ceil_div(pairs, 16) < (1LL << 31), "conv3x3_wino_wgrad: too many pairs");

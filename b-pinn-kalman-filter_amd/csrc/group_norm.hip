@@ -262,7 +262,9 @@ __global__ __launch_bounds__(64) void gn_affine_kernel(const float* __restrict__
                                                        const float* __restrict__ bias_nc,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta,
-                                                       float2* __restrict__ ss, int C, int G,
+                                                       float2* __restrict__ ss,
+                                                       float* __restrict__ mean_out,
+                                                       float* __restrict__ rstd_out, int C, int G,
                                                        int splits, float eps) {
   __shared__ float s_stat[2];
   const int ng = blockIdx.x;
@@ -274,6 +276,8 @@ __global__ __launch_bounds__(64) void gn_affine_kernel(const float* __restrict__
     combine_partials(part + (int64_t)ng * splits * 3, splits, mean, m2, count);
     s_stat[0] = mean;
     s_stat[1] = 1.f / sqrtf(m2 / count + eps);
+    if (mean_out) mean_out[ng] = mean;
+    if (rstd_out) rstd_out[ng] = s_stat[1];
   }
   __syncthreads();
   for (int j = threadIdx.x; j < cpg; j += blockDim.x) {
@@ -702,10 +706,11 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
   return BPK_OK;
 }
 
-extern "C" int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float* gamma,
-                                         const float* beta, float* scale_shift, void* workspace,
-                                         int N, int C, int64_t HW, int G, float eps,
-                                         void* stream) {
+extern "C" int bpk_group_norm_affine_stats_f32(const float* x, const float* bias_nc,
+                                               const float* gamma, const float* beta,
+                                               float* scale_shift, float* mean, float* rstd,
+                                               void* workspace, int N, int C, int64_t HW, int G,
+                                               float eps, void* stream) {
   BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && G > 0, "group_norm_affine: bad shape");
   BPK_REQUIRE(C % G == 0, "group_norm_affine: C (%d) not divisible by G (%d)", C, G);
   BPK_REQUIRE(workspace != nullptr, "group_norm_affine: workspace required");
@@ -724,9 +729,17 @@ extern "C" int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, c
                        (int)HW, G, p.splits);
   BPK_LAUNCH_CHECK("group_norm_affine(partial)");
   hipLaunchKernelGGL(gn_affine_kernel, dim3(N * G), dim3(64), 0, st, part, bias_nc, gamma, beta,
-                     reinterpret_cast<float2*>(scale_shift), C, G, p.splits, eps);
+                     reinterpret_cast<float2*>(scale_shift), mean, rstd, C, G, p.splits, eps);
   BPK_LAUNCH_CHECK("group_norm_affine");
   return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float* gamma,
+                                         const float* beta, float* scale_shift, void* workspace,
+                                         int N, int C, int64_t HW, int G, float eps,
+                                         void* stream) {
+  return bpk_group_norm_affine_stats_f32(x, bias_nc, gamma, beta, scale_shift, nullptr, nullptr,
+                                         workspace, N, C, HW, G, eps, stream);
 }
 
 // ---------------------------------------------------------------- statistics from partials
@@ -739,7 +752,8 @@ namespace {
 __global__ __launch_bounds__(256) void gn_affine_partials_kernel(
     const float2* __restrict__ part, const float2* __restrict__ part2, int C1, int R, float cnt,
     const float* __restrict__ bias_nc, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float2* __restrict__ ss, int C, int G, float eps) {
+    const float* __restrict__ beta, float2* __restrict__ ss, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int C, int G, float eps) {
   __shared__ float sbuf[256 / kWave];
   __shared__ float s_stat[2];
   const int ng = blockIdx.x;
@@ -769,6 +783,8 @@ __global__ __launch_bounds__(256) void gn_affine_partials_kernel(
   if (threadIdx.x == 0) {
     s_stat[0] = mean;
     s_stat[1] = 1.f / sqrtf(m2 / ((float)K * cnt) + eps);
+    if (mean_out) mean_out[ng] = mean;
+    if (rstd_out) rstd_out[ng] = s_stat[1];
   }
   __syncthreads();
   for (int j = threadIdx.x; j < cpg; j += blockDim.x) {
@@ -802,10 +818,11 @@ __global__ __launch_bounds__(256) void gn_chunk_partials_kernel(const float* __r
 }
 }  // namespace
 
-extern "C" int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt,
-                                                  const float* bias_nc, const float* gamma,
-                                                  const float* beta, float* scale_shift, int N,
-                                                  int C, int G, float eps, void* stream) {
+extern "C" int bpk_group_norm_affine_partials_stats_f32(const float* part, int R, int cnt,
+                                                        const float* bias_nc, const float* gamma,
+                                                        const float* beta, float* scale_shift,
+                                                        float* mean, float* rstd, int N, int C,
+                                                        int G, float eps, void* stream) {
   BPK_REQUIRE(N >= 0 && C > 0 && G > 0 && R > 0 && cnt > 0,
               "group_norm_affine_partials: bad shape");
   BPK_REQUIRE(C % G == 0, "group_norm_affine_partials: C (%d) not divisible by G (%d)", C, G);
@@ -813,9 +830,18 @@ extern "C" int bpk_group_norm_affine_partials_f32(const float* part, int R, int 
   if (N == 0) return BPK_OK;
   hipLaunchKernelGGL(gn_affine_partials_kernel, dim3(N * G), dim3(256), 0, bpk::as_stream(stream),
                      reinterpret_cast<const float2*>(part), nullptr, C, R, (float)cnt, bias_nc,
-                     gamma, beta, reinterpret_cast<float2*>(scale_shift), C, G, eps);
+                     gamma, beta, reinterpret_cast<float2*>(scale_shift), mean, rstd, C, G, eps);
   BPK_LAUNCH_CHECK("group_norm_affine_partials");
   return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt,
+                                                  const float* bias_nc, const float* gamma,
+                                                  const float* beta, float* scale_shift, int N,
+                                                  int C, int G, float eps, void* stream) {
+  return bpk_group_norm_affine_partials_stats_f32(part, R, cnt, bias_nc, gamma, beta,
+                                                  scale_shift, nullptr, nullptr, N, C, G, eps,
+                                                  stream);
 }
 
 extern "C" int bpk_group_norm_affine_partials2_f32(const float* part, int C1, const float* part2,
@@ -831,7 +857,7 @@ extern "C" int bpk_group_norm_affine_partials2_f32(const float* part, int C1, co
   hipLaunchKernelGGL(gn_affine_partials_kernel, dim3(N * G), dim3(256), 0, bpk::as_stream(stream),
                      reinterpret_cast<const float2*>(part), reinterpret_cast<const float2*>(part2),
                      C1, R, (float)cnt, bias_nc, gamma, beta,
-                     reinterpret_cast<float2*>(scale_shift), C, G, eps);
+                     reinterpret_cast<float2*>(scale_shift), nullptr, nullptr, C, G, eps);
   BPK_LAUNCH_CHECK("group_norm_affine_partials2");
   return BPK_OK;
 }
@@ -847,5 +873,55 @@ extern "C" int bpk_group_norm_chunk_partials_f32(const float* x, float* part, in
                      dim3(256), 0, bpk::as_stream(stream), x, reinterpret_cast<float2*>(part),
                      nchunks);
   BPK_LAUNCH_CHECK("group_norm_chunk_partials");
+  return BPK_OK;
+}
+
+// ---------------------------------------------------------------- per-(n, c) affine + SiLU
+// y = silu(x * s + t), (s, t) = scale_shift[n][c]: the activation the Winograd conv's
+// GroupNorm prologue computes in its patch load, materialised when a weight gradient needs it
+// (op.norm_act.affine_silu; the same expression as the prologue: one FMA, __expf, rcp).
+namespace {
+__global__ __launch_bounds__(256) void affine_silu_kernel(const float* __restrict__ x,
+                                                          const float2* __restrict__ ss,
+                                                          float* __restrict__ y, int64_t planes,
+                                                          int HW, int vec) {
+  const int64_t pl = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (pl >= planes) return;
+  const float2 st = ss[pl];
+  const int64_t base = pl * HW;
+  if (vec) {
+    for (int e = (blockIdx.x * 256 + threadIdx.x) * 4; e < HW; e += gridDim.x * 256 * 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + base + e);
+      float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float z = o[q] * st.x + st.y;
+        o[q] = z * __builtin_amdgcn_rcpf(1.f + __expf(-z));
+      }
+      *reinterpret_cast<float4*>(y + base + e) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  } else {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < HW; e += gridDim.x * 256) {
+      const float z = x[base + e] * st.x + st.y;
+      y[base + e] = z * __builtin_amdgcn_rcpf(1.f + __expf(-z));
+    }
+  }
+}
+}  // namespace
+
+extern "C" int bpk_affine_silu_f32(const float* x, const float* scale_shift, float* y, int N,
+                                   int C, int64_t HW, void* stream) {
+  BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && HW < (1ll << 31), "affine_silu: bad shape");
+  BPK_REQUIRE(x && scale_shift && y, "affine_silu: null pointer");
+  const int64_t planes = (int64_t)N * C;
+  if (planes == 0) return BPK_OK;
+  const int vec = (HW % 4 == 0 && is_aligned16(x) && is_aligned16(y)) ? 1 : 0;
+  const int64_t per = vec ? bpk::ceil_div(HW, 4) : HW;
+  const unsigned bx = (unsigned)std::min<int64_t>(bpk::ceil_div(per, 256), 64);
+  const dim3 grid(bx, (unsigned)std::min<int64_t>(planes, 65535),
+                  (unsigned)bpk::ceil_div(planes, 65535));
+  hipLaunchKernelGGL(affine_silu_kernel, grid, dim3(256), 0, bpk::as_stream(stream), x,
+                     reinterpret_cast<const float2*>(scale_shift), y, planes, (int)HW, vec);
+  BPK_LAUNCH_CHECK("affine_silu");
   return BPK_OK;
 }

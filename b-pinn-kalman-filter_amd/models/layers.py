@@ -118,6 +118,7 @@ _IN_FUSED = True      # InstanceNorm+ELU (+ backward, double backward) as one ke
 _GN_STATS = True      # GroupNorm partial statistics from the producing conv's epilogue
 _GEMM1X1 = True       # 1x1 convs on the MFMA GEMM kernels
 _DDPM_FUSED = True    # ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs
+_GN_CONV_AD = __import__("os").environ.get("BPK_GN_CONV_AD", "1") != "0"  # TEMP A/B
 
 
 def _is_3x3(x, conv: nn.Conv2d):
@@ -175,6 +176,26 @@ def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=N
     ss = group_norm_affine(x, gn, bias_nc)
     return conv_op.conv3x3(x, conv.weight, conv_bias, skip=skip, div=div, pre=ss,
                            stats=_GN_STATS and conv_op.wino_supported(x, conv.weight))
+
+
+def gn_silu_conv_ad(x, gn: nn.GroupNorm, conv: nn.Conv2d, act, bias_nc=None, conv_bias=None,
+                    skip=None, div=1.0):
+    """gn_silu_conv under autograd (training, DPS): conv(SiLU(GroupNorm(x + bias_nc)))
+    [+ residual tail] with the normalization inside the Winograd conv's input load and a
+    backward that recomputes it (op.conv.gn_silu_conv3x3_ad); None when it does not apply
+    (no autograd graph to record, another activation, a conv the kernel does not take)."""
+    if not (_GN_CONV_AD and torch.is_grad_enabled() and isinstance(act, nn.SiLU)
+            and _is_3x3(x, conv)):
+        return None
+    if skip is not None and skip.shape[1] != conv.out_channels:
+        return None
+    return conv_op.gn_silu_conv3x3_ad(x, gn.num_groups, gn.weight if gn.affine else None,
+                                      gn.bias if gn.affine else None, gn.eps, conv.weight,
+                                      conv_bias, skip, div, bias_nc)
+
+
+def _dropout_off(m: nn.Dropout) -> bool:
+    return not m.training or m.p == 0
 
 
 def conv_residual(h, conv: nn.Conv2d, bias, skip, div, stats=False):
@@ -375,15 +396,22 @@ class ResnetBlockDDPM(nn.Module):
             if h is None:
                 h = conv_nobias(gn_act(x, self.GroupNorm_0, self.act), self.Conv_0)
             return self._fused_tail(h, x, None, temb)
-        h = gn_act(x, self.GroupNorm_0, self.act)
-        h = conv_nobias(h, self.Conv_0)
+        h = gn_silu_conv_ad(x, self.GroupNorm_0, self.Conv_0, self.act)
+        if h is None:
+            h = gn_act(x, self.GroupNorm_0, self.act)
+            h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
         if temb is not None:
             bias_nc = bias_nc + temb_proj(self.Dense_0, self.act, temb)
-        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
-        h = self.Dropout_0(h)
         if self.in_ch != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
+        if _dropout_off(self.Dropout_0):
+            out = gn_silu_conv_ad(h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
+                                  self.Conv_1.bias, x, 1.0)
+            if out is not None:
+                return out
+        h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)
+        h = self.Dropout_0(h)
         return conv_residual(h, self.Conv_1, self.Conv_1.bias, x, 1.0)
 
     def forward_pair(self, x1, x2, temb=None):

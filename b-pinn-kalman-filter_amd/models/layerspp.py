@@ -293,6 +293,9 @@ class ResnetBlockBigGANpp(nn.Module):
         if fused and not (self.up or self.down):
             # GroupNorm_0 + SiLU applied inside Conv_0's input load (inference)
             h = layers.gn_silu_conv(x, self.GroupNorm_0, self.Conv_0)
+        if h is None and not (self.up or self.down):
+            # under autograd: the same fusion with a backward that recomputes the normalization
+            h = layers.gn_silu_conv_ad(x, self.GroupNorm_0, self.Conv_0, self.act)
         if h is None:
             h = gn_act(x, self.GroupNorm_0, self.act)
             h = self._resample(h)
@@ -311,6 +314,11 @@ class ResnetBlockBigGANpp(nn.Module):
         if fused:
             # GroupNorm_1 (+ time bias) + SiLU + Conv_1 + residual tail: two launches
             out = layers.gn_silu_conv(h, self.GroupNorm_1, self.Conv_1, bias_nc, bias, x, div)
+            if out is not None:
+                return out
+        elif layers._dropout_off(self.Dropout_0):
+            out = layers.gn_silu_conv_ad(h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc, bias,
+                                         x, div)
             if out is not None:
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)

@@ -19,6 +19,7 @@ import os
 
 import torch
 import torch.nn.functional as F
+from torch.autograd.function import once_differentiable
 
 from . import flops
 from ._lib import check, lib, require_hip, stream_ptr, mark_inputs, want_grad
@@ -219,10 +220,12 @@ def wgrad_supported(x, weight):
     return bool(lib.bpk_conv3x3_wino_wgrad_supported(N, C, cout, H, W))
 
 
-def conv3x3_wgrad_raw(x, gy, wshape, bias_grad=False):
+def conv3x3_wgrad_raw(x, gy, wshape, bias_grad=False, pre=None):
     """dw [Cout, Cin, 3, 3] of conv3x3(x, w) for the output gradient gy (Winograd split-K,
     csrc/conv_winograd_wgrad.hip); == torch.nn.grad.conv2d_weight(x, wshape, gy, padding=1).
-    bias_grad=True: returns (dw, db) with db = gy.sum((0, 2, 3)) from the same kernel."""
+    bias_grad=True: returns (dw, db) with db = gy.sum((0, 2, 3)) from the same kernel.
+    pre [N, Cin, 2] = (s, t): the convolved input is silu(x * s + t) (the GroupNorm+SiLU
+    prologue of gn_silu_conv3x3_ad), applied in the kernel's patch load."""
     x = x.detach().contiguous()
     gy = gy.detach().contiguous()
     N, C, H, W = x.shape
@@ -234,9 +237,13 @@ def conv3x3_wgrad_raw(x, gy, wshape, bias_grad=False):
     ws = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
     dw = torch.empty((Cout, C, 3, 3), dtype=torch.float32, device=x.device)
     db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if bias_grad else None
-    check(lib.bpk_conv3x3_wino_wgrad_bias_f32(
-        x.data_ptr(), gy.data_ptr(), dw.data_ptr(), None if db is None else db.data_ptr(),
-        ws.data_ptr(), N, C, Cout, H, W, stream_ptr(x.device)), "conv3x3_wgrad")
+    pr = None if pre is None else pre.detach().contiguous()
+    if pr is not None and tuple(pr.shape) != (N, C, 2):
+        raise RuntimeError(f"conv3x3_wgrad: pre must be [N, Cin, 2], got {tuple(pr.shape)}")
+    check(lib.bpk_conv3x3_wino_wgrad_pre_f32(
+        x.data_ptr(), None if pr is None else pr.data_ptr(), gy.data_ptr(), dw.data_ptr(),
+        None if db is None else db.data_ptr(), ws.data_ptr(), N, C, Cout, H, W,
+        stream_ptr(x.device)), "conv3x3_wgrad")
     flops.wino3x3("wino_wgrad", N, C, Cout, H, W)
     return (dw, db) if bias_grad else dw
 
@@ -839,6 +846,87 @@ def conv3x3(x, weight, bias=None, skip=None, div=1.0, pre=None, stats=False):
     if stats and wino_supported(x, weight) and not _needs_grad(x, weight, bias, skip):
         return conv3x3_fwd_raw(x, weight, bias, skip, div, None, stats)
     return _Conv3x3.apply(x, weight, bias, skip, div)
+
+
+class _GNSiLUConv3x3(torch.autograd.Function):
+    """y = (skip + conv3x3(SiLU(GroupNorm(x + bias_nc)), w) + b) / div under autograd, with the
+    normalization applied in the Winograd conv's input load (reference layerspp.py:242-274,
+    layers.py:626-655: GroupNorm -> act -> Conv), so the normalized activation is never
+    stored in the forward.  Backward: the backward-data conv gives d/d(activation); the
+    GroupNorm+SiLU backward recomputes the normalization from x and the saved group
+    statistics; the weight gradient (only when the engine wants it: DPS differentiates
+    w.r.t. the input alone) applies the same (s, t) in its own patch load (or, for shapes the
+    Winograd weight gradient does not take, runs on the activation recomputed from them).
+    First order only (the score nets are differentiated once)."""
+
+    @staticmethod
+    def forward(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats):
+        from .norm_act import group_norm_affine_stats
+        mark_inputs(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats)
+        ss, mean, rstd = group_norm_affine_stats(x, G, gamma, beta, eps, bias_nc)
+        x = x.detach()
+        if gn_partials(x) is None:
+            x = x.contiguous()
+        y = conv3x3_fwd_raw(x, weight.detach(), bias, skip, div, pre=ss, stats=stats)
+        ctx.save_for_backward(x, bias_nc, gamma, beta, weight, mean, rstd, ss)
+        ctx.G, ctx.div = G, float(div)
+        ctx.has_bias, ctx.has_skip = bias is not None, skip is not None
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gy):
+        from .norm_act import ACT_SILU, affine_silu, group_norm_act_backward
+        x, bnc, gamma, beta, w, mean, rstd, ss = ctx.saved_tensors
+        gy = gy.contiguous()
+        if ctx.div != 1.0:
+            gy = gy / ctx.div
+        gskip = gy if ctx.has_skip and want_grad(ctx, 6) else None
+        want_w, want_cb = want_grad(ctx, 4), ctx.has_bias and want_grad(ctx, 5)
+        gw = gcb = None
+        if want_w and wgrad_supported(x, tuple(w.shape)):  # the activation never stored
+            r = conv3x3_wgrad_raw(x, gy, tuple(w.shape), bias_grad=want_cb, pre=ss)
+            gw, gcb = r if want_cb else (r, None)
+        elif want_w:
+            gw, gcb = _wgrad_impl(affine_silu(x, ss), gy, tuple(w.shape), want_cb)
+        elif want_cb:
+            gcb = gy.sum((0, 2, 3))
+        dx = d_bnc = dgamma = dbeta = None
+        want_x, want_bnc = want_grad(ctx, 0), bnc is not None and want_grad(ctx, 1)
+        want_g = gamma is not None and want_grad(ctx, 2)
+        want_b = beta is not None and want_grad(ctx, 3)
+        if want_x or want_bnc or want_g or want_b:
+            ga = _fwd_ft_impl(gy, w)
+            dx, d_bnc, dgamma, dbeta = group_norm_act_backward(
+                ga, x, bnc, gamma, beta, mean, rstd, ctx.G, ACT_SILU, want_bnc, want_g, want_b)
+        return dx, d_bnc, dgamma, dbeta, gw, gcb, gskip, None, None, None, None
+
+
+def gn_silu_conv3x3_ad_supported(x, weight):
+    """shapes the autograd GroupNorm+SiLU+conv form takes: the 16-cin Winograd kernel's (with
+    the output's GroupNorm partial statistics) or the 8-wide pair form"""
+    if x.dim() != 4 or not x.is_cuda or x.dtype != torch.float32 or not _shape_ok(x, weight):
+        return False
+    if weight.shape[1] > 1024:  # the prologue's GroupNorm table (kPreMaxCin)
+        return False
+    return wino_supported(x, weight) or (wino_pair_supported(x, weight)
+                                         and 2 * weight.shape[1] <= 1024)
+
+
+def gn_silu_conv3x3_ad(x, num_groups, gamma, beta, eps, weight, bias=None, skip=None, div=1.0,
+                       bias_nc=None):
+    """(skip + conv3x3(SiLU(GroupNorm(x + bias_nc)), weight) + bias) / div, differentiable
+    (first order), the normalization inside the conv's input load; the output carries
+    GroupNorm partial statistics for the next GroupNorm when the 16-cin kernel runs.  None
+    when the shape does not qualify (gn_silu_conv3x3_ad_supported)."""
+    require_hip(x, weight, bias, skip, bias_nc, what="gn_silu_conv3x3_ad")
+    if not gn_silu_conv3x3_ad_supported(x, weight):
+        return None
+    if skip is not None and tuple(skip.shape) != (x.shape[0], weight.shape[0]) + tuple(x.shape[2:]):
+        return None
+    stats = bool(wino_supported(x, weight))
+    return _GNSiLUConv3x3.apply(x, bias_nc, gamma, beta, weight, bias, skip, num_groups,
+                                float(eps), float(div), stats)
 
 
 def up2_supported(x, weight):

@@ -54,26 +54,35 @@ class _GroupNormAct(Function):
     @staticmethod
     def backward(ctx, dy):
         x, bnc, weight, bias, mean, rstd = ctx.saved_tensors
-        dy = dy.contiguous()
-        N, C = x.shape[:2]
-        HW = x.numel() // max(N * C, 1)
-        G = ctx.num_groups
-        dx = torch.empty_like(x)
-        need_affine = weight is not None and (want_grad(ctx, 2) or want_grad(ctx, 3))
-        dg = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
-        db = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
-        ws = _ws(N, C, HW, G, x.device)
-        check(lib.bpk_group_norm_bwd_f32(
-            dy.data_ptr(), x.data_ptr(), bnc.data_ptr() if bnc is not None else None,
-            weight.data_ptr() if weight is not None else None,
-            bias.data_ptr() if bias is not None else None, mean.data_ptr(), rstd.data_ptr(),
-            dx.data_ptr(), dg.data_ptr() if dg is not None else None,
-            db.data_ptr() if db is not None else None, ws.data_ptr() if ws is not None else None,
-            N, C, HW, G, ctx.act, stream_ptr(x.device)), "group_norm_act_bwd")
-        d_bnc = dx.reshape(N, C, -1).sum(-1) if (ctx.has_bnc and want_grad(ctx, 1)) else None
-        dw = dg.sum(0) if dg is not None and want_grad(ctx, 2) else None
-        dbeta = db.sum(0) if db is not None and want_grad(ctx, 3) else None
+        dx, d_bnc, dw, dbeta = group_norm_act_backward(
+            dy, x, bnc, weight, bias, mean, rstd, ctx.num_groups, ctx.act,
+            ctx.has_bnc and want_grad(ctx, 1), want_grad(ctx, 2), want_grad(ctx, 3))
         return dx, d_bnc, dw, dbeta, None, None, None
+
+
+def group_norm_act_backward(dy, x, bnc, weight, bias, mean, rstd, G, act, want_bnc, want_w,
+                            want_b):
+    """(dx, d bias_nc, d gamma, d beta) of y = act(GroupNorm(x + bias_nc)) for the output
+    gradient dy, from the forward's group statistics (None where not wanted)."""
+    dy = dy.contiguous()
+    N, C = x.shape[:2]
+    HW = x.numel() // max(N * C, 1)
+    dx = torch.empty_like(x)
+    need_affine = weight is not None and (want_w or want_b)
+    dg = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
+    db = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
+    ws = _ws(N, C, HW, G, x.device)
+    check(lib.bpk_group_norm_bwd_f32(
+        dy.data_ptr(), x.data_ptr(), bnc.data_ptr() if bnc is not None else None,
+        weight.data_ptr() if weight is not None else None,
+        bias.data_ptr() if bias is not None else None, mean.data_ptr(), rstd.data_ptr(),
+        dx.data_ptr(), dg.data_ptr() if dg is not None else None,
+        db.data_ptr() if db is not None else None, ws.data_ptr() if ws is not None else None,
+        N, C, HW, G, act, stream_ptr(x.device)), "group_norm_act_bwd")
+    d_bnc = dx.reshape(N, C, -1).sum(-1) if (bnc is not None and want_bnc) else None
+    dw = dg.sum(0) if dg is not None and want_w else None
+    dbeta = db.sum(0) if db is not None and want_b else None
+    return dx, d_bnc, dw, dbeta
 
 
 def group_norm_act(x, gn: torch.nn.GroupNorm, act: int = ACT_SILU, bias_nc=None):
@@ -139,6 +148,53 @@ def group_norm_affine(x, gn: torch.nn.GroupNorm, bias_nc=None):
         ws.data_ptr() if ws is not None else None, N, C, HW, G, float(gn.eps),
         stream_ptr(x.device)), "group_norm_affine")
     return ss
+
+
+def group_norm_affine_stats(x, num_groups, weight, bias, eps, bias_nc=None):
+    """(ss [N, C, 2], mean [N, G], rstd [N, G]): the affine form of SiLU(GroupNorm(x + bias_nc))
+    (as group_norm_affine) plus the group statistics it was built from, for the backward of a
+    conv that applied it in its input load (op.conv.gn_silu_conv3x3_ad).  From the producer's
+    partial statistics when x carries them (no pass over x), else one read of x."""
+    require_hip(x, bias_nc, what="group_norm_affine_stats")
+    from .conv import gn_partials
+    x = x.contiguous() if gn_partials(x) is None else x
+    N, C = x.shape[:2]
+    G = num_groups
+    HW = x.numel() // max(N * C, 1)
+    ss = torch.empty((N, C, 2), device=x.device, dtype=torch.float32)
+    mean = torch.empty((N, G), device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    bnc = bias_nc.detach().contiguous() if bias_nc is not None else None
+    wp = weight.detach().data_ptr() if weight is not None else None
+    bp = bias.detach().data_ptr() if bias is not None else None
+    bncp = bnc.data_ptr() if bnc is not None else None
+    part = gn_partials(x)
+    if part is not None:
+        pt, R, cnt = part
+        check(lib.bpk_group_norm_affine_partials_stats_f32(
+            pt.data_ptr(), R, cnt, bncp, wp, bp, ss.data_ptr(), mean.data_ptr(),
+            rstd.data_ptr(), N, C, G, float(eps), stream_ptr(x.device)),
+            "group_norm_affine_partials_stats")
+    else:
+        ws = _ws(N, C, HW, G, x.device)
+        check(lib.bpk_group_norm_affine_stats_f32(
+            x.data_ptr(), bncp, wp, bp, ss.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+            ws.data_ptr() if ws is not None else None, N, C, HW, G, float(eps),
+            stream_ptr(x.device)), "group_norm_affine_stats")
+    return ss, mean, rstd
+
+
+def affine_silu(x, ss):
+    """silu(x * s + t) for ss [N, C, 2] = (s, t): the activation the Winograd conv's GroupNorm
+    prologue computes, materialised (for the conv's weight gradient)."""
+    require_hip(x, ss, what="affine_silu")
+    x = x.contiguous()
+    N, C = x.shape[:2]
+    y = torch.empty_like(x)
+    check(lib.bpk_affine_silu_f32(x.data_ptr(), ss.contiguous().data_ptr(), y.data_ptr(), N, C,
+                                  x.numel() // max(N * C, 1), stream_ptr(x.device)),
+          "affine_silu")
+    return y
 
 
 class _Residual(Function):

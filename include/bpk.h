@@ -226,12 +226,25 @@ int bpk_group_norm_fwd_f32(const float* x, const float* bias_nc, const float* ga
 int bpk_group_norm_affine_f32(const float* x, const float* bias_nc, const float* gamma,
                               const float* beta, float* scale_shift, void* workspace, int N, int C,
                               int64_t HW, int G, float eps, void* stream);
+/* Same, also writing the group statistics mean / rstd [N, G] the affine form was built from
+ * (may be NULL): the GroupNorm backward (bpk_group_norm_bwd_f32) of a conv that applied the
+ * normalization in its input load under autograd (op.norm_act.group_norm_affine_stats). */
+int bpk_group_norm_affine_stats_f32(const float* x, const float* bias_nc, const float* gamma,
+                                    const float* beta, float* scale_shift, float* mean,
+                                    float* rstd, void* workspace, int N, int C, int64_t HW, int G,
+                                    float eps, void* stream);
 /* The same affine form from per-(n, channel, region) partial statistics written by the
  * producer of x (bpk_conv3x3_wino_ex_f32): part [N, C, R, 2] = (mean, M2) of cnt values
  * each; no pass over x.  Deterministic (fixed reduction order). */
 int bpk_group_norm_affine_partials_f32(const float* part, int R, int cnt, const float* bias_nc,
                                        const float* gamma, const float* beta, float* scale_shift,
                                        int N, int C, int G, float eps, void* stream);
+/* Same, also writing mean / rstd [N, G] (may be NULL). */
+int bpk_group_norm_affine_partials_stats_f32(const float* part, int R, int cnt,
+                                             const float* bias_nc, const float* gamma,
+                                             const float* beta, float* scale_shift, float* mean,
+                                             float* rstd, int N, int C, int G, float eps,
+                                             void* stream);
 /* Same for the channel concatenation [x1 (C1 channels), x2 (C - C1)] from the two tensors'
  * own partials (part [N, C1, R, 2], part2 [N, C - C1, R, 2]) -- the up path's
  * torch.cat([h, hs.pop()], 1) (reference models/ncsnpp.py:318) without concatenating
@@ -245,6 +258,11 @@ int bpk_group_norm_affine_partials2_f32(const float* part, int C1, const float* 
  * above consume (R = HW / 128, cnt = 128).  One read of x. */
 int bpk_group_norm_chunk_partials_f32(const float* x, float* part, int N, int C, int64_t HW,
                                       void* stream);
+/* y = silu(x * s + t) with scale_shift[n][c] = (s, t): the activation the Winograd conv's
+ * GroupNorm prologue computes, materialised for the conv's weight gradient under autograd
+ * (same arithmetic as the prologue). */
+int bpk_affine_silu_f32(const float* x, const float* scale_shift, float* y, int N, int C,
+                        int64_t HW, void* stream);
 int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc,
                            const float* gamma, const float* beta, const float* mean,
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,
@@ -420,6 +438,12 @@ int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float* dw, float
 int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, float* dw, float* db,
                                     float* workspace, int N, int Cin, int Cout, int H, int W,
                                     void* stream);
+/* Same with the convolved input silu(x * s + t), pre[n][cin] = (s, t) (may be NULL: x itself):
+ * the weight gradient of the GroupNorm+SiLU-prologue conv (bpk_conv3x3_wino_ex_f32 with pre)
+ * without materialising the activation. */
+int bpk_conv3x3_wino_wgrad_pre_f32(const float* x, const float* pre, const float* gy, float* dw,
+                                   float* db, float* workspace, int N, int Cin, int Cout, int H,
+                                   int W, void* stream);
 
 /* 3x3 / stride 1 / pad 1 conv with a small channel count on one side (VALU, HBM-bound):
  * the score networks' conv_in (Cin = image channels, models/ncsnpp.py) and output_skip

@@ -784,6 +784,59 @@ def test_resblock_forward_pair_matches_concat(hip, hs_stats):
     assert gn_partials(out) is not None
 
 
+@pytest.mark.parametrize("kind,cin,cout,hw", [("biggan", 128, 128, 32), ("biggan", 128, 256, 8),
+                                              ("ddpm", 128, 128, 32), ("ddpm", 256, 128, 16)])
+def test_gn_silu_conv_under_autograd_matches_unfused(hip, kind, cin, cout, hw):
+    """The residual blocks under autograd (training, DPS) with GroupNorm+SiLU inside the
+    Winograd convs' input loads (op.conv.gn_silu_conv3x3_ad; 8x8 images on the pair form) ==
+    the unfused composition (GroupNorm+SiLU kernel, conv, residual): output, d/dx and every
+    parameter gradient within 2e-5 of the tensor's max; and d/dx alone (the DPS call:
+    torch.autograd.grad w.r.t. the input, no weight gradients computed)."""
+    import models.layers as layers
+    import models.layerspp as lpp
+    torch.manual_seed(0)
+    if kind == "biggan":
+        blk = lpp.ResnetBlockBigGANpp(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=64,
+                                      skip_rescale=True, init_scale=0., dropout=0.0)
+    else:
+        blk = layers.ResnetBlockDDPM(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=64,
+                                     dropout=0.0)
+    blk = blk.to(hip).train()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    g = torch.Generator().manual_seed(cin + cout + hw)
+    x0 = (torch.randn(4, cin, hw, hw, generator=g) * 1.5 + 0.3).to(hip)
+    temb = torch.randn(4, 64, generator=g).to(hip)
+    gout = torch.randn(4, cout, hw, hw, generator=g).to(hip)
+
+    def run(fused):
+        old = layers._GN_CONV_AD
+        layers._GN_CONV_AD = fused
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = blk(x, temb)
+            (y * gout).sum().backward()
+            grads = [p.grad.clone() for p in blk.parameters()]
+            x2 = x0.clone().requires_grad_()
+            gx_only = torch.autograd.grad((blk(x2, temb) * gout).sum(), x2)[0]
+        finally:
+            layers._GN_CONV_AD = old
+        return y.detach(), x.grad, grads, gx_only
+    yf, gxf, gpf, gof = run(True)
+    yu, gxu, gpu_, gou = run(False)
+
+    def close(a, b, what):
+        scale = b.abs().max().item()
+        assert (a - b).abs().max().item() <= 2e-5 * scale + 1e-30, what
+    close(yf, yu, "output")
+    close(gxf, gxu, "d/dx")
+    close(gof, gou, "d/dx (input-only call)")
+    for (name, _), a, b in zip(blk.named_parameters(), gpf, gpu_):
+        close(a, b, name)
+
+
 @pytest.mark.parametrize("k,stride,pad,cin,cout", [(3, 2, 1, 1, 16), (3, 2, 1, 16, 32), (1, 1, 0, 64, 128)])
 def test_conv2d_general_double_backward(hip, k, stride, pad, cin, cout):
     """conv2d_general (MIOpen kernels, derivatives of every order as convolutions / conv
@@ -1032,6 +1085,7 @@ _IG_CASES = [
     (64, 6, 64, 64, 6, 3, 1, 1),     # PINN 6-channel conv at 64^2: >64 wgrad splits (two-level sum)
     (2, 5, 10, 11, 7, 3, 3, 1),      # stride 3, small: backward-data as one launch (MODE 1)
     (16, 128, 65, 65, 256, 3, 2, 0),  # NCSN++ FIR-down conv: backward-data by pixel class (MODE 3)
+    (16, 128, 32, 32, 16, 3, 1, 1),  # PINN 16-channel conv: weight gradient on 16 x 256 tiles
 ]
 
 
