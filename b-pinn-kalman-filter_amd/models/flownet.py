@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from op import correlation, grid_sample
+from op import channels, correlation, grid_sample
 from op.fused_act import LeakyReLU, leaky_relu
 
 from . import layers
@@ -52,8 +52,8 @@ def project(f, u, dt):
     exactly as the reference pairs them; border padding, align_corners=True.
     """
     grid = _base_grid(u.shape, u.device)
-    step = torch.cat([u[:, 1:2] / ((f.size(2) - 1.0) / 2.0),
-                      u[:, 0:1] / ((f.size(3) - 1.0) / 2.0)], 1)
+    # torch.cat([u[:, 1:2] / .., u[:, 0:1] / ..], 1) as one op in every derivative order
+    step = channels.swap_scale(u, (f.size(2) - 1.0) / 2.0, (f.size(3) - 1.0) / 2.0)
     return grid_sample.grid_sample_2d(input=f, grid=(grid - step * dt).permute(0, 2, 3, 1),
                                       padding_mode="border", align_corners=True)
 
@@ -115,14 +115,25 @@ class FeatureExtractor(nn.Module):
         self.feature_extractors = nn.ModuleList(
             get_conv_feature_layer(a, b) for a, b in zip(widths[:-1], widths[1:]))
 
-    def forward(self, f, x, y, t):
-        pyramid = []
-        semb = self.spatial_emb(x, y)
+    def embeddings(self, x, y, t, channels_in):
+        """The (spatial, timestep) embedding added before each level: the same tensors for
+        both frames, so FlowNet computes them once (the reference builds them per frame:
+        identical values, and every derivative pass of the PINN residual then runs through
+        one copy of the sin / sqrt / pool chain instead of two)."""
+        out, semb, c = [], self.spatial_emb(x, y), channels_in
         for level in self.feature_extractors:
-            temb = layers.get_timestep_embedding(t, f.shape[1])[:, :, None, None]
+            out.append((semb, layers.get_timestep_embedding(t, c)[:, :, None, None]))
+            semb = self.semb_down(semb)
+            c = level[-2].out_channels
+        return out
+
+    def forward(self, f, x, y, t, emb=None):
+        pyramid = []
+        if emb is None:
+            emb = self.embeddings(x, y, t, f.shape[1])
+        for level, (semb, temb) in zip(self.feature_extractors, emb):
             f = level(f + semb + temb)
             pyramid.append(f)
-            semb = self.semb_down(semb)
         return pyramid
 
 
@@ -156,7 +167,7 @@ class SubpixelRefinement(nn.Module):
 
     def forward(self, feature1, feature2, flow):
         warped = project(feature2, flow, -self.dt)
-        return flow + self.flow_conv(torch.cat([feature1, warped, flow], dim=1))
+        return flow + self.flow_conv(channels.cat([feature1, warped, flow], dim=1))
 
 
 class InferenceUnit(nn.Module):
@@ -179,7 +190,7 @@ class Upsample(nn.Module):
 
     def forward(self, f1, f2, x, size):
         x = F.interpolate(input=x, size=size, mode="bilinear", align_corners=False)
-        return x + self.up(torch.cat([f1, f2, x], dim=1))
+        return x + self.up(channels.cat([f1, f2, x], dim=1))
 
 
 class FlowNet(nn.Module):
@@ -196,8 +207,9 @@ class FlowNet(nn.Module):
         self.upsample = Upsample()
 
     def forward(self, f1, f2, x, y, t, size=None):
-        p1 = self.feature_extractor(f1, x, y, t)
-        p2 = self.feature_extractor(f2, x, y, t)
+        emb = self.feature_extractor.embeddings(x, y, t, f1.shape[1])
+        p1 = self.feature_extractor(f1, x, y, t, emb)
+        p2 = self.feature_extractor(f2, x, y, t, emb)
         flows, flow = [], None
         for unit in self.inference_units:
             flow = unit(p1[unit.level], p2[unit.level], flow)
@@ -260,7 +272,7 @@ class PressureNet(nn.Module):
 
     def get_norm_feature(self, flow):
         """features of [u, v, -(u^2 + v^2)] (reference flownet.py:280-283)."""
-        return self.flow_feature(torch.cat([flow, -(flow ** 2).sum(dim=1, keepdim=True)], dim=1))
+        return self.flow_feature(channels.cat([flow, -(flow ** 2).sum(dim=1, keepdim=True)], dim=1))
 
     def get_semb_list(self, x, y):
         out = [self.spatial_emb(x, y)]
@@ -279,7 +291,7 @@ class PressureNet(nn.Module):
         skips.pop()
         for i, (up, up_conv) in enumerate(zip(self.up, self.up_conv)):
             ffeat = self.get_norm_feature(cascaded_flow[i + 2].detach().clone()) + temb + semb[-1 - i]
-            h = up_conv(torch.cat([skips[-1 - i], up(h), ffeat], dim=1))
+            h = up_conv(channels.cat([skips[-1 - i], up(h), ffeat], dim=1))
         return self.end(h)
 
     def data_mse(self, pressure, target, error_fn=torch.nn.MSELoss()):

@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from op import channels
 from op import conv as conv_op
 from op import matmul as matmul_op
 from op import norm_act as norm_act_op
@@ -118,7 +119,7 @@ _IN_FUSED = True      # InstanceNorm+ELU (+ backward, double backward) as one ke
 _GN_STATS = True      # GroupNorm partial statistics from the producing conv's epilogue
 _GEMM1X1 = True       # 1x1 convs on the MFMA GEMM kernels
 _DDPM_FUSED = True    # ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs
-_GN_CONV_AD = __import__("os").environ.get("BPK_GN_CONV_AD", "1") != "0"  # TEMP A/B
+_GN_CONV_AD = True    # eval-mode autograd (DPS): GroupNorm+SiLU inside the conv's input load
 
 
 def _is_3x3(x, conv: nn.Conv2d):
@@ -178,14 +179,18 @@ def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=N
                            stats=_GN_STATS and conv_op.wino_supported(x, conv.weight))
 
 
-def gn_silu_conv_ad(x, gn: nn.GroupNorm, conv: nn.Conv2d, act, bias_nc=None, conv_bias=None,
-                    skip=None, div=1.0):
-    """gn_silu_conv under autograd (training, DPS): conv(SiLU(GroupNorm(x + bias_nc)))
-    [+ residual tail] with the normalization inside the Winograd conv's input load and a
-    backward that recomputes it (op.conv.gn_silu_conv3x3_ad); None when it does not apply
-    (no autograd graph to record, another activation, a conv the kernel does not take)."""
-    if not (_GN_CONV_AD and torch.is_grad_enabled() and isinstance(act, nn.SiLU)
-            and _is_3x3(x, conv)):
+def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act, bias_nc=None,
+                    conv_bias=None, skip=None, div=1.0):
+    """gn_silu_conv under autograd for an eval-mode block (DPS: gradients of the score w.r.t.
+    the input through the net): conv(SiLU(GroupNorm(x + bias_nc))) [+ residual tail] with the
+    normalization inside the Winograd conv's input load and a backward that recomputes it
+    (op.conv.gn_silu_conv3x3_ad); None when it does not apply (training, no autograd graph to
+    record, another activation, a conv the kernel does not take).  Training keeps the unfused
+    composition: on the DSM and CIFAR train steps the fused form measured 2.8 % and 1.5 %
+    slower (the weight gradient's per-element SiLU in its patch load, the igemm choice lost
+    on small images), DPS 4.1 % faster (profiles/r05_gn_conv_ad_ab.txt)."""
+    if not (_GN_CONV_AD and not module.training and torch.is_grad_enabled()
+            and isinstance(act, nn.SiLU) and _is_3x3(x, conv)):
         return None
     if skip is not None and skip.shape[1] != conv.out_channels:
         return None
@@ -260,7 +265,7 @@ def get_timestep_embedding(timesteps, embedding_dim, max_positions=10000):
     rate = math.log(max_positions) / (half - 1)
     freqs = torch.exp(torch.arange(half, dtype=torch.float32, device=timesteps.device) * -rate)
     arg = timesteps.float()[:, None] * freqs[None, :]
-    emb = torch.cat([torch.sin(arg), torch.cos(arg)], dim=1)
+    emb = channels.cat([torch.sin(arg), torch.cos(arg)], dim=1)  # = torch.cat, any derivative order
     if embedding_dim % 2 == 1:
         emb = F.pad(emb, (0, 1), mode="constant")
     return emb
@@ -396,7 +401,7 @@ class ResnetBlockDDPM(nn.Module):
             if h is None:
                 h = conv_nobias(gn_act(x, self.GroupNorm_0, self.act), self.Conv_0)
             return self._fused_tail(h, x, None, temb)
-        h = gn_silu_conv_ad(x, self.GroupNorm_0, self.Conv_0, self.act)
+        h = gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act)
         if h is None:
             h = gn_act(x, self.GroupNorm_0, self.act)
             h = conv_nobias(h, self.Conv_0)
@@ -406,7 +411,7 @@ class ResnetBlockDDPM(nn.Module):
         if self.in_ch != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
         if _dropout_off(self.Dropout_0):
-            out = gn_silu_conv_ad(h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
+            out = gn_silu_conv_ad(self, h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
                                   self.Conv_1.bias, x, 1.0)
             if out is not None:
                 return out

@@ -294,8 +294,8 @@ class ResnetBlockBigGANpp(nn.Module):
             # GroupNorm_0 + SiLU applied inside Conv_0's input load (inference)
             h = layers.gn_silu_conv(x, self.GroupNorm_0, self.Conv_0)
         if h is None and not (self.up or self.down):
-            # under autograd: the same fusion with a backward that recomputes the normalization
-            h = layers.gn_silu_conv_ad(x, self.GroupNorm_0, self.Conv_0, self.act)
+            # eval-mode autograd (DPS): the same fusion, its backward recomputing the normalization
+            h = layers.gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act)
         if h is None:
             h = gn_act(x, self.GroupNorm_0, self.act)
             h = self._resample(h)
@@ -317,8 +317,8 @@ class ResnetBlockBigGANpp(nn.Module):
             if out is not None:
                 return out
         elif layers._dropout_off(self.Dropout_0):
-            out = layers.gn_silu_conv_ad(h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc, bias,
-                                         x, div)
+            out = layers.gn_silu_conv_ad(self, h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
+                                         bias, x, div)
             if out is not None:
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)

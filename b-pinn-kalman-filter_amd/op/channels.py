@@ -1,0 +1,79 @@
+"""Concatenation and channel swap with derivatives of every order that stay single ops.
+
+The PINN residual (reference pinn.py:72-111) differentiates FlowNet / PressureNet three
+times (the first-order sensitivities w.r.t. x, y, t with create_graph, the second-order ones,
+then the loss w.r.t. the parameters).  torch.cat's backward returns narrow views of the
+gradient; differentiated again, every view becomes `slice_backward` -- a zero fill of the
+whole gradient plus a copy into the slice -- and the pieces are summed with adds: 3k - 1
+launches per k-input concatenation per pass, ~2.5 k of the PINN step's launches.  Here the
+backward of `cat` is `split` (views, no launch) and the backward of `split` is one `cat`.
+The reference's own ops (models/flownet.py: torch.cat in SubpixelRefinement, Upsample,
+PressureNet; layers.py get_timestep_embedding) keep their values bit for bit: the forward is
+torch.cat itself.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+
+class _Cat(Function):
+    @staticmethod
+    def forward(ctx, dim, *xs):
+        ctx.dim = dim
+        ctx.sizes = tuple(x.shape[dim] for x in xs)
+        return torch.cat(xs, dim)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(_Split.apply(g, ctx.dim, ctx.sizes))
+
+
+class _Split(Function):
+    @staticmethod
+    def forward(ctx, g, dim, sizes):
+        ctx.dim = dim
+        ctx.shape = tuple(g.shape)
+        ctx.sizes = sizes
+        return tuple(torch.split(g, list(sizes), dim))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        return _Cat.apply(ctx.dim, *gs), None, None
+
+
+def cat(tensors, dim=0):
+    """torch.cat(tensors, dim) whose derivatives of every order are single cat / split ops."""
+    tensors = list(tensors)
+    if len(tensors) == 1:
+        return tensors[0]
+    if not torch.is_grad_enabled() or not any(t.requires_grad for t in tensors):
+        return torch.cat(tensors, dim)
+    return _Cat.apply(dim % tensors[0].dim(), *tensors)
+
+
+class _SwapScale(Function):
+    """out[:, 0] = u[:, 1] / c0, out[:, 1] = u[:, 0] / c1 for u [B, 2, ...]: a linear map whose
+    adjoint is the same map with the divisors exchanged."""
+
+    @staticmethod
+    def forward(ctx, u, c0, c1):
+        ctx.c = (c0, c1)
+        out = torch.empty_like(u)
+        torch.div(u[:, 1:2], c0, out=out[:, 0:1])
+        torch.div(u[:, 0:1], c1, out=out[:, 1:2])
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        c0, c1 = ctx.c
+        return _SwapScale.apply(g, c1, c0), None, None
+
+
+def swap_scale(u, c0, c1):
+    """torch.cat([u[:, 1:2] / c0, u[:, 0:1] / c1], 1), every derivative one such op."""
+    if u.shape[1] != 2:
+        raise RuntimeError(f"swap_scale: 2 channels expected, got {tuple(u.shape)}")
+    if not torch.is_grad_enabled() or not u.requires_grad:
+        return torch.cat([u[:, 1:2] / c0, u[:, 0:1] / c1], 1)
+    return _SwapScale.apply(u, float(c0), float(c1))

@@ -784,14 +784,32 @@ def test_resblock_forward_pair_matches_concat(hip, hs_stats):
     assert gn_partials(out) is not None
 
 
+def _count_gn_conv_ad():
+    """calls of op.conv._GNSiLUConv3x3.forward from now on"""
+    from op import conv
+    n = [0]
+    orig = conv._GNSiLUConv3x3.forward
+
+    def fwd(ctx, *a):
+        n[0] += 1
+        return orig(ctx, *a)
+    conv._GNSiLUConv3x3.forward = staticmethod(fwd)
+
+    def calls():
+        conv._GNSiLUConv3x3.forward = staticmethod(orig)
+        return n[0]
+    return calls
+
+
 @pytest.mark.parametrize("kind,cin,cout,hw", [("biggan", 128, 128, 32), ("biggan", 128, 256, 8),
                                               ("ddpm", 128, 128, 32), ("ddpm", 256, 128, 16)])
 def test_gn_silu_conv_under_autograd_matches_unfused(hip, kind, cin, cout, hw):
-    """The residual blocks under autograd (training, DPS) with GroupNorm+SiLU inside the
+    """The residual blocks in eval mode under autograd (DPS) with GroupNorm+SiLU inside the
     Winograd convs' input loads (op.conv.gn_silu_conv3x3_ad; 8x8 images on the pair form) ==
     the unfused composition (GroupNorm+SiLU kernel, conv, residual): output, d/dx and every
-    parameter gradient within 2e-5 of the tensor's max; and d/dx alone (the DPS call:
-    torch.autograd.grad w.r.t. the input, no weight gradients computed)."""
+    parameter gradient (the weight gradient with the prologue in its patch load) within 2e-5
+    of the tensor's max; and d/dx alone (the DPS call: torch.autograd.grad w.r.t. the input,
+    no weight gradients computed)."""
     import models.layers as layers
     import models.layerspp as lpp
     torch.manual_seed(0)
@@ -801,7 +819,7 @@ def test_gn_silu_conv_under_autograd_matches_unfused(hip, kind, cin, cout, hw):
     else:
         blk = layers.ResnetBlockDDPM(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=64,
                                      dropout=0.0)
-    blk = blk.to(hip).train()
+    blk = blk.to(hip).eval()
     with torch.no_grad():
         for p in blk.parameters():
             p.add_(torch.randn_like(p) * 0.05)
@@ -816,7 +834,9 @@ def test_gn_silu_conv_under_autograd_matches_unfused(hip, kind, cin, cout, hw):
         try:
             blk.zero_grad(set_to_none=True)
             x = x0.clone().requires_grad_()
+            calls = _count_gn_conv_ad()
             y = blk(x, temb)
+            assert (calls() > 0) == fused  # the fused path ran (or did not)
             (y * gout).sum().backward()
             grads = [p.grad.clone() for p in blk.parameters()]
             x2 = x0.clone().requires_grad_()

@@ -18,6 +18,17 @@ SKIP = {"empty", "empty_strided", "view", "_unsafe_view", "detach", "t", "as_str
         "expand", "reshape", "permute", "transpose", "unsqueeze", "squeeze", "slice", "select",
         "alias", "_reshape_alias", "lift_fresh", "split", "unbind", "is_same_size"}
 cnt = collections.Counter()
+sites = collections.Counter()  # (op, innermost repo frame) of the ops issued outside any node
+TRACE = {"clone", "zeros_like", "zeros", "add", "mul", "_to_copy", "div", "copy_", "sum",
+         "empty_like"}
+
+
+def _site():
+    import traceback
+    for fr in reversed(traceback.extract_stack()[:-3]):
+        if REPO in fr.filename and "pinn_op_sources" not in fr.filename:
+            return f"{os.path.relpath(fr.filename, REPO)}:{fr.lineno} {fr.line}"
+    return "?"
 
 
 class Mode(TorchDispatchMode):
@@ -26,6 +37,8 @@ class Mode(TorchDispatchMode):
         if name not in SKIP:
             node = torch._C._current_autograd_node()
             cnt[(name, node.name() if node is not None else "<forward>")] += 1
+            if node is None and name in TRACE:
+                sites[(name, _site())] += 1
         return func(*args, **(kwargs or {}))
 
 
@@ -51,3 +64,6 @@ for (op, _), v in cnt.items():
 print("by op:", by_op.most_common(25))
 for (op, node), v in cnt.most_common(60):
     print(f"{v:6d}  {op:28s} {node}")
+print("ops outside any autograd node, by call site:")
+for (op, site), v in sites.most_common(40):
+    print(f"{v:6d}  {op:12s} {site}")
