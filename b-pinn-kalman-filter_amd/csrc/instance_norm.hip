@@ -19,8 +19,9 @@
 // (derivation: DESIGN.md section 4b; e'(z) = exp(z), e''(z) = exp(z) for z <= 0, else 1, 0,
 // the branch aten's elu_backward takes at z = 0.)
 //
-// One wave per plane (4 planes per 256-thread block): reductions are lane-strided sums in a
-// fixed order followed by a butterfly, so results are deterministic; no LDS, no barriers.
+// Small planes (<= 256 elements) and very large ones: one wave per plane (4 planes per
+// 256-thread block), reductions lane-strided sums in a fixed order followed by a butterfly;
+// 257..4096 elements: one workgroup per plane (below).  Deterministic either way.
 #include "bpk_common.h"
 
 #include <cmath>
@@ -166,7 +167,236 @@ __global__ __launch_bounds__(256) void in_bwd2(const T* __restrict__ v, const T*
   }
 }
 
+// Planes of 257..4096 elements (PressureNet at 32^2 and 64^2): one 256-thread workgroup per
+// plane holding it in registers, so every pass after the first reads registers instead of
+// re-reading HBM and the plane's loads are all in flight at once (the one-wave kernels above
+// walk a 64^2 plane in 64 dependent steps per pass).  A thread owns V runs of W consecutive
+// elements (W = 4: 16-byte accesses, fp32 planes of M % 4 == 0), run k at (thread + 256 k) W.
+// Sums: per-thread in element order, wave butterfly, then the four wave sums in order
+// (deterministic).
+template <typename T>
+__device__ inline T bsum(T v, T* sh) {
+  v = wsum(v);
+  __syncthreads();  // the previous sum's readers are done with sh
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+template <typename T, int W>
+__device__ inline void ld(const T* p, T* v) {
+  static_assert(W == 1 || sizeof(T) == 4, "16-byte runs are fp32 only");
+  if constexpr (W == 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    v[0] = *p;
+  }
+}
+template <typename T, int W>
+__device__ inline void st(T* p, const T* v) {
+  if constexpr (W == 4)
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else
+    *p = v[0];
+}
+
+template <typename T, int V, int W>
+__global__ __launch_bounds__(256) void in_fwd_blk(const T* __restrict__ x, T* __restrict__ y,
+                                                  T* __restrict__ mean, T* __restrict__ rstd,
+                                                  int64_t M, T eps, int act) {
+  __shared__ T sh[4];
+  const int64_t p = blockIdx.x;
+  T xv[V][W];
+  T s = T(0);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = (threadIdx.x + 256 * (int64_t)k) * W;
+    if (e < M) ld<T, W>(x + p * M + e, xv[k]);
+    else
+#pragma unroll
+      for (int j = 0; j < W; ++j) xv[k][j] = T(0);
+#pragma unroll
+    for (int j = 0; j < W; ++j) s += xv[k][j];
+  }
+  const T mu = bsum(s, sh) / T(M);
+  T s2 = T(0);
+#pragma unroll
+  for (int k = 0; k < V; ++k)
+    if ((threadIdx.x + 256 * (int64_t)k) * W < M)
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T d = xv[k][j] - mu;
+        s2 += d * d;
+      }
+  const T r = T(1) / sqrt(bsum(s2, sh) / T(M) + eps);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = (threadIdx.x + 256 * (int64_t)k) * W;
+    if (e >= M) continue;
+    T o[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) o[j] = act_f((xv[k][j] - mu) * r, act);
+    st<T, W>(y + p * M + e, o);
+  }
+  if (threadIdx.x == 0) {
+    mean[p] = mu;
+    rstd[p] = r;
+  }
+}
+
+template <typename T, int V, int W>
+__global__ __launch_bounds__(256) void in_bwd_blk(const T* __restrict__ dy, const T* __restrict__ x,
+                                                  const T* __restrict__ mean,
+                                                  const T* __restrict__ rstd, T* __restrict__ dx,
+                                                  int64_t M, int act) {
+  __shared__ T sh[4];
+  const int64_t p = blockIdx.x;
+  const T mu = mean[p], r = rstd[p];
+  T z[V][W], g[V][W];
+  T sg = T(0), sgz = T(0);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = (threadIdx.x + 256 * (int64_t)k) * W;
+    T xv[W], dv[W];
+    if (e < M) {
+      ld<T, W>(x + p * M + e, xv);
+      ld<T, W>(dy + p * M + e, dv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < W; ++j) xv[j] = dv[j] = T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      z[k][j] = e < M ? (xv[j] - mu) * r : T(0);
+      g[k][j] = e < M ? dv[j] * act_d1(z[k][j], act) : T(0);
+      sg += g[k][j];
+      sgz += g[k][j] * z[k][j];
+    }
+  }
+  const T mg = bsum(sg, sh) / T(M);
+  const T mgz = bsum(sgz, sh) / T(M);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = (threadIdx.x + 256 * (int64_t)k) * W;
+    if (e >= M) continue;
+    T o[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) o[j] = r * (g[k][j] - mg - z[k][j] * mgz);
+    st<T, W>(dx + p * M + e, o);
+  }
+}
+
+template <typename T, int V, int W>
+__global__ __launch_bounds__(256) void in_bwd2_blk(const T* __restrict__ v,
+                                                   const T* __restrict__ dy,
+                                                   const T* __restrict__ x,
+                                                   const T* __restrict__ mean,
+                                                   const T* __restrict__ rstd,
+                                                   T* __restrict__ gdy, T* __restrict__ gx,
+                                                   int64_t M, int act) {
+  __shared__ T sh[4];
+  const int64_t p = blockIdx.x;
+  const T mu = mean[p], r = rstd[p];
+  T z[V][W], d[V][W], vv[V][W];  // z, dy, v
+  T sv = T(0), svz = T(0), sg = T(0), sgz = T(0), sgv = T(0);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = (threadIdx.x + 256 * (int64_t)k) * W;
+    T xv[W];
+    if (e < M) {
+      ld<T, W>(x + p * M + e, xv);
+      ld<T, W>(dy + p * M + e, d[k]);
+      ld<T, W>(v + p * M + e, vv[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < W; ++j) xv[j] = d[k][j] = vv[k][j] = T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      z[k][j] = e < M ? (xv[j] - mu) * r : T(0);
+      const T gj = d[k][j] * act_d1(z[k][j], act);
+      sv += vv[k][j];
+      svz += vv[k][j] * z[k][j];
+      sg += gj;
+      sgz += gj * z[k][j];
+      sgv += gj * vv[k][j];
+    }
+  }
+  const T inv = T(1) / T(M);
+  const T mv = bsum(sv, sh) * inv, mvz = bsum(svz, sh) * inv, mg = bsum(sg, sh) * inv;
+  const T mgz = bsum(sgz, sh) * inv, mgv = bsum(sgv, sh) * inv;
+  const T S = mgv - mg * mv - mgz * mvz;
+  T mq = T(0), mqz = T(0);
+  if (gx) {
+    T sq = T(0), sqz = T(0);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if ((threadIdx.x + 256 * (int64_t)k) * W >= M) continue;
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T d1 = act_d1(z[k][j], act);
+        const T gj = d[k][j] * d1;
+        const T w = r * (vv[k][j] - mv - z[k][j] * mvz);
+        const T q = d[k][j] * act_d2(z[k][j], act) * w - r * (gj * mvz + vv[k][j] * mgz);
+        sq += q;
+        sqz += q * z[k][j];
+      }
+    }
+    mq = bsum(sq, sh) * inv;
+    mqz = bsum(sqz, sh) * inv;
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = (threadIdx.x + 256 * (int64_t)k) * W;
+    if (e >= M) continue;
+    T o1[W], o2[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T d1 = act_d1(z[k][j], act);
+      const T w = r * (vv[k][j] - mv - z[k][j] * mvz);
+      o1[j] = w * d1;
+      const T gj = d[k][j] * d1;
+      const T q = d[k][j] * act_d2(z[k][j], act) * w - r * (gj * mvz + vv[k][j] * mgz);
+      o2[j] = r * (q - mq - z[k][j] * mqz) - r * r * z[k][j] * S;
+    }
+    if (gdy) st<T, W>(gdy + p * M + e, o1);
+    if (gx) st<T, W>(gx + p * M + e, o2);
+  }
+}
+
 unsigned blocks_for(int64_t planes) { return (unsigned)bpk::ceil_div(planes, kWaves); }
+
+// runs per thread of the workgroup-per-plane kernels (0: the one-wave kernels); W = 4 when
+// the planes are whole 16-byte vectors
+int blk_runs(int64_t M, int W) {
+  if (M <= 256 || M > 256 * 16) return 0;
+  const int64_t v = bpk::ceil_div(M, 256 * (int64_t)W);
+  return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : 16;
+}
+template <typename T>
+int blk_w(const void* a, const void* b, const void* c, int64_t M) {
+  const auto al = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  return (sizeof(T) == 4 && M % 4 == 0 && al(a) && al(b) && al(c)) ? 4 : 1;
+}
+#define IN_BLK_V(KERNEL, T, W, ...)                                                              \
+  switch (blk_runs(M, W)) {                                                                      \
+    case 1: hipLaunchKernelGGL((KERNEL<T, 1, W>), dim3((unsigned)planes), dim3(256), 0, st, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL((KERNEL<T, 2, W>), dim3((unsigned)planes), dim3(256), 0, st, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL((KERNEL<T, 4, W>), dim3((unsigned)planes), dim3(256), 0, st, __VA_ARGS__); break; \
+    case 8: hipLaunchKernelGGL((KERNEL<T, 8, W>), dim3((unsigned)planes), dim3(256), 0, st, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL((KERNEL<T, 16, W>), dim3((unsigned)planes), dim3(256), 0, st, __VA_ARGS__); break; \
+  }
+#define IN_BLK(KERNEL, T, WSEL, ...)                                                             \
+  if constexpr (sizeof(T) == 4) {                                                                \
+    if ((WSEL) == 4) {                                                                           \
+      IN_BLK_V(KERNEL, T, 4, __VA_ARGS__)                                                        \
+    } else {                                                                                     \
+      IN_BLK_V(KERNEL, T, 1, __VA_ARGS__)                                                        \
+    }                                                                                            \
+  } else {                                                                                       \
+    IN_BLK_V(KERNEL, T, 1, __VA_ARGS__)                                                          \
+  }
 
 #define IN_CHECK(what)                                                                   \
   BPK_REQUIRE(planes >= 0 && M > 0, "%s: bad geometry planes=%lld M=%lld", what,         \
@@ -180,8 +410,13 @@ int fwd_impl(const T* x, T* y, T* mean, T* rstd, int64_t planes, int64_t M, doub
   IN_CHECK("instance_norm_act_fwd");
   BPK_REQUIRE(x && y && mean && rstd, "instance_norm_act_fwd: null pointer");
   if (planes == 0) return BPK_OK;
-  hipLaunchKernelGGL(in_fwd<T>, dim3(blocks_for(planes)), dim3(256), 0, bpk::as_stream(stream),
-                     x, y, mean, rstd, planes, M, (T)eps, act);
+  hipStream_t st = bpk::as_stream(stream);
+  if (blk_runs(M, 1) && planes < (1ll << 31)) {
+    IN_BLK(in_fwd_blk, T, (blk_w<T>(x, y, nullptr, M)), x, y, mean, rstd, M, (T)eps, act)
+  } else {
+    hipLaunchKernelGGL(in_fwd<T>, dim3(blocks_for(planes)), dim3(256), 0, st, x, y, mean, rstd,
+                       planes, M, (T)eps, act);
+  }
   BPK_LAUNCH_CHECK("instance_norm_act_fwd");
   return BPK_OK;
 }
@@ -192,8 +427,14 @@ int bwd_impl(const T* dy, const T* x, const T* mean, const T* rstd, T* dx, int64
   IN_CHECK("instance_norm_act_bwd");
   BPK_REQUIRE(dy && x && mean && rstd && dx, "instance_norm_act_bwd: null pointer");
   if (planes == 0) return BPK_OK;
-  hipLaunchKernelGGL(in_bwd<T>, dim3(blocks_for(planes)), dim3(256), 0, bpk::as_stream(stream),
-                     dy, x, mean, rstd, dx, planes, M, act);
+  hipStream_t st = bpk::as_stream(stream);
+  if (blk_runs(M, 1) && planes < (1ll << 31)) {
+    const int w = blk_w<T>(dy, x, dx, M);
+    IN_BLK(in_bwd_blk, T, w, dy, x, mean, rstd, dx, M, act)
+  } else {
+    hipLaunchKernelGGL(in_bwd<T>, dim3(blocks_for(planes)), dim3(256), 0, st, dy, x, mean, rstd,
+                       dx, planes, M, act);
+  }
   BPK_LAUNCH_CHECK("instance_norm_act_bwd");
   return BPK_OK;
 }
@@ -204,8 +445,14 @@ int bwd2_impl(const T* v, const T* dy, const T* x, const T* mean, const T* rstd,
   IN_CHECK("instance_norm_act_bwd2");
   BPK_REQUIRE(v && dy && x && mean && rstd, "instance_norm_act_bwd2: null input pointer");
   if (planes == 0 || (!gdy && !gx)) return BPK_OK;
-  hipLaunchKernelGGL(in_bwd2<T>, dim3(blocks_for(planes)), dim3(256), 0, bpk::as_stream(stream),
-                     v, dy, x, mean, rstd, gdy, gx, planes, M, act);
+  hipStream_t st = bpk::as_stream(stream);
+  if (blk_runs(M, 1) && planes < (1ll << 31)) {
+    const int w = blk_w<T>(v, dy, x, M) == 4 && blk_w<T>(gdy, gx, nullptr, M) == 4 ? 4 : 1;
+    IN_BLK(in_bwd2_blk, T, w, v, dy, x, mean, rstd, gdy, gx, M, act)
+  } else {
+    hipLaunchKernelGGL(in_bwd2<T>, dim3(blocks_for(planes)), dim3(256), 0, st, v, dy, x, mean,
+                       rstd, gdy, gx, planes, M, act);
+  }
   BPK_LAUNCH_CHECK("instance_norm_act_bwd2");
   return BPK_OK;
 }

@@ -1247,7 +1247,8 @@ def test_conv_transpose2d_general_vs_torch(hip, cin, cout, k, s, p, op, groups):
 # ------------------------------------------------------------------ InstanceNorm + ELU
 
 @pytest.mark.parametrize("shape", [(4, 16, 64, 64), (4, 128, 4, 4), (3, 5, 2, 2), (2, 3, 7, 5),
-                                   (1, 1, 1, 1)])
+                                   (1, 1, 1, 1), (2, 8, 32, 32), (2, 4, 24, 20), (1, 3, 50, 60),
+                                   (1, 2, 90, 50)])
 def test_instance_norm_elu_matches_oracle(hip, shape):
     """csrc/instance_norm.hip forward / backward / double backward vs the float64 numpy
     restatement (pinned against torch's CPU composite in tests/test_oracle.py).  fp32:
@@ -1284,6 +1285,10 @@ def test_instance_norm_elu_gradgradcheck_and_third_order_refused(hip):
     f = lambda a: instance_norm_act(a[:, :, 1:])  # non-contiguous input, as a slice
     assert torch.autograd.gradcheck(f, (x,))
     assert torch.autograd.gradgradcheck(f, (x,))
+    # a plane of 300 elements: the workgroup-per-plane kernels (257..4096)
+    x3 = torch.randn(1, 2, 15, 20, dtype=torch.float64, device=hip, requires_grad=True)
+    assert torch.autograd.gradcheck(instance_norm_act, (x3,))
+    assert torch.autograd.gradgradcheck(instance_norm_act, (x3,))
     y = f(x)
     (dx,) = torch.autograd.grad(y.sum(), x, create_graph=True)
     (ddx,) = torch.autograd.grad((dx ** 2).sum(), x, create_graph=True)
