@@ -100,6 +100,9 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   // bias gradient (sum of dy over n, h, w): the cin-block-0 workgroups add up the gradient
   // tiles they load anyway; per-(split, cout) partials, reduced with dw
   const bool want_b = part_b != nullptr && cbk == 0;
+  // Cout % 64 != 0 (multiples of 16): the last cout block's waves past Cout skip their gradient
+  // loads, MFMAs and stores (wave-uniform); they still stage and transform the shared patch
+  const bool wvalid = __builtin_amdgcn_readfirstlane(cout0 + 16 * NB * (tid >> 6)) < g.Cout;
   float bsum[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) bsum[nb] = 0.f;
@@ -107,6 +110,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const int co = cout0 + 16 * NB * wave + 16 * nb + jj;
+      if (!wvalid) continue;
       if (want_b && kq == 0) part_b[(int64_t)split * g.Cout + co] = 0.f;
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
@@ -235,6 +239,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   auto load_g = [&](float2 (&dst)[NB][2][2]) {  // gradient tiles of chunk gcur, then advance
     const Strip s = gcur;
     advance(gcur);
+    if (!wvalid) return;  // past Cout: its MFMAs run on stale registers, never stored
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
@@ -345,6 +350,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   }
   if (j < nk) step(std::integral_constant<int, 0>{});
 
+  if (!wvalid) return;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int co = gco + 16 * nb;
@@ -435,7 +441,7 @@ WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
   g.strips_x = pair ? 1 : W / 16;
   g.strips_y = H / 2;
   g.cin_blocks = Cin / kCB;
-  g.cout_blocks = Cout / (kOB * nb);
+  g.cout_blocks = (Cout + kOB * nb - 1) / (kOB * nb);  // Cout % 16 == 0; the last may be partial
   g.chunks = (int64_t)(pair ? N / 2 : N) * g.strips_y * g.strips_x;
   // ~512 resident workgroups' worth (two per CU at NB = 1, one at NB = 2, twice the work
   // each): enough K-splits to fill the chip, no more (each split adds a [Cin][Cout][16]
@@ -450,7 +456,7 @@ WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
 }  // namespace
 
 extern "C" int bpk_conv3x3_wino_wgrad_supported(int N, int Cin, int Cout, int H, int W) {
-  return N > 0 && Cin > 0 && Cout > 0 && Cin % kCB == 0 && Cout % kOB == 0 && H % 2 == 0 &&
+  return N > 0 && Cin > 0 && Cout > 0 && Cin % kCB == 0 && Cout % 16 == 0 && H % 2 == 0 &&
          (W % 16 == 0 || wgrad_pair(N, W)) && (int64_t)H * W * kCB * 4 < (1LL << 31);
 }
 
@@ -480,7 +486,7 @@ extern "C" int bpk_conv3x3_wino_wgrad_pre_f32(const float* x, const float* pre, 
                                               int Cin, int Cout, int H, int W, void* stream) {
   BPK_REQUIRE(bpk_conv3x3_wino_wgrad_supported(N, Cin, Cout, H, W),
               "conv3x3_wino_wgrad: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin "
-              "%% 32, Cout %% 64, H %% 2, W %% 16 == 0 or W == 8 with N even)", N, Cin, Cout,
+              "%% 32, Cout %% 16, H %% 2, W %% 16 == 0 or W == 8 with N even)", N, Cin, Cout,
               H, W);
   BPK_REQUIRE(workspace != nullptr, "conv3x3_wino_wgrad: workspace is NULL");
   const WgradGeo g = make_geo(N, Cin, Cout, H, W);

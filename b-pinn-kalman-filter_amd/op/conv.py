@@ -654,7 +654,9 @@ def _wgrad_impl(x, gy, wshape, want_b):
     """(dw, db or None) without autograd: the Winograd weight gradient (+ bias) when the
     shape qualifies, MIOpen backward-weights otherwise."""
     if wgrad_supported(x, tuple(wshape)):
-        if (_small_img(x) and x.is_cuda and x.dtype == torch.float32
+        # small images, and couts past a 64-cout block (the Winograd kernel's idle waves),
+        # are timed against the implicit GEMM once per distinct call
+        if ((_small_img(x) or wshape[0] % 64) and x.is_cuda and x.dtype == torch.float32
                 and igemm_supported(x, tuple(wshape), 1, 1)):
             key = ("w3", tuple(x.shape), tuple(wshape))
             dw, db = _pick_any(key, [

@@ -427,7 +427,8 @@ int bpk_conv3x3_wino_up2_f32(const float* x, const float* U, const float* bias, 
  * gy [N, Cout, H, W].  Winograd F(2x2,3x3): per transform position a split-K GEMM
  * dU_pos = sum_tiles V_pos^T (A gy A^T)_pos, then dw = G^T dU G.  `workspace` holds the
  * split-K partial slabs (bpk_conv3x3_wino_wgrad_workspace_bytes, device memory).
- * supported(): Cin % 32 == 0, Cout % 64 == 0, H % 2 == 0, W % 16 == 0.  Deterministic. */
+ * supported(): Cin % 32 == 0, Cout % 16 == 0, H % 2 == 0, W % 16 == 0 (or W == 8, N even:
+ * two images per strip).  Deterministic. */
 int bpk_conv3x3_wino_wgrad_supported(int N, int Cin, int Cout, int H, int W);
 int64_t bpk_conv3x3_wino_wgrad_workspace_bytes(int N, int Cin, int Cout, int H, int W);
 int bpk_conv3x3_wino_wgrad_f32(const float* x, const float* gy, float* dw, float* workspace,

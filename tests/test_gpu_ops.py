@@ -354,7 +354,10 @@ def test_conv3x3_winograd_backward_and_filter_cache(hip, cin):
                                              (3, 96, 64, 10, 48), (2, 256, 128, 32, 32),
                                              (1, 32, 128, 2, 16), (4, 128, 256, 64, 64),
                                              (3, 64, 384, 18, 16), (128, 256, 256, 8, 8),
-                                             (2, 32, 64, 8, 8), (16, 512, 256, 8, 8)])
+                                             (2, 32, 64, 8, 8), (16, 512, 256, 8, 8),
+                                             (4, 128, 16, 64, 64), (2, 64, 32, 32, 32),
+                                             (3, 192, 96, 32, 32), (2, 64, 160, 16, 16),
+                                             (4, 32, 48, 8, 8)])
 def test_conv3x3_winograd_weight_gradient(hip, N, cin, cout, h, w):
     """Winograd split-K weight gradient vs a float64 direct computation (and MIOpen's fp32
     backward-weights held to the same bound): 2e-5 relative to max|ref|.  Shapes cover one

@@ -3,7 +3,7 @@
 # capture -- InstanceNorm / PINN / graph tests, PINN bench (B=64, per-rank B=8), kernel count.
 mkdir -p gpurun_out/r05l; export TMPDIR=/tmp
 O=gpurun_out/r05l
-timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_configs.py tests/test_gpu_pinn.py tests/test_gpu_graph.py -x -q --timeout 300 --timeout-method thread -k "instance_norm or pinn" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_configs.py tests/test_gpu_pinn.py tests/test_gpu_graph.py -x -q --timeout 300 --timeout-method thread -k "instance_norm or pinn or weight_gradient" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 400 python bench.py --no-cpu-baseline --ns-steps 0 --ncddpmpp-steps 0 --no-train --no-dps --cifar-steps 0 --steps 1 --warmup 1 > $O/bench.log 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 python tools/show_line.py $O/bench.log
