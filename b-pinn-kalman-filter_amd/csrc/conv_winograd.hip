@@ -50,12 +50,11 @@ constexpr int kOutRows = 2 * kTR, kOutCols = 2 * kTC;  // 8 x 16 pixels
 // its B operands for all positions with four 16-B loads)
 // Cout not a multiple of 64: U is laid out for CoutP = Cout rounded up to 64 couts, the
 // extra couts zero (the conv computes them and never stores them).
-__global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restrict__ w,
-                                                          float* __restrict__ U, int Cin,
-                                                          int Cout, int CoutP, int ft) {
+__device__ inline void wino_filter_range(const float* __restrict__ w, float* __restrict__ U,
+                                         int Cin, int Cout, int CoutP, int ft, int64_t first,
+                                         int64_t stride) {
   const int64_t total = (int64_t)Cin * CoutP;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = first; i < total; i += stride) {
     const int co = (int)(i % CoutP);
     const int ci = (int)(i / CoutP);
     if (co >= Cout) {
@@ -87,6 +86,24 @@ __global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restric
       u[4 * r + 3] = a2;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restrict__ w,
+                                                          float* __restrict__ U, int Cin,
+                                                          int Cout, int CoutP, int ft) {
+  wino_filter_range(w, U, Cin, Cout, CoutP, ft, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                    (int64_t)gridDim.x * blockDim.x);
+}
+
+// many filters in one launch (op.conv.FilterBatch: every 3x3 conv weight of a model, forward
+// and flipped, refreshed once per training step instead of one launch per conv call): job j =
+// jobs[6 j .. 6 j + 5] = (w, U, Cin, Cout, CoutP, ft), blockIdx.y = j
+__global__ __launch_bounds__(256) void wino_filter_batch_kernel(const int64_t* __restrict__ jobs) {
+  const int64_t* jb = jobs + 6 * (int64_t)blockIdx.y;
+  wino_filter_range(reinterpret_cast<const float*>(jb[0]), reinterpret_cast<float*>(jb[1]),
+                    (int)jb[2], (int)jb[3], (int)jb[4], (int)jb[5],
+                    (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                    (int64_t)gridDim.x * blockDim.x);
 }
 
 struct WinoGeo {
@@ -1196,6 +1213,17 @@ extern "C" int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Ci
 extern "C" int bpk_conv3x3_wino_filter_ft_f32(const float* weight, float* U, int Cin, int Cout,
                                               void* stream) {
   return wino_filter(weight, U, Cin, Cout, 1, stream);
+}
+
+extern "C" int bpk_conv3x3_wino_filter_batch_f32(const int64_t* jobs, int n, int max_elems,
+                                                 void* stream) {
+  BPK_REQUIRE(n >= 0 && n < 65536 && max_elems >= 0, "conv3x3_wino_filter_batch: bad job count");
+  if (n == 0 || max_elems == 0) return BPK_OK;
+  BPK_REQUIRE(jobs != nullptr, "conv3x3_wino_filter_batch: jobs is NULL");
+  const dim3 grid((unsigned)std::min<int64_t>(bpk::ceil_div(max_elems, 256), 64), (unsigned)n);
+  hipLaunchKernelGGL(wino_filter_batch_kernel, grid, dim3(256), 0, bpk::as_stream(stream), jobs);
+  BPK_LAUNCH_CHECK("conv3x3_wino_filter_batch");
+  return BPK_OK;
 }
 
 // The PAIR form of the 16-cin kernel (8-pixel-wide images, two per region): one source, no

@@ -148,10 +148,14 @@ def get_step_fn(sde, train, optimize_fn=None, reduce_mean=False, continuous=True
     def step_fn(state, batch):
         model = state["model"]
         if train:
+            from op import conv as conv_op
             optimizer = state["optimizer"]
             optimizer.zero_grad(set_to_none=True)
-            loss = loss_fn(model, batch)
-            loss.backward()
+            # every Winograd filter of the step transformed in one launch (the weights change
+            # after each optimizer step)
+            with conv_op.batched_filters(model, enabled=batch.is_cuda):
+                loss = loss_fn(model, batch)
+                loss.backward()
             optimize_fn(optimizer, model.parameters(), step=state["step"])
             state["step"] += 1
             state["ema"].update(model.parameters())
@@ -360,8 +364,10 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
                 bucketer[0] = GradBucketer(model.parameters(), ctx)
             opt_flow.zero_grad()
             opt_pres.zero_grad()
-            loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
-            loss.backward()
+            from op import conv as conv_op
+            with conv_op.batched_filters(model, enabled=batch[0].is_cuda):
+                loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
+                loss.backward()
             # the values only: a returned loss that still carries the spent autograd graph
             # keeps the parameters' AccumulateGrad nodes alive, and a hipGraph captured later
             # on another stream (get_pinn_step_fn(graph=True)) then accumulates through them
@@ -454,8 +460,9 @@ class _PinnGraphStep:
                 for _ in range(2):  # kernel choices, allocator, lazy state: off the capture
                     for p in params:
                         p.grad = None
-                    loss, _pl, _dl = self.loss_fn(model, sop, self.static, self.noise)
-                    loss.backward(inputs=params)
+                    with conv_op.batched_filters(model):
+                        loss, _pl, _dl = self.loss_fn(model, sop, self.static, self.noise)
+                        loss.backward(inputs=params)
             # nothing of the warm-up may be freed while the capture runs: a block released
             # mid-capture went back to the general pool and could be handed to the graph, which
             # then shared it with eager allocations after the capture (replays read garbage a
@@ -477,8 +484,11 @@ class _PinnGraphStep:
             # inputs' .grad (unused; the eager step accumulates them as the reference does)
             # is neither computed nor accumulated by the replays
             with torch.cuda.graph(g, stream=s):
-                loss, pl, dl = self.loss_fn(model, sop, self.static, self.noise)
-                loss.backward(inputs=params)
+                # one recorded launch transforms every Winograd filter of the step (the job
+                # table and the transform buffers were built by the warm-up)
+                with conv_op.batched_filters(model):
+                    loss, pl, dl = self.loss_fn(model, sop, self.static, self.noise)
+                    loss.backward(inputs=params)
                 live = [(gb, p.grad) for gb, p in zip(gbufs, params) if p.grad is not None]
                 torch._foreach_copy_([a for a, _ in live], [b for _, b in live])
                 obuf[:3].copy_(torch.stack([loss.detach(), pl.detach(), dl.detach()]))

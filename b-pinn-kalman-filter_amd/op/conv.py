@@ -93,10 +93,100 @@ def refresh_filters(registry: list):
             registry[i] = (weight, U, ft, weight._version)
 
 
+_FILTER_BATCH = None  # {(weight data_ptr, ft): (shape, U)} while a FilterBatch is active
+
+
+class FilterBatch:
+    """The Winograd filter transforms of every 3x3 / stride-1 / pad-1 conv weight of a module
+    (forward and flipped), in static buffers refreshed by ONE launch
+    (bpk_conv3x3_wino_filter_batch_f32) instead of one per conv call: a training step's
+    weights change after every optimizer step, and the PINN step's graph recorded ~250
+    transform launches.  `refresh()` transforms the current weights (capturable: the job
+    table is device memory built once); inside `active()`, filter_transform returns these
+    buffers -- the weights must not change in place within the block."""
+
+    def __init__(self, module):
+        jobs, self.map, self.params = [], {}, []
+        dev = None
+        for m in module.modules():
+            if not (isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)
+                    and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1)
+                    and m.groups == 1):
+                continue
+            w = m.weight
+            if not (w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()):
+                continue
+            dev = w.device
+            self.params.append(w)
+            for ft in (False, True):
+                Cout, Cin = (w.shape[1], w.shape[0]) if ft else (w.shape[0], w.shape[1])
+                key = (w.data_ptr(), ft)
+                if Cin % 8 or Cout % 16 or key in self.map:
+                    continue  # not a Winograd filter shape
+                CoutP = lib.bpk_conv3x3_wino_filter_bytes(Cin, Cout) // (16 * 4 * Cin)
+                U = torch.empty((Cin, CoutP, 16), dtype=torch.float32, device=w.device)
+                # keyed by storage (the conv paths pass detached views of the parameter)
+                self.map[key] = (tuple(w.shape), U)
+                jobs.append([w.data_ptr(), U.data_ptr(), Cin, Cout, CoutP, int(ft)])
+        self.n = len(jobs)
+        self.max_elems = max((j[2] * j[4] for j in jobs), default=0)
+        self.jobs = torch.tensor(jobs, dtype=torch.int64).to(dev) if jobs else None
+        self.ptrs = [w.data_ptr() for w in self.params]
+
+    def valid_for(self, module) -> bool:
+        """the recorded weights still live where the job table points (a weight replaced by
+        another tensor is simply not found by filter_transform: per-call transforms)"""
+        return all(w.data_ptr() == p for w, p in zip(self.params, self.ptrs))
+
+    def refresh(self):
+        if self.n:
+            check(lib.bpk_conv3x3_wino_filter_batch_f32(
+                self.jobs.data_ptr(), self.n, self.max_elems, stream_ptr(self.jobs.device)),
+                "conv3x3 filter batch")
+
+    @contextlib.contextmanager
+    def active(self):
+        global _FILTER_BATCH
+        prev, _FILTER_BATCH = _FILTER_BATCH, self.map
+        try:
+            yield self
+        finally:
+            _FILTER_BATCH = prev
+
+
+def filter_batch_for(module) -> "FilterBatch":
+    """The FilterBatch of `module`, built on first use and kept on it (rebuilt when a weight
+    tensor was replaced)."""
+    fb = getattr(module, "_bpk_filter_batch", None)
+    if fb is None or not fb.valid_for(module):
+        fb = FilterBatch(module)
+        object.__setattr__(module, "_bpk_filter_batch", fb)
+    return fb
+
+
+@contextlib.contextmanager
+def batched_filters(module, enabled=True):
+    """refresh() the module's FilterBatch and make it active for the block (a no-op when
+    disabled or the module has no HIP 3x3 conv)."""
+    if not enabled:
+        yield None
+        return
+    fb = filter_batch_for(module)
+    fb.refresh()
+    with fb.active():
+        yield fb
+
+
 def filter_transform(weight, ft=False):
     """U [Cin, CoutP, 16] (CoutP = Cout rounded up to 64), cached on `weight` while its
     version counter is unchanged.  ft=True: the transform of _flip_t(weight) (the filter of
-    the backward-data conv, Cin = weight.shape[0]), read from `weight` in place."""
+    the backward-data conv, Cin = weight.shape[0]), read from `weight` in place.  Inside an
+    active FilterBatch: its static buffer."""
+    fbm = _FILTER_BATCH
+    if fbm is not None and weight.is_contiguous():
+        e = fbm.get((weight.data_ptr(), bool(ft)))
+        if e is not None and e[0] == tuple(weight.shape):
+            return e[1]
     attr = "_bpk_wino_u_ft" if ft else "_bpk_wino_u"
     # under hipGraph capture the transform is recorded (and the cache left alone): replays
     # run after optimizer steps have rewritten the weight in place, so a cached U baked into

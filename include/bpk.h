@@ -372,6 +372,10 @@ int bpk_conv3x3_wino_filter_f32(const float* weight, float* U, int Cin, int Cout
  * backward-data of nn.Conv2d) -- read in place, no flipped copy of w. */
 int bpk_conv3x3_wino_filter_ft_f32(const float* weight, float* U, int Cin, int Cout,
                                    void* stream);
+/* Many filter transforms in one launch: jobs (device memory) = n records of six int64
+ * (weight ptr, U ptr, Cin, Cout, CoutP, ft) with the meaning of the two entries above (ft = 1:
+ * the flipped, transposed filter); max_elems = the largest Cin * CoutP among them. */
+int bpk_conv3x3_wino_filter_batch_f32(const int64_t* jobs, int n, int max_elems, void* stream);
 int bpk_conv3x3_wino_supported(int N, int Cin, int Cout, int H, int W);
 /* The 16-cin kernel's pair form, used by bpk_conv3x3_wino_ex_f32 / _splitk_f32 when W == 8 (and
  * the W % 16 form does not apply): two 8 x 8 images side by side per 8 x 16 region -- N even,

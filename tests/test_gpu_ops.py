@@ -1653,3 +1653,40 @@ def test_attention_block_training_on_native_gemm(hip, monkeypatch):
     ref = run()
     for a, r in zip(got, ref):
         assert (a - r).abs().max().item() <= 1e-5 * r.abs().max().item()
+
+
+def test_filter_batch_matches_per_weight_transforms(hip):
+    """op.conv.FilterBatch: one launch transforms every 3x3 conv weight of a module (forward
+    and flipped) bit-identically to the per-weight entries; inside active() filter_transform
+    returns those buffers; refresh() after an in-place weight update re-transforms; convs
+    through the batch == convs without it."""
+    import torch.nn as nn
+    from op import conv as conv_op
+    torch.manual_seed(3)
+    m = nn.Sequential(nn.Conv2d(16, 32, 3, padding=1), nn.Conv2d(32, 48, 3, padding=1),
+                      nn.Conv2d(48, 16, 1), nn.Conv2d(49, 64, 3, padding=1),
+                      nn.Conv2d(64, 64, 3, stride=2, padding=1)).to(hip)
+    fb = conv_op.FilterBatch(m)
+    assert fb.n == 4  # 16->32 and 32->48, forward + flipped; not 49->64 (49 channels), not 1x1 / stride 2
+    fb.refresh()
+    convs = [c for c in m if isinstance(c, nn.Conv2d)]
+    for c in convs:
+        for ft in (False, True):
+            e = fb.map.get((c.weight.data_ptr(), ft))
+            if e is not None:  # per-weight entry (outside the batch)
+                assert torch.equal(e[1], conv_op.filter_transform(c.weight, ft)), (e[0], ft)
+    with fb.active():
+        assert conv_op.filter_transform(m[0].weight) is fb.map[(m[0].weight.data_ptr(), False)][1]
+        # the conv paths pass detached views of the parameter
+        assert conv_op.filter_transform(m[1].weight.detach(), True) is \
+            fb.map[(m[1].weight.data_ptr(), True)][1]
+    with torch.no_grad():
+        m[0].weight.mul_(1.5)
+    fb.refresh()
+    U0 = fb.map[(m[0].weight.data_ptr(), False)][1]
+    assert torch.equal(U0, conv_op.filter_transform(m[0].weight))
+    x = torch.randn(2, 16, 16, 16, device=hip)
+    with conv_op.batched_filters(m):
+        y1 = conv_op.conv3x3(x, m[0].weight, m[0].bias)
+    y0 = conv_op.conv3x3(x, m[0].weight, m[0].bias)
+    assert torch.equal(y1, y0)
