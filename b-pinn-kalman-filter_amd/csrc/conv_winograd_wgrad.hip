@@ -32,7 +32,7 @@ constexpr int kCB = 32;              // cin per workgroup
 constexpr int kOB = 64;              // cout per workgroup per N-block of the waves (NB)
 constexpr int kT = 8;                // tiles per K-chunk (1 tile row x 8 tile cols)
 constexpr int kXR = 4;               // input patch rows
-constexpr int kRec = 20;             // LDS stride of one 16-position record
+constexpr int kRec = 24;             // LDS stride of one 16-position record
 
 struct WgradGeo {
   int N, Cin, Cout, H, W;
@@ -50,11 +50,12 @@ struct WgradGeo {
 //   * chunk c's input patch is loaded at step c-3 (2 x 16 B + one halo word per thread and
 //     (cin, row)), stored to LDS at step c-2, transformed into V records at step c-1 while
 //     the MFMAs of the previous chunk run (double-buffered patch and V), one barrier per chunk;
-//   * V records of tile t sit at t * 644 + cin * 20 floats: conflict-free 16-B writes,
-//     2-way 16-B operand reads.
+//   * V records of tile t sit at t * 772 + cin * 24 floats: conflict-free 16-B writes and
+//     16-B operand reads (a 20-float record made the operand reads 2-way: 45% of LDS cycles
+//     were bank-conflict cycles, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, round 5).
 constexpr int kXRS = 24;                     // LDS patch row: halo at 3, interior at 4..19, halo 20
 constexpr int kXCS = kXR * kXRS + 16;        // per-cin stride (2-way transform reads)
-constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records (644)
+constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records (772)
 
 // NB = 16-cout blocks per wave: NB = 1 -> 64 couts per workgroup, two workgroups per CU (the
 // form that runs).  NB = 2 (128 couts per workgroup, 256 accumulators per lane, one workgroup
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ part,
     float* __restrict__ part_b, WgradGeo g, int xcd_remap, const float2* __restrict__ pre) {
   __shared__ __attribute__((aligned(16))) float s_x[2][kCB * kXCS];   // 2 x 14.3 KB
-  __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 20.6 KB
+  __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 24.7 KB
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;

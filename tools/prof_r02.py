@@ -4,6 +4,7 @@
    mix       the NCSN++ PRE-conv mix of bench.conv_roofline, once (B = 64)
    ns        3 ns_step full steps, B = 256 x 192^2
    upfirdn   the four bench upfirdn2d shapes, 3 launches each (B = 64)
+   wgrad_one the Winograd weight gradient 128->128 @128^2 at B=16, 3 launches
 Kernel names / grid sizes in the counter CSV identify the dispatches."""
 import os
 import sys
@@ -40,6 +41,12 @@ if mode in ("wino_one", "mix"):
                 conv3x3(x, w, b, skip=skip, div=2 ** 0.5, pre=pre, stats=True)
         torch.cuda.synchronize()
         del x, skip
+elif mode == "wgrad_one":
+    from op.conv import conv3x3_wgrad_raw
+    x = torch.randn(16, 128, 128, 128, device=dev, generator=g)
+    gy = torch.randn(16, 128, 128, 128, device=dev, generator=g)
+    for _ in range(3):
+        conv3x3_wgrad_raw(x, gy, (128, 128, 3, 3))
 elif mode == "ns":
     from op import ns_step
     f, v, p = (torch.tensor(a, device=dev) for a in bench._ns_fields(np.random.default_rng(0), 256, 192))
