@@ -116,7 +116,11 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
   constexpr int NBM = WTM / 16, NBN = WTN / 16;  // MFMA blocks per wave
   constexpr int NLA = TM / 16, NLB = TN / 16;    // A / B elements each thread stages per chunk
   constexpr int kAP = BK + 1;                    // LDS pitch of the A tile [m][k]
-  constexpr int kBP = TN + 16;  // LDS pitch of the B tile [k][n]: MFMA reads conflict-free
+  // LDS pitch of the B tile [k][n]: TN + 16 makes the MFMA operand reads conflict-free; the
+  // weight gradient stores the tile k-fastest (16 lanes = 16 k), where that pitch put 8 lanes
+  // on one bank -- TN + 18 (= 18 mod 32: 16 distinct even banks per half-wave) leaves its
+  // stores conflict-free and 2 of 32 lanes of each operand read 2-way
+  constexpr int kBP = TN + (MODE == 2 ? 18 : 16);
   __shared__ float s_a[2][TM * kAP];
   __shared__ float s_b[2][BK * kBP];
 
@@ -141,6 +145,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
   bool pvalid = false;
   int bc[NLB], br[NLB], bs[NLB];  // MODE 2: the (c, r, s) of this thread's columns
   bool bcol_ok[NLB], bcol_one[NLB];
+  // MODE 2 with a compile-time filter (<= 16 taps): column j's element offset from the tap
+  // origin (c HW + r W + s) and its bit in the chunk's valid-tap mask (bit 16: the bias column,
+  // 0: past the last column), so a gathered element costs a mask test and an add
+  constexpr bool kMask2 = MODE == 2 && KH_ > 0 && KH_ * KW_ <= 16;
+  int boff[NLB];
+  unsigned bbit[NLB];
   if (MODE != 2) {
     const int p = n0 + bn;
     pvalid = p < g.Ncol;
@@ -175,6 +185,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
       bc[j] = c;
       br[j] = r;
       bs[j] = s;
+      if (kMask2) {
+        boff[j] = c * g.HW + r * g.W + s;
+        bbit[j] = !bcol_ok[j] ? 0u : bcol_one[j] ? (1u << 16) : (1u << (r * KW_ + s));
+      }
     }
   }
 
@@ -273,6 +287,29 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
               v = B0[bbase + ((int64_t)c * g.Ho + oy) * g.Wo + ox];
           }
         }
+        rb[j] = v;
+      }
+    } else if (kMask2) {
+      const int k = kb + bk;  // pixel
+      const bool kv = k < g.K;
+      const int kk = kv ? k : 0;
+      const int n = fdiv(kk, g.f_howo), pix = kk - n * g.HoWo;
+      const int oy = fdiv(pix, g.f_wo), ox = pix - oy * g.Wo;
+      const int iy0 = oy * g.sh - g.ph, ix0 = ox * g.sw - g.pw;
+      unsigned rm = 0, sm = 0, vm = 0;
+#pragma unroll
+      for (int r = 0; r < KH_; ++r) rm |= (unsigned)((unsigned)(iy0 + r) < (unsigned)g.H) << r;
+#pragma unroll
+      for (int q = 0; q < KW_; ++q) sm |= (unsigned)((unsigned)(ix0 + q) < (unsigned)g.W) << q;
+#pragma unroll
+      for (int r = 0; r < KH_; ++r) vm |= ((rm >> r) & 1u) ? sm << (r * KW_) : 0u;
+      vm = kv ? vm | (1u << 16) : 0u;
+      // the tap origin's element offset; negative only where the mask excludes the tap
+      const int pb = n * g.Cin * g.HW + iy0 * g.W + ix0;
+#pragma unroll
+      for (int j = 0; j < NLB; ++j) {
+        float v = 0.f;
+        if (vm & bbit[j]) v = bcol_one[j] ? 1.f : B0[(unsigned)(pb + boff[j])];
         rb[j] = v;
       }
     } else {

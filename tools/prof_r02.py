@@ -5,6 +5,8 @@
    ns        3 ns_step full steps, B = 256 x 192^2
    upfirdn   the four bench upfirdn2d shapes, 3 launches each (B = 64)
    wgrad_one the Winograd weight gradient 128->128 @128^2 at B=16, 3 launches
+   igemm_set the PINN step's heaviest implicit-GEMM shapes (B = 64), 3 launches each:
+             fwd 34->128 @32^2, dgrad 128->49 and 128->34 @32^2, wgrad 128->16 @64^2 (bias)
 Kernel names / grid sizes in the counter CSV identify the dispatches."""
 import os
 import sys
@@ -47,6 +49,21 @@ elif mode == "wgrad_one":
     gy = torch.randn(16, 128, 128, 128, device=dev, generator=g)
     for _ in range(3):
         conv3x3_wgrad_raw(x, gy, (128, 128, 3, 3))
+elif mode == "igemm_set":
+    from op.conv import conv2d_igemm_raw, conv2d_input_igemm_raw, conv2d_weight_igemm_raw
+    x = torch.randn(64, 34, 32, 32, device=dev, generator=g)
+    w = torch.randn(128, 34, 3, 3, device=dev, generator=g)
+    for _ in range(3):
+        conv2d_igemm_raw(x, w, None, 1, 1)
+    gy = torch.randn(64, 128, 32, 32, device=dev, generator=g)
+    for c in (49, 34):
+        w = torch.randn(128, c, 3, 3, device=dev, generator=g)
+        for _ in range(3):
+            conv2d_input_igemm_raw((64, c, 32, 32), w, gy, 1, 1)
+    x = torch.randn(64, 128, 64, 64, device=dev, generator=g)
+    gy = torch.randn(64, 16, 64, 64, device=dev, generator=g)
+    for _ in range(3):
+        conv2d_weight_igemm_raw(x, (16, 128, 3, 3), gy, 1, 1, True)
 elif mode == "ns":
     from op import ns_step
     f, v, p = (torch.tensor(a, device=dev) for a in bench._ns_fields(np.random.default_rng(0), 256, 192))
