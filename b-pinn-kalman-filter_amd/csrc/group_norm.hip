@@ -528,6 +528,64 @@ __global__ __launch_bounds__(256) void gn_bwd_apply2(
   }
 }
 
+// The reductions behind the backward's parameter gradients, one launch: d bias_nc[n, c] =
+// sum over the plane of dx (the per-(n, c) bias added before the norm: the time-embedding
+// Dense_0 output), dgamma[c] / dbeta[c] = sum over n of the kernels' per-(n, c) partials.
+// Blocks [0, rows): one (n, c) plane each; the rest: 64 channels each.
+// Fixed summation orders (deterministic); replaced three aten reductions per backward.
+__global__ __launch_bounds__(256) void gn_param_grads_kernel(
+    const float* __restrict__ dx, const float* __restrict__ dg_nc, const float* __restrict__ db_nc,
+    float* __restrict__ d_bnc, float* __restrict__ dgamma, float* __restrict__ dbeta, int N,
+    int C, int HW, int rows) {
+  __shared__ float sbuf[256 / kWave];
+  if ((int)blockIdx.x < rows) {
+    const float* p = dx + (int64_t)blockIdx.x * HW;
+    float v = 0.f;
+    if ((HW & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+      const float4* p4 = reinterpret_cast<const float4*>(p);
+      for (int i = threadIdx.x; i < HW / 4; i += 256) {
+        const float4 q = p4[i];
+        v += (q.x + q.y) + (q.z + q.w);
+      }
+    } else {
+      for (int i = threadIdx.x; i < HW; i += 256) v += p[i];
+    }
+    v = block_sum<256>(v, sbuf);
+    if (threadIdx.x == 0) d_bnc[blockIdx.x] = v;
+    return;
+  }
+  // 64 channels per block (one per lane); wave w adds n in [w nq, (w + 1) nq) in order, eight
+  // loads in flight at a time (a serial chain of N dependent loads took ~N load latencies),
+  // then the four wave partials in wave order
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = ((int)blockIdx.x - rows) * 64 + lane;
+  const int nq = (N + 3) / 4, n0 = w * nq, n1 = min(N, n0 + nq);
+  float sg = 0.f, sb = 0.f;
+  if (c < C) {
+    for (int n = n0; n < n1; n += 8) {
+      float tg[8], tb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool in = n + u < n1;
+        tg[u] = dgamma && in ? dg_nc[(int64_t)(n + u) * C + c] : 0.f;
+        tb[u] = dbeta && in ? db_nc[(int64_t)(n + u) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sg += tg[u];
+        sb += tb[u];
+      }
+    }
+  }
+  red[0][w][lane] = sg;
+  red[1][w][lane] = sb;
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+  if (dgamma) dgamma[c] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
+  if (dbeta) dbeta[c] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
+}
+
 // ---------------------------------------------------------------- dispatch
 
 constexpr int kSplitChunk = 256 * 16 * 4;  // floats per split-path chunk (W = 4)
@@ -703,6 +761,24 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
                        act);
   }
   BPK_LAUNCH_CHECK("group_norm_bwd_apply");
+  return BPK_OK;
+}
+
+extern "C" int bpk_group_norm_param_grads_f32(const float* dx, const float* dgamma_nc,
+                                              const float* dbeta_nc, float* d_bias_nc,
+                                              float* dgamma, float* dbeta, int N, int C,
+                                              int64_t HW, void* stream) {
+  BPK_REQUIRE(N > 0 && C > 0 && HW > 0 && HW < (1ll << 31), "group_norm_param_grads: bad shape");
+  BPK_REQUIRE(!d_bias_nc || dx, "group_norm_param_grads: d_bias_nc needs dx");
+  BPK_REQUIRE(!dgamma || dgamma_nc, "group_norm_param_grads: dgamma needs dgamma_nc");
+  BPK_REQUIRE(!dbeta || dbeta_nc, "group_norm_param_grads: dbeta needs dbeta_nc");
+  const int rows = d_bias_nc ? N * C : 0;
+  const int cols = (dgamma || dbeta) ? (int)bpk::ceil_div(C, 64) : 0;
+  if (rows + cols == 0) return BPK_OK;
+  hipLaunchKernelGGL(gn_param_grads_kernel, dim3(rows + cols), dim3(256), 0,
+                     bpk::as_stream(stream), dx, dgamma_nc, dbeta_nc, d_bias_nc, dgamma, dbeta, N,
+                     C, (int)HW, rows);
+  BPK_LAUNCH_CHECK("group_norm_param_grads");
   return BPK_OK;
 }
 

@@ -79,9 +79,20 @@ def group_norm_act_backward(dy, x, bnc, weight, bias, mean, rstd, G, act, want_b
         dx.data_ptr(), dg.data_ptr() if dg is not None else None,
         db.data_ptr() if db is not None else None, ws.data_ptr() if ws is not None else None,
         N, C, HW, G, act, stream_ptr(x.device)), "group_norm_act_bwd")
-    d_bnc = dx.reshape(N, C, -1).sum(-1) if (bnc is not None and want_bnc) else None
-    dw = dg.sum(0) if dg is not None and want_w else None
-    dbeta = db.sum(0) if db is not None and want_b else None
+    # the three reductions in one launch (bpk_group_norm_param_grads_f32)
+    d_bnc = (torch.empty((N, C), device=x.device, dtype=torch.float32)
+             if (bnc is not None and want_bnc) else None)
+    dw = torch.empty(C, device=x.device, dtype=torch.float32) if dg is not None and want_w else None
+    dbeta = (torch.empty(C, device=x.device, dtype=torch.float32)
+             if db is not None and want_b else None)
+    if d_bnc is not None or dw is not None or dbeta is not None:
+        check(lib.bpk_group_norm_param_grads_f32(
+            dx.data_ptr(), dg.data_ptr() if dg is not None else None,
+            db.data_ptr() if db is not None else None,
+            d_bnc.data_ptr() if d_bnc is not None else None,
+            dw.data_ptr() if dw is not None else None,
+            dbeta.data_ptr() if dbeta is not None else None, N, C, HW, stream_ptr(x.device)),
+            "group_norm_param_grads")
     return dx, d_bnc, dw, dbeta
 
 

@@ -268,6 +268,12 @@ int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,
                            void* workspace, int N, int C, int64_t HW, int G, int act,
                            void* stream);
+/* The parameter gradients behind that backward in one launch (NULL outputs skipped):
+ * d_bias_nc [N, C] = sum over the plane of dx [N, C, HW]; dgamma / dbeta [C] = sum over n of
+ * its dgamma_nc / dbeta_nc [N, C].  Fixed summation order. */
+int bpk_group_norm_param_grads_f32(const float* dx, const float* dgamma_nc, const float* dbeta_nc,
+                                   float* d_bias_nc, float* dgamma, float* dbeta, int N, int C,
+                                   int64_t HW, void* stream);
 
 /* out[n,c,:] = (x + (h + bias[c])) / div -- the skip_rescale residual of the
  * BigGAN / DDPM++ blocks with Conv_1's bias folded in (models/layerspp.py:266-274,
