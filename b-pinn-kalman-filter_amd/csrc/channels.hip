@@ -1,0 +1,59 @@
+// Flow-component swap + scale of FlowNet's `project` (reference models/flownet.py:8-25):
+// out[n, 0] = u[n, 1] / c0, out[n, 1] = u[n, 0] / c1 for a two-channel flow u [N, 2, P].
+// The map is linear and its adjoint is the same map with c0 and c1 exchanged, so every
+// derivative order of the PINN residual (pinn_kalman/pinn.py:72-111) runs this one kernel
+// (op.channels.swap_scale) -- aten needed two divisions into slices of an empty output per
+// call.  Division by a scalar as aten performs it -- multiplication by the fp32 reciprocal
+// 1.f / c -- so the results are bit-identical.
+#include "bpk_common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace {
+
+template <int V>
+__global__ __launch_bounds__(256) void swap_scale_kernel(const float* __restrict__ u,
+                                                         float* __restrict__ out, int64_t units,
+                                                         int64_t pv, float c0, float c1) {
+  const float r0 = 1.f / c0, r1 = 1.f / c1;
+  using vec = typename std::conditional<V == 4, float4, float>::type;
+  const vec* uv = reinterpret_cast<const vec*>(u);
+  vec* ov = reinterpret_cast<vec*>(out);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < units;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t n = i / pv, p = i - n * pv;
+    const int64_t a = 2 * n * pv + p, b = a + pv;  // channel 0 / channel 1 element
+    const vec x0 = uv[a], x1 = uv[b];
+    if constexpr (V == 4) {
+      ov[a] = make_float4(x1.x * r0, x1.y * r0, x1.z * r0, x1.w * r0);
+      ov[b] = make_float4(x0.x * r1, x0.y * r1, x0.z * r1, x0.w * r1);
+    } else {
+      ov[a] = x1 * r0;
+      ov[b] = x0 * r1;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c0,
+                                  float c1, void* stream) {
+  BPK_REQUIRE(N >= 0 && P >= 0, "swap_scale: bad shape N=%lld P=%lld", (long long)N,
+              (long long)P);
+  BPK_REQUIRE(u && out && u != out, "swap_scale: null or aliased pointers");
+  if (N == 0 || P == 0) return BPK_OK;
+  const bool v4 = P % 4 == 0 && (reinterpret_cast<uintptr_t>(u) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const int64_t pv = v4 ? P / 4 : P, units = N * pv;
+  const unsigned blocks = (unsigned)std::min<int64_t>(bpk::ceil_div(units, 256), 4096);
+  hipStream_t st = bpk::as_stream(stream);
+  if (v4)
+    hipLaunchKernelGGL(swap_scale_kernel<4>, dim3(blocks), dim3(256), 0, st, u, out, units, pv,
+                       c0, c1);
+  else
+    hipLaunchKernelGGL(swap_scale_kernel<1>, dim3(blocks), dim3(256), 0, st, u, out, units, pv,
+                       c0, c1);
+  BPK_LAUNCH_CHECK("swap_scale");
+  return BPK_OK;
+}

@@ -799,8 +799,11 @@ def _conv_ft_any(x, w):
 
 class _Conv3x3FT(torch.autograd.Function):
     """y = conv3x3(x, _flip_t(w)) for w [Co, Ci, 3, 3] (x has Co channels).  Adjoint:
-    d/dx = conv3x3(gy, w) (flip_t is an involution); d/dw = _flip_t(wgrad(x, gy)).  Both
-    differentiable again (second derivatives of the PINN residual)."""
+    d/dx = conv3x3(gy, w) (flip_t is an involution); d/dw = _flip_t(wgrad(x, gy)), which is
+    the weight gradient with the roles of input and output gradient exchanged,
+    d/dw[a][b][r][s] = sum_q x[a](q) gy[b](q + (r - 1, s - 1)) = wgrad(gy, x) -- computed in
+    w's own layout (no flip launch, and a contiguous gradient AccumulateGrad can take without
+    a copy).  Both differentiable again (second derivatives of the PINN residual)."""
 
     @staticmethod
     def forward(ctx, x, w):
@@ -815,11 +818,10 @@ class _Conv3x3FT(torch.autograd.Function):
         if want_grad(ctx, 0):
             gx = _conv_any(gy, w)
         if want_grad(ctx, 1):
-            fshape = (w.shape[1], w.shape[0], 3, 3)
             if torch.is_grad_enabled():
-                gw = _flip_t(_Wgrad3x3.apply(x, gy, fshape))
+                gw = _Wgrad3x3.apply(gy, x, tuple(w.shape))
             else:
-                gw = _flip_t(_wgrad_impl(x, gy, fshape, False)[0])
+                gw = _wgrad_impl(gy, x, tuple(w.shape), False)[0]
         return gx, gw
 
 

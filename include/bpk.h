@@ -275,6 +275,13 @@ int bpk_group_norm_param_grads_f32(const float* dx, const float* dgamma_nc, cons
                                    float* d_bias_nc, float* dgamma, float* dbeta, int N, int C,
                                    int64_t HW, void* stream);
 
+/* out[n, 0] = u[n, 1] / c0, out[n, 1] = u[n, 0] / c1 for u, out [N, 2, P] (distinct buffers):
+ * the flow-component swap + scale of FlowNet's project (reference models/flownet.py:8-25,
+ * torch.cat([u[:, 1:2] / c0, u[:, 0:1] / c1], 1)); a tensor-by-scalar division as aten runs it
+ * (times the fp32 reciprocal 1.f / c): bit-identical. */
+int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c0, float c1,
+                       void* stream);
+
 /* out[n,c,:] = (x + (h + bias[c])) / div -- the skip_rescale residual of the
  * BigGAN / DDPM++ blocks with Conv_1's bias folded in (models/layerspp.py:266-274,
  * :200-209).  bias may be NULL.  x, h, out: [N, C, HW]. */

@@ -138,6 +138,35 @@ def test_native_leaky_relu_bit_identical_to_aten_to_third_order(hip, slope):
     assert torch.autograd.gradgradcheck(lambda v: leaky_relu(v, slope), (x,))
 
 
+@pytest.mark.parametrize("shape", [(3, 2, 16, 20), (2, 2, 5, 7), (64, 2, 32, 32)])
+def test_swap_scale_native_bit_identical_to_aten(hip, shape):
+    """op.channels.swap_scale (FlowNet's project: torch.cat([u[:, 1:2] / c0, u[:, 0:1] / c1], 1))
+    on the native kernel (csrc/channels.hip; float4 and scalar paths) == aten bit for bit, in
+    the forward and through three derivative orders."""
+    from op import channels
+    g = torch.Generator().manual_seed(shape[0])
+    u0 = torch.randn(*shape, generator=g).to(hip)
+    c0, c1 = (shape[2] - 1.0) / 2.0, (shape[3] - 1.0) / 2.0
+
+    def derivs(fn):
+        u = u0.clone().requires_grad_()
+        y = fn(u)
+        w = torch.sin(torch.arange(y.numel(), device=hip, dtype=torch.float32)).view_as(y)
+        (d1,) = torch.autograd.grad((y * w).sum(), u, create_graph=True)
+        return y.detach(), d1.detach()
+
+    got = derivs(lambda u: channels.swap_scale(u * u, c0, c1))
+    ref = derivs(lambda u: torch.cat([(u * u)[:, 1:2] / c0, (u * u)[:, 0:1] / c1], 1))
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    # the adjoint's own backward (third order in the PINN residual) is the same kernel
+    u = u0.clone().requires_grad_()
+    y = channels.swap_scale(u, c0, c1)
+    (g1,) = torch.autograd.grad(y, u, torch.ones_like(y), create_graph=True)
+    assert torch.equal(g1[:, 0], torch.ones_like(g1[:, 0]) / c1)
+    assert torch.equal(g1[:, 1], torch.ones_like(g1[:, 1]) / c0)
+
+
 # ------------------------------------------------------------------ GroupNorm + SiLU
 @pytest.mark.parametrize("N,C,H,G", [(2, 64, 16, 16), (3, 128, 32, 32), (2, 256, 64, 32),
                                       (2, 384, 64, 32), (1, 8, 5, 2), (2, 32, 128, 8),

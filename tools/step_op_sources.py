@@ -1,8 +1,8 @@
 """Which autograd nodes issue a bench step's aten launches: the step bench.py counts FLOPs on
 (bench.counted, one eager step after the warm-up) runs under a TorchDispatchMode; every aten op
 is keyed by (op, the autograd node running it or "<forward>"), ops outside any node also by
-their innermost repo call site.  python tools/step_op_sources.py cifar (configs[1] train step;
-the DSM 128^2 step runs the same NCSN++ family inside bench.main)"""
+their innermost repo call site.  python tools/step_op_sources.py cifar|pinn (configs[1] train
+step / configs[3] PINN step; the DSM 128^2 step runs the NCSN++ family inside bench.main)"""
 import collections
 import os
 import sys
@@ -24,7 +24,8 @@ cnt, sites = collections.Counter(), collections.Counter()
 
 def _site():
     for fr in reversed(traceback.extract_stack()[:-3]):
-        if REPO in fr.filename and "step_op_sources" not in fr.filename:
+        if (REPO in fr.filename and "step_op_sources" not in fr.filename
+                and not fr.filename.endswith("op/flops.py")):
             return f"{os.path.relpath(fr.filename, REPO)}:{fr.lineno} {fr.line}"
     return "?"
 
@@ -50,12 +51,12 @@ def counted(fn, dev):
 
 bench.counted = counted
 which = sys.argv[1]
-sys.argv = ["bench.py", "--cifar-steps", "1", "--train-steps", "1", "--train-warmup", "1"]
+sys.argv = ["bench.py", "--cifar-steps", "1", "--pinn-steps", "1", "--pinn-warmup", "1"]
 args = bench.parse()
 ctx = dist.init_from_env()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-{"cifar": bench.bench_cifar_train}[which](args, ctx, dev)
+{"cifar": bench.bench_cifar_train, "pinn": bench.bench_pinn}[which](args, ctx, dev)
 tot = sum(cnt.values())
 print(f"{which}: {tot} aten ops in one step (views skipped)")
 by_op = collections.Counter()
