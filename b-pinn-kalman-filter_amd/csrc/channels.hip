@@ -35,19 +35,60 @@ __global__ __launch_bounds__(256) void swap_scale_kernel(const float* __restrict
   }
 }
 
+// the channels-last layout [N, P, 2] (the gradients the PINN residual sends back through
+// project's NHWC grid view): two pixels' (c0, c1) pairs per float4
+__global__ __launch_bounds__(256) void swap_scale_pairs_kernel(const float4* __restrict__ u,
+                                                               float4* __restrict__ out,
+                                                               int64_t units, float c0, float c1) {
+  const float r0 = 1.f / c0, r1 = 1.f / c1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < units;
+       i += (int64_t)gridDim.x * 256) {
+    const float4 x = u[i];
+    out[i] = make_float4(x.y * r0, x.x * r1, x.w * r0, x.z * r1);
+  }
+}
+
+__global__ __launch_bounds__(256) void swap_scale_pair_kernel(const float2* __restrict__ u,
+                                                              float2* __restrict__ out,
+                                                              int64_t units, float c0, float c1) {
+  const float r0 = 1.f / c0, r1 = 1.f / c1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < units;
+       i += (int64_t)gridDim.x * 256) {
+    const float2 x = u[i];
+    out[i] = make_float2(x.y * r0, x.x * r1);
+  }
+}
+
 }  // namespace
 
 extern "C" int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c0,
-                                  float c1, void* stream) {
+                                  float c1, int channels_last, void* stream) {
   BPK_REQUIRE(N >= 0 && P >= 0, "swap_scale: bad shape N=%lld P=%lld", (long long)N,
               (long long)P);
   BPK_REQUIRE(u && out && u != out, "swap_scale: null or aliased pointers");
   if (N == 0 || P == 0) return BPK_OK;
-  const bool v4 = P % 4 == 0 && (reinterpret_cast<uintptr_t>(u) & 15) == 0 &&
+  hipStream_t st = bpk::as_stream(stream);
+  const bool al = (reinterpret_cast<uintptr_t>(u) & 15) == 0 &&
                   (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  if (channels_last) {
+    const int64_t pix = N * P;
+    const bool v4 = al && pix % 2 == 0;
+    const int64_t units = v4 ? pix / 2 : pix;
+    const unsigned blocks = (unsigned)std::min<int64_t>(bpk::ceil_div(units, 256), 4096);
+    if (v4)
+      hipLaunchKernelGGL(swap_scale_pairs_kernel, dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(u), reinterpret_cast<float4*>(out),
+                         units, c0, c1);
+    else
+      hipLaunchKernelGGL(swap_scale_pair_kernel, dim3(blocks), dim3(256), 0, st,
+                         reinterpret_cast<const float2*>(u), reinterpret_cast<float2*>(out),
+                         units, c0, c1);
+    BPK_LAUNCH_CHECK("swap_scale");
+    return BPK_OK;
+  }
+  const bool v4 = P % 4 == 0 && al;
   const int64_t pv = v4 ? P / 4 : P, units = N * pv;
   const unsigned blocks = (unsigned)std::min<int64_t>(bpk::ceil_div(units, 256), 4096);
-  hipStream_t st = bpk::as_stream(stream);
   if (v4)
     hipLaunchKernelGGL(swap_scale_kernel<4>, dim3(blocks), dim3(256), 0, st, u, out, units, pv,
                        c0, c1);

@@ -219,10 +219,12 @@ __global__ __launch_bounds__(256) void gs_grad2(
     const int64_t n = idx / ((int64_t)Ho * Wo);
     const T gx = grid[idx * 2], gy = grid[idx * 2 + 1];
     q = corners(gx, gy, H, W, padding, align != 0);
-    const T dx = g2_grid[idx * 2] * q.gix_mult;
-    const T dy = g2_grid[idx * 2 + 1] * q.giy_mult;
+    // a NULL g2_grid / g2_inp is an all-zero incoming gradient (autograd passes None for an
+    // output nothing depends on; materialising zeros cost a fill launch and a read)
+    const T dx = g2_grid ? g2_grid[idx * 2] * q.gix_mult : T(0);
+    const T dy = g2_grid ? g2_grid[idx * 2 + 1] * q.giy_mult : T(0);
     const T* ip = inp + n * C * H * W;
-    const T* g2p = g2_inp + n * C * H * W;
+    const T* g2p = g2_inp ? g2_inp + n * C * H * W : nullptr;
     T* gip = grad_inp + n * C * H * W;
     const int64_t oofs = n * C * Ho * Wo + (int64_t)h * Wo + w;
     const bool b_nw = inb(q.iy_nw, q.ix_nw, H, W), b_ne = inb(q.iy_ne, q.ix_ne, H, W),
@@ -237,10 +239,10 @@ __global__ __launch_bounds__(256) void gs_grad2(
       const T ne_v = b_ne ? ip[pc + q.iy_ne * W + q.ix_ne] : T(0);
       const T sw_v = b_sw ? ip[pc + q.iy_sw * W + q.ix_sw] : T(0);
       const T se_v = b_se ? ip[pc + q.iy_se * W + q.ix_se] : T(0);
-      const T g2_nw = b_nw ? g2p[pc + q.iy_nw * W + q.ix_nw] : T(0);
-      const T g2_ne = b_ne ? g2p[pc + q.iy_ne * W + q.ix_ne] : T(0);
-      const T g2_sw = b_sw ? g2p[pc + q.iy_sw * W + q.ix_sw] : T(0);
-      const T g2_se = b_se ? g2p[pc + q.iy_se * W + q.ix_se] : T(0);
+      const T g2_nw = g2p && b_nw ? g2p[pc + q.iy_nw * W + q.ix_nw] : T(0);
+      const T g2_ne = g2p && b_ne ? g2p[pc + q.iy_ne * W + q.ix_ne] : T(0);
+      const T g2_sw = g2p && b_sw ? g2p[pc + q.iy_sw * W + q.ix_sw] : T(0);
+      const T g2_se = g2p && b_se ? g2p[pc + q.iy_se * W + q.ix_se] : T(0);
       T ggo = T(0);
       ggo += g2_nw * q.nw + g2_ne * q.ne + g2_sw * q.sw + g2_se * q.se;
       ggo += nw_v * nw_tmp + ne_tmp * ne_v + sw_tmp * sw_v + se_tmp * se_v;

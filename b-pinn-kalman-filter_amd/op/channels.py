@@ -62,11 +62,17 @@ class _SwapScale(Function):
     def forward(ctx, u, c0, c1):
         ctx.c = (c0, c1)
         if u.is_cuda and u.dtype == torch.float32:
-            # one launch (csrc/channels.hip) instead of two divisions into output slices
-            u = u.contiguous()
-            out = torch.empty_like(u)
+            # one launch (csrc/channels.hip) instead of two divisions into output slices; the
+            # gradients coming back through project's NHWC grid view are channels-last and run
+            # in that layout (no copy)
+            cl = u.dim() == 4 and not u.is_contiguous() and u.permute(0, 2, 3, 1).is_contiguous()
+            if not cl:
+                u = u.contiguous()
+            out = torch.empty_like(u)  # same strides as u (dense)
+            if out.stride() != u.stride():
+                raise RuntimeError(f"swap_scale: output strides {out.stride()} != {u.stride()}")
             check(lib.bpk_swap_scale_f32(u.data_ptr(), out.data_ptr(), u.shape[0],
-                                         u[0, 0].numel(), c0, c1, stream_ptr(u.device)),
+                                         u[0, 0].numel(), c0, c1, int(cl), stream_ptr(u.device)),
                   "swap_scale")
             return out
         out = torch.empty_like(u)  # float64 (gradcheck) / CPU tensors

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import check, lib, require_hip, stream_ptr
+from ._lib import check, lib, ptr, require_hip, stream_ptr
 
 _PADDING = {"zeros": 0, "border": 1}
 
@@ -59,13 +59,14 @@ def grid_sample2d_bwd_raw(grad_out, input, grid, padding_mode, align_corners, ne
 
 def grid_sample2d_grad2_raw(g2_input, g2_grid, grad_out, input, grid, padding_mode,
                             align_corners):
-    args = [t.contiguous() for t in (g2_input, g2_grid, grad_out, input, grid)]
+    """g2_input / g2_grid may be None: an all-zero incoming gradient (no fill, no read)."""
+    args = [t if t is None else t.contiguous() for t in (g2_input, g2_grid, grad_out, input, grid)]
     g2_input, g2_grid, grad_out, input, grid = args
     N, C, H, W, Ho, Wo = _geom(input, grid)
     ggo = torch.empty_like(grad_out)
     gi = torch.zeros_like(input)
     gg = torch.empty_like(grid)
-    check(_fns(input.dtype)[2](g2_input.data_ptr(), g2_grid.data_ptr(), grad_out.data_ptr(),
+    check(_fns(input.dtype)[2](ptr(g2_input), ptr(g2_grid), grad_out.data_ptr(),
                                input.data_ptr(), grid.data_ptr(), ggo.data_ptr(), gi.data_ptr(),
                                gg.data_ptr(), N, C, H, W, Ho, Wo, padding_mode, int(align_corners),
                                stream_ptr(input.device)), "grid_sample2d_grad2")
@@ -106,10 +107,7 @@ class _GridSample2dBackward(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g2_input, g2_grid):
         grad_output, input, grid = ctx.saved_tensors
-        if g2_input is None:
-            g2_input = torch.zeros_like(input)
-        if g2_grid is None:
-            g2_grid = torch.zeros_like(grid)
+        # a None incoming gradient goes to the kernel as NULL (all zero)
         ggo, gi, gg = grid_sample2d_grad2_raw(g2_input, g2_grid, grad_output, input, grid,
                                               ctx.padding_mode, ctx.align_corners)
         return ggo, gi, gg, None, None

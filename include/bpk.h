@@ -87,7 +87,8 @@ int bpk_fused_bias_act_f64(const double* x, const double* bias, const double* re
  * bwd: grad_input (may be NULL) must be zero-filled by the caller (atomics);
  *      grad_grid (may be NULL) is overwritten.
  * grad2: outputs grad_grad_output (overwritten), grad_input (zero-filled by the
- *      caller, atomics), grad_grid (overwritten).
+ *      caller, atomics), grad_grid (overwritten); g2_input / g2_grid may be NULL (an
+ *      all-zero incoming gradient, the None autograd passes).
  * ------------------------------------------------------------------------- */
 int bpk_grid_sample2d_fwd_f32(const float* input, const float* grid, float* out, int N, int C,
                               int H_in, int W_in, int H_out, int W_out, int padding_mode,
@@ -275,12 +276,13 @@ int bpk_group_norm_param_grads_f32(const float* dx, const float* dgamma_nc, cons
                                    float* d_bias_nc, float* dgamma, float* dbeta, int N, int C,
                                    int64_t HW, void* stream);
 
-/* out[n, 0] = u[n, 1] / c0, out[n, 1] = u[n, 0] / c1 for u, out [N, 2, P] (distinct buffers):
+/* out[n, 0] = u[n, 1] / c0, out[n, 1] = u[n, 0] / c1 for u, out [N, 2, P] (distinct buffers;
+ * channels_last != 0: both stored [N, P, 2]):
  * the flow-component swap + scale of FlowNet's project (reference models/flownet.py:8-25,
  * torch.cat([u[:, 1:2] / c0, u[:, 0:1] / c1], 1)); a tensor-by-scalar division as aten runs it
  * (times the fp32 reciprocal 1.f / c): bit-identical. */
 int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c0, float c1,
-                       void* stream);
+                       int channels_last, void* stream);
 
 /* out[n,c,:] = (x + (h + bias[c])) / div -- the skip_rescale residual of the
  * BigGAN / DDPM++ blocks with Conv_1's bias folded in (models/layerspp.py:266-274,

@@ -165,6 +165,14 @@ def test_swap_scale_native_bit_identical_to_aten(hip, shape):
     (g1,) = torch.autograd.grad(y, u, torch.ones_like(y), create_graph=True)
     assert torch.equal(g1[:, 0], torch.ones_like(g1[:, 0]) / c1)
     assert torch.equal(g1[:, 1], torch.ones_like(g1[:, 1]) / c0)
+    # channels-last input (the gradients coming back through project's NHWC grid view): run in
+    # that layout, same bits
+    ucl = u0.permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
+    assert not ucl.is_contiguous()
+    with torch.no_grad():
+        y = channels._SwapScale.apply(ucl, c0, c1)
+    assert y.stride() == ucl.stride()
+    assert torch.equal(y, torch.cat([ucl[:, 1:2] / c0, ucl[:, 0:1] / c1], 1))
 
 
 # ------------------------------------------------------------------ GroupNorm + SiLU

@@ -65,6 +65,10 @@ for (op, _), v in cnt.items():
 print("by op:", by_op.most_common(25))
 for (op, node), v in cnt.most_common(40):
     print(f"{v:6d}  {op:28s} {node}")
+print("every (op, node) of the launch-heavy ops:")
+for (op, node), v in sorted(cnt.items(), key=lambda kv: (kv[0][0], -kv[1])):
+    if op in ("clone", "copy_", "add", "zeros_like", "zeros", "mul", "div", "neg", "sum", "cat"):
+        print(f"{v:6d}  {op:12s} {node}")
 print("ops outside any autograd node, by call site:")
 for (op, site), v in sites.most_common(60):
     if not site.startswith(("_", "torch::")) and "Backward" not in site:
