@@ -1,8 +1,8 @@
 """Which autograd nodes issue a bench step's aten launches: the step bench.py counts FLOPs on
 (bench.counted, one eager step after the warm-up) runs under a TorchDispatchMode; every aten op
 is keyed by (op, the autograd node running it or "<forward>"), ops outside any node also by
-their innermost repo call site.  python tools/step_op_sources.py cifar|pinn (configs[1] train
-step / configs[3] PINN step; the DSM 128^2 step runs the NCSN++ family inside bench.main)"""
+their innermost repo call site.  python tools/step_op_sources.py cifar|pinn|dps (configs[1]
+train step / configs[3] PINN step / one configs[5] DPS function evaluation; the DSM 128^2 step runs the NCSN++ family inside bench.main)"""
 import collections
 import os
 import sys
@@ -51,12 +51,14 @@ def counted(fn, dev):
 
 bench.counted = counted
 which = sys.argv[1]
-sys.argv = ["bench.py", "--cifar-steps", "1", "--pinn-steps", "1", "--pinn-warmup", "1"]
+sys.argv = ["bench.py", "--cifar-steps", "1", "--pinn-steps", "1", "--pinn-warmup", "1",
+            "--dps-steps", "1"]
 args = bench.parse()
 ctx = dist.init_from_env()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-{"cifar": bench.bench_cifar_train, "pinn": bench.bench_pinn}[which](args, ctx, dev)
+{"cifar": bench.bench_cifar_train, "pinn": bench.bench_pinn, "dps": bench.bench_dps}[which](
+    args, ctx, dev)
 tot = sum(cnt.values())
 print(f"{which}: {tot} aten ops in one step (views skipped)")
 by_op = collections.Counter()
@@ -67,7 +69,8 @@ for (op, node), v in cnt.most_common(40):
     print(f"{v:6d}  {op:28s} {node}")
 print("every (op, node) of the launch-heavy ops:")
 for (op, node), v in sorted(cnt.items(), key=lambda kv: (kv[0][0], -kv[1])):
-    if op in ("clone", "copy_", "add", "zeros_like", "zeros", "mul", "div", "neg", "sum", "cat"):
+    if op in ("clone", "copy_", "add", "zeros_like", "zeros", "mul", "div", "neg", "sum", "cat",
+              "linalg_vector_norm", "_to_copy", "fill_"):
         print(f"{v:6d}  {op:12s} {node}")
 print("ops outside any autograd node, by call site:")
 for (op, site), v in sites.most_common(60):
