@@ -254,14 +254,18 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
       }
     }
   };
-  // Gbar = A dY A^T with A = [[1,0],[1,1],[1,-1],[0,-1]]: 16 values, position 4 i + j
+  // Gbar' = A' dY A'^T with A' = [[1,0],[1,1],[1,-1],[0,1]]: 16 values, position 4 i + j.
+  // A' is the transform's A = [[1,0],[1,1],[1,-1],[0,-1]] with its last row negated, so
+  // Gbar' = D Gbar D (D = diag(1,1,1,-1)) and the partial sums come out as D M D; the reduce
+  // kernel's output transform absorbs D (G' = D G, exact sign flips: bit-identical dw) and the
+  // 16 negations per k-step leave the MFMA loop
   auto gbar = [&](const float2 (&t)[2], f4 (&bq)[4]) {
     const float a = t[0].x, bb = t[0].y, c = t[1].x, dd = t[1].y;
-    const float rows[4][2] = {{a, bb}, {a + c, bb + dd}, {a - c, bb - dd}, {-c, -dd}};
+    const float rows[4][2] = {{a, bb}, {a + c, bb + dd}, {a - c, bb - dd}, {c, dd}};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float p = rows[i][0], q = rows[i][1];
-      bq[i] = f4{p, p + q, p - q, -q};
+      bq[i] = f4{p, p + q, p - q, q};
     }
   };
 
@@ -375,7 +379,8 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   }
 }
 
-// dw[cout][cin] = G^T (sum_s part[s][cin][cout]) G,  G^T = [[1,.5,.5,0],[0,.5,-.5,0],[0,.5,.5,1]]
+// dw[cout][cin] = G'^T (sum_s part[s][cin][cout]) G',  G'^T = [[1,.5,.5,0],[0,.5,-.5,0],[0,.5,.5,-1]]
+// (G' = D G: the partials are D M D, see gbar in wino_wgrad_pipe_kernel)
 // Block = 16 (cin, cout) pairs x 4 float4 columns of their 16 partial values x 4 groups of
 // splits (group g sums splits g, g + 4, ...; the groups combine in a fixed order in LDS):
 // deterministic, and 16x the parallelism of one thread per pair (the PINN shapes have few
@@ -411,12 +416,12 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
       f4 u[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) u[r] = red[0][4 * threadIdx.x + r];
-      float t[3][4];  // G^T dU (rows of dU = u[row])
+      float t[3][4];  // G'^T dU (rows of dU = u[row])
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         t[0][j] = u[0][j] + 0.5f * (u[1][j] + u[2][j]);
         t[1][j] = 0.5f * (u[1][j] - u[2][j]);
-        t[2][j] = 0.5f * (u[1][j] + u[2][j]) + u[3][j];
+        t[2][j] = 0.5f * (u[1][j] + u[2][j]) - u[3][j];
       }
       const int ci = (int)(pi / Cout), co = (int)(pi % Cout);
       float* o = dw + ((int64_t)co * Cin + ci) * 9;
@@ -424,7 +429,7 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
       for (int r = 0; r < 3; ++r) {
         o[3 * r + 0] = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
         o[3 * r + 1] = 0.5f * (t[r][1] - t[r][2]);
-        o[3 * r + 2] = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
+        o[3 * r + 2] = 0.5f * (t[r][1] + t[r][2]) - t[r][3];
       }
     }
   }
