@@ -174,11 +174,16 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const int hx = xh ? ox0 + 16 : ox0 - 1;
     xhalo_ok = hx >= 0 && hx < g.W;
     const int hxc = min(max(hx, 0), g.W - 1);
-    const int rowoff = (xc * plane + iyc * g.W) * 4;
+    // without the prologue, rows / halo columns outside the image read as zero through the
+    // buffer's range check (offsets past num_records = kCB * plane * 4 < 2^31 return 0): no
+    // zeroing multiplies in store_x.  With it, silu(0 * s + t) != 0, so store_x masks.
+    constexpr unsigned kOOB = 0x80000000u;
+    const unsigned rowoff = (!PRE && !xrow_ok) ? kOOB : (unsigned)((xc * plane + iyc * g.W) * 4);
+    const unsigned hoff = (!PRE && !(xrow_ok && xhalo_ok)) ? kOOB : rowoff + (unsigned)(hxc * 4);
     using u4 = __attribute__((ext_vector_type(4))) unsigned;
-    const u4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, rowoff + (ox0 + 8 * xh) * 4, 0, 0);
-    const u4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, rowoff + (ox0 + 8 * xh + 4) * 4, 0, 0);
-    const unsigned hv = __builtin_amdgcn_raw_buffer_load_b32(rs, rowoff + hxc * 4, 0, 0);
+    const u4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(rowoff + (unsigned)((ox0 + 8 * xh) * 4)), 0, 0);
+    const u4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(rowoff + (unsigned)((ox0 + 8 * xh + 4) * 4)), 0, 0);
+    const unsigned hv = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)hoff, 0, 0);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       xv[e] = __uint_as_float(a[e]);
@@ -188,23 +193,26 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   };
   auto store_x = [&](float* sx) {
     float* row = sx + xc * kXCS + xpy * kXRS;
-    const float z = xrow_ok ? 1.f : 0.f;
-    if (PRE) {
+    if (PRE) {  // padding stays zero after the activation: mask here
+      const float z = xrow_ok ? 1.f : 0.f;
 #pragma unroll
       for (int e = 0; e < 9; ++e) {
         const float u = xv[e] * xst.x + xst.y;
         xv[e] = u * __builtin_amdgcn_rcpf(1.f + __expf(-u));
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] *= z;
+      xv[8] = (xrow_ok && xhalo_ok) ? xv[8] : 0.f;
     }
     if (PAIR) {  // image xh's 8 pixels at columns 4 + 10 xh (8-byte aligned for xh = 1)
       float2* r2 = reinterpret_cast<float2*>(row + 4 + 10 * xh);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) r2[e] = make_float2(xv[2 * e] * z, xv[2 * e + 1] * z);
+      for (int e = 0; e < 4; ++e) r2[e] = make_float2(xv[2 * e], xv[2 * e + 1]);
       return;
     }
-    *reinterpret_cast<f4*>(row + 4 + 8 * xh) = f4{xv[0] * z, xv[1] * z, xv[2] * z, xv[3] * z};
-    *reinterpret_cast<f4*>(row + 8 + 8 * xh) = f4{xv[4] * z, xv[5] * z, xv[6] * z, xv[7] * z};
-    row[xh ? 20 : 3] = (xrow_ok && xhalo_ok) ? xv[8] : 0.f;
+    *reinterpret_cast<f4*>(row + 4 + 8 * xh) = f4{xv[0], xv[1], xv[2], xv[3]};
+    *reinterpret_cast<f4*>(row + 8 + 8 * xh) = f4{xv[4], xv[5], xv[6], xv[7]};
+    row[xh ? 20 : 3] = xv[8];
   };
 
   // ---- V = B^T d B of one (tile, cin) per thread: c = tid >> 3, tile = tid & 7
@@ -237,20 +245,33 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   const int gco = cout0 + 16 * NB * wave + jj;
   float2 gq[NB][2][2];  // [nb][ks][row], one chunk ahead
   Strip gcur = strip_at(0);
+  // buffer loads: the chunk's base (image, this wave's first cout, strip origin) is uniform --
+  // a scalar resource and soffset -- and the lane's part (cout jj + 16 nb, tile column) a
+  // fixed 32-bit voffset: no per-chunk 64-bit address arithmetic on the vector unit
+  const int gwave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gvo0 = (jj * plane + 2 * kq) * 4;  // + 16 nb planes; + W floats for row 1
   auto load_g = [&](float2 (&dst)[NB][2][2]) {  // gradient tiles of chunk gcur, then advance
     const Strip s = gcur;
     advance(gcur);
     if (!wvalid) return;  // past Cout: its MFMAs run on stale registers, never stored
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < 2; ++ks) {
+      {
         // tile 4 ks + kq; PAIR: k-step ks is image 2n + ks, tile column kq
-        const float* src = gy + ((int64_t)(PAIR ? 2 * s.n + ks : s.n) * g.Cout + gco + 16 * nb) * plane +
-                           (int64_t)(2 * s.sy) * g.W + (PAIR ? 0 : 16 * s.sx);
-        const float* p = src + 2 * (PAIR ? kq : 4 * ks + kq);
-        dst[nb][ks][0] = *reinterpret_cast<const float2*>(p);
-        dst[nb][ks][1] = *reinterpret_cast<const float2*>(p + g.W);
+        const int img = PAIR ? 2 * s.n + ks : s.n;
+        const float* base = gy + ((int64_t)img * g.Cout + cout0 + 16 * NB * gwave) * plane;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(base), 0, 16 * NB * plane * 4, 0x00020000);
+        const int so = (2 * s.sy * g.W + (PAIR ? 0 : 16 * s.sx + 8 * ks)) * 4;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          using u2 = __attribute__((ext_vector_type(2))) unsigned;
+          const int vo = gvo0 + 16 * nb * plane * 4;
+          const u2 r0 = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0);
+          const u2 r1 = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + g.W * 4, so, 0);
+          dst[nb][ks][0] = make_float2(__uint_as_float(r0[0]), __uint_as_float(r0[1]));
+          dst[nb][ks][1] = make_float2(__uint_as_float(r1[0]), __uint_as_float(r1[1]));
+        }
       }
     }
   };
