@@ -40,6 +40,10 @@ def step_bytes(mode, counter):
     red = os.path.join(SRC, pdir(mode, counter.split("_")[0].lower()) + ".json")
     if os.path.exists(red):
         d = json.load(open(red))
+        # a pass reduced on the box records the kernel sources it ran; one from another tree
+        # (a pass that crashed this time leaves the previous run's file) is not this tree's
+        want = provenance("step")["src_sha1"]
+        assert d.get("src_sha1") == want, (mode, counter, "stale pass", d.get("src_sha1"), want)
         return d["sum_kb"], d["dispatches"]
     per = collections.OrderedDict()
     for r in rows(pdir(mode, counter.split("_")[0].lower())):
@@ -154,7 +158,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 3 and sys.argv[3] == "reduce-step":
         # on the GPU box: reduce one step pass (argv[4] = mode, argv[5] = counter) to JSON
         kb, n = step_bytes(sys.argv[4], sys.argv[5])
-        json.dump({"sum_kb": kb, "dispatches": n},
+        json.dump({"sum_kb": kb, "dispatches": n, "src_sha1": provenance("step")["src_sha1"]},
                   open(os.path.join(SRC, pdir(sys.argv[4], sys.argv[5].split("_")[0].lower())
                                     + ".json"), "w"))
         print("reduced", sys.argv[4], sys.argv[5], kb, n)
