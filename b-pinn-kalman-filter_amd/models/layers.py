@@ -7,6 +7,7 @@ the fused HIP ops of `op.norm_act` (GroupNorm + bias + SiLU, residual rescale).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -120,6 +121,8 @@ _GN_STATS = True      # GroupNorm partial statistics from the producing conv's e
 _GEMM1X1 = True       # 1x1 convs on the MFMA GEMM kernels
 _DDPM_FUSED = True    # ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs
 _GN_CONV_AD = True    # eval-mode autograd (DPS): GroupNorm+SiLU inside the conv's input load
+# the same under training (A/B switch, BPK_GN_CONV_AD_TRAIN=1)
+_GN_CONV_AD_TRAIN = os.environ.get("BPK_GN_CONV_AD_TRAIN", "0") == "1"
 
 
 def _is_3x3(x, conv: nn.Conv2d):
@@ -189,7 +192,7 @@ def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act
     composition: on the DSM and CIFAR train steps the fused form measured 2.8 % and 1.5 %
     slower (the weight gradient's per-element SiLU in its patch load, the igemm choice lost
     on small images), DPS 4.1 % faster (profiles/r05_gn_conv_ad_ab.txt)."""
-    if not (_GN_CONV_AD and not module.training and torch.is_grad_enabled()
+    if not (_GN_CONV_AD and (not module.training or _GN_CONV_AD_TRAIN) and torch.is_grad_enabled()
             and isinstance(act, nn.SiLU) and _is_3x3(x, conv)):
         return None
     if skip is not None and skip.shape[1] != conv.out_channels:

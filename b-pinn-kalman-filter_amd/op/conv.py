@@ -978,7 +978,9 @@ class _GNSiLUConv3x3(torch.autograd.Function):
         gskip = gy if ctx.has_skip and want_grad(ctx, 6) else None
         want_w, want_cb = want_grad(ctx, 4), ctx.has_bias and want_grad(ctx, 5)
         gw = gcb = None
-        if want_w and wgrad_supported(x, tuple(w.shape)):  # the activation never stored
+        if want_w and wgrad_supported(x, tuple(w.shape)) and not _small_img(x):
+            # the activation never stored (small images: materialised below, so the timed
+            # Winograd / implicit-GEMM choice of _wgrad_impl still applies)
             r = conv3x3_wgrad_raw(x, gy, tuple(w.shape), bias_grad=want_cb, pre=ss)
             gw, gcb = r if want_cb else (r, None)
         elif want_w:
