@@ -59,7 +59,54 @@ __global__ __launch_bounds__(256) void swap_scale_pair_kernel(const float2* __re
   }
 }
 
+// y[p][i][j] = (x[p][2i][2j] + x[p][2i][2j+1]) + (x[p][2i+1][2j] + x[p][2i+1][2j+1]) over planes
+// p: the adjoint of the nearest x2 upsample (the `ddpm` net's Upsample under autograd, DPS:
+// op.conv._ConvUp2's input gradient).  aten ran it as a strided reduction over a 6-D view
+// (≈470 us per call at 256^2); one pass here, two output pixels per thread from two float4 rows
+template <bool V4>
+__global__ __launch_bounds__(256) void sum2x2_kernel(const float* __restrict__ x,
+                                                     float* __restrict__ y, int64_t units,
+                                                     int H, int W) {
+  const int Wq = V4 ? W / 2 : W;  // units per output row: pairs of output pixels (V4) or pixels
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < units;
+       u += (int64_t)gridDim.x * 256) {
+    const int64_t row = u / Wq;  // output row index over all planes
+    const int c = (int)(u - row * Wq);
+    const int64_t p = row / H;
+    const int i = (int)(row - p * H);
+    const float* r0 = x + (p * 2 * H + 2 * i) * (int64_t)(2 * W);
+    const float* r1 = r0 + 2 * W;
+    if constexpr (V4) {
+      const float4 a = reinterpret_cast<const float4*>(r0)[c];
+      const float4 b = reinterpret_cast<const float4*>(r1)[c];
+      reinterpret_cast<float2*>(y + row * W)[c] =
+          make_float2((a.x + a.y) + (b.x + b.y), (a.z + a.w) + (b.z + b.w));
+    } else {
+      y[row * W + c] = (r0[2 * c] + r0[2 * c + 1]) + (r1[2 * c] + r1[2 * c + 1]);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int bpk_sum2x2_f32(const float* x, float* y, int64_t planes, int H, int W,
+                              void* stream) {
+  BPK_REQUIRE(planes >= 0 && H > 0 && W > 0, "sum2x2: bad shape");
+  BPK_REQUIRE(x && y, "sum2x2: null pointer");
+  if (planes == 0) return BPK_OK;
+  const bool v4 = W % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(y) & 7) == 0;
+  const int64_t units = planes * H * (v4 ? W / 2 : W);
+  const unsigned blocks = (unsigned)std::min<int64_t>(bpk::ceil_div(units, 256), 8192);
+  if (v4)
+    hipLaunchKernelGGL(sum2x2_kernel<true>, dim3(blocks), dim3(256), 0, bpk::as_stream(stream), x,
+                       y, units, H, W);
+  else
+    hipLaunchKernelGGL(sum2x2_kernel<false>, dim3(blocks), dim3(256), 0, bpk::as_stream(stream), x,
+                       y, units, H, W);
+  BPK_LAUNCH_CHECK("sum2x2");
+  return BPK_OK;
+}
 
 extern "C" int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c0,
                                   float c1, int channels_last, void* stream) {

@@ -1052,10 +1052,32 @@ def _up2_raw(x, weight, bias):
     return y
 
 
+class _Sum2x2(torch.autograd.Function):
+    """the sum of each 2 x 2 block (adjoint of the nearest x2 upsample) on the native kernel
+    (csrc/channels.hip; aten's strided reduction over the 6-D view took ~470 us per call at
+    256^2); its adjoint is the nearest x2 upsample, so higher orders stay recorded ops"""
+
+    @staticmethod
+    def forward(ctx, g):
+        N, C, H2, W2 = g.shape
+        if g.is_cuda and g.dtype == torch.float32:
+            g = g.contiguous()
+            y = torch.empty((N, C, H2 // 2, W2 // 2), device=g.device, dtype=g.dtype)
+            check(lib.bpk_sum2x2_f32(g.data_ptr(), y.data_ptr(), N * C, H2 // 2, W2 // 2,
+                                     stream_ptr(g.device)), "sum2x2")
+            return y
+        return g.reshape(N, C, H2 // 2, 2, W2 // 2, 2).sum((3, 5))
+
+    @staticmethod
+    def backward(ctx, gg):
+        return F.interpolate(gg, scale_factor=2, mode="nearest")
+
+
 def _sum2x2(g):
     """adjoint of the nearest x2 upsample: the sum of each 2 x 2 block"""
-    N, C, H2, W2 = g.shape
-    return g.reshape(N, C, H2 // 2, 2, W2 // 2, 2).sum((3, 5))
+    if g.shape[2] % 2 or g.shape[3] % 2:
+        raise RuntimeError(f"_sum2x2: even spatial sizes expected, got {tuple(g.shape)}")
+    return _Sum2x2.apply(g)
 
 
 class _ConvUp2(torch.autograd.Function):

@@ -283,6 +283,10 @@ int bpk_group_norm_param_grads_f32(const float* dx, const float* dgamma_nc, cons
  * (times the fp32 reciprocal 1.f / c): bit-identical. */
 int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c0, float c1,
                        int channels_last, void* stream);
+/* y [planes, H, W] = the 2 x 2 block sums of x [planes, 2H, 2W]: the adjoint of the nearest
+ * x2 upsample (the `ddpm` net's Upsample(with_conv=True), reference layers.py:576-590, under
+ * autograd -- the input gradient of bpk_conv3x3_wino_up2_f32's fused upsample + conv). */
+int bpk_sum2x2_f32(const float* x, float* y, int64_t planes, int H, int W, void* stream);
 
 /* out[n,c,:] = (x + (h + bias[c])) / div -- the skip_rescale residual of the
  * BigGAN / DDPM++ blocks with Conv_1's bias folded in (models/layerspp.py:266-274,

@@ -50,3 +50,14 @@ def test_third_derivatives_match_torch():
     a = _third_order(lambda t: channels.swap_scale(t, 0.7, 1.3), [u], wu)
     b = _third_order(lambda t: torch.cat([t[:, 1:2] / 0.7, t[:, 0:1] / 1.3], 1), [u], wu)
     torch.testing.assert_close(a[0], b[0], rtol=1e-12, atol=1e-12)
+
+
+def test_sum2x2_adjoint_pair_cpu_f64():
+    """op.conv._sum2x2 (the 2 x 2 block sum behind conv3x3_up2's input gradient) on the host
+    path: first and second derivatives by gradcheck; its adjoint is the nearest upsample."""
+    from op.conv import _sum2x2
+    x = torch.randn(2, 3, 4, 6, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(_sum2x2, (x,))
+    assert torch.autograd.gradgradcheck(_sum2x2, (x,))
+    y = _sum2x2(x)
+    assert torch.allclose(y, x.reshape(2, 3, 2, 2, 3, 2).sum((3, 5)))

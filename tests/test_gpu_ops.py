@@ -175,6 +175,25 @@ def test_swap_scale_native_bit_identical_to_aten(hip, shape):
     assert torch.equal(y, torch.cat([ucl[:, 1:2] / c0, ucl[:, 0:1] / c1], 1))
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 8, 12), (3, 5, 6, 10), (1, 2, 4, 6)])
+def test_sum2x2_native_vs_block_sum(hip, shape):
+    """the 2 x 2 block sum behind conv3x3_up2's input gradient (csrc/channels.hip; float2 and
+    scalar output paths) vs the reshape-sum it replaces (1e-6 of max|ref|: a different
+    summation order), and its adjoint is the nearest upsample (gradient check in float32)."""
+    from op.conv import _sum2x2
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g).to(hip)
+    N, C, H2, W2 = shape
+    ref = x.reshape(N, C, H2 // 2, 2, W2 // 2, 2).sum((3, 5))
+    got = _sum2x2(x)
+    assert got.shape == ref.shape
+    assert (got - ref).abs().max().item() <= 1e-6 * max(1.0, ref.abs().max().item())
+    xr = x.clone().requires_grad_()
+    gy = torch.randn(ref.shape, generator=g).to(hip)
+    (gx,) = torch.autograd.grad(_sum2x2(xr), xr, gy)
+    assert torch.equal(gx, torch.nn.functional.interpolate(gy, scale_factor=2, mode="nearest"))
+
+
 # ------------------------------------------------------------------ GroupNorm + SiLU
 @pytest.mark.parametrize("N,C,H,G", [(2, 64, 16, 16), (3, 128, 32, 32), (2, 256, 64, 32),
                                       (2, 384, 64, 32), (1, 8, 5, 2), (2, 32, 128, 8),
