@@ -295,7 +295,8 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ bias_nc,
     const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, float* __restrict__ dx,
-    float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C, int HW, int G, int act) {
+    float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C, int HW, int G, int act,
+    const float* __restrict__ addend) {
   extern __shared__ float sdyn[];  // [T/64] reduce buffer + 2*cpg channel partials
   float* sbuf = sdyn;
   float* s_dg = sdyn + T / kWave;
@@ -352,6 +353,12 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
       float o[W];
 #pragma unroll
       for (int q = 0; q < W; ++q) o[q] = rstd * (dxh[k][q] - A - xh[k][q] * Bm);
+      if (addend) {  // another consumer's gradient of x, added where the autograd engine would
+        float ad[W];
+        Vec<W>::load(addend + base + e, ad);
+#pragma unroll
+        for (int q = 0; q < W; ++q) o[q] = ad[q] + o[q];
+      }
       Vec<W>::store(dx + base + e, o);
     }
   }
@@ -466,7 +473,7 @@ __global__ __launch_bounds__(256) void gn_bwd_apply2(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const float2* __restrict__ part_ab, const float2* __restrict__ part_c, float* __restrict__ dx,
     float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C, int HW, int G, int CH,
-    int act) {
+    int act, const float* __restrict__ addend) {
   const int bi = blockIdx.x, bpg = gridDim.x;
   const int ng = blockIdx.y;
   const int n = ng / G;
@@ -511,6 +518,12 @@ __global__ __launch_bounds__(256) void gn_bwd_apply2(
           const float xhat = (xv[u][q] + b - mean) * rstd;
           const float dxhat = gv[u][q] * act_bwd(xhat * ga + be, act) * ga;
           o[q] = rstd * (dxhat - A - xhat * B);
+        }
+        if (addend) {
+          float ad[W];
+          Vec<W>::load(addend + base + (u ? e2 : e), ad);
+#pragma unroll
+          for (int q = 0; q < W; ++q) o[q] = ad[q] + o[q];
         }
         Vec<W>::store(dx + base + (u ? e2 : e), o);
       }
@@ -635,7 +648,7 @@ template <int W>
 int bwd_resident_dispatch(int64_t S, const float* dy, const float* x, const float* bias,
                           const float* gamma, const float* beta, const float* mean,
                           const float* rstd, float* dx, float* dg, float* db, int N, int C, int HW,
-                          int G, int act, hipStream_t st) {
+                          int G, int act, const float* addend, hipStream_t st) {
   const int64_t units = bpk::ceil_div(S, W);
   const int cpg = C / G;
   dim3 grid(N * G);
@@ -643,7 +656,7 @@ int bwd_resident_dispatch(int64_t S, const float* dy, const float* x, const floa
   if (units <= (int64_t)(T_) * (V_)) {                                                         \
     const size_t sh = sizeof(float) * ((T_) / kWave + 2 * cpg);                                \
     hipLaunchKernelGGL((gn_bwd_resident<T_, V_, W>), grid, dim3(T_), sh, st, dy, x, bias,     \
-                       gamma, beta, mean, rstd, dx, dg, db, C, HW, G, act);                    \
+                       gamma, beta, mean, rstd, dx, dg, db, C, HW, G, act, addend);            \
     BPK_LAUNCH_CHECK("group_norm_bwd_resident");                                              \
     return BPK_OK;                                                                             \
   }
@@ -720,6 +733,16 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
                                       const float* rstd, float* dx, float* dgamma_nc,
                                       float* dbeta_nc, void* workspace, int N, int C, int64_t HW,
                                       int G, int act, void* stream) {
+  return bpk_group_norm_bwd_add_f32(dy, x, bias_nc, gamma, beta, mean, rstd, nullptr, dx,
+                                    dgamma_nc, dbeta_nc, workspace, N, C, HW, G, act, stream);
+}
+
+extern "C" int bpk_group_norm_bwd_add_f32(const float* dy, const float* x, const float* bias_nc,
+                                          const float* gamma, const float* beta,
+                                          const float* mean, const float* rstd,
+                                          const float* addend, float* dx, float* dgamma_nc,
+                                          float* dbeta_nc, void* workspace, int N, int C,
+                                          int64_t HW, int G, int act, void* stream) {
   BPK_REQUIRE(N >= 0 && C > 0 && HW > 0 && G > 0, "group_norm_bwd: bad shape");
   BPK_REQUIRE(C % G == 0, "group_norm_bwd: C (%d) not divisible by G (%d)", C, G);
   BPK_REQUIRE(act == 0 || act == 1, "group_norm_bwd: act must be 0 or 1");
@@ -728,14 +751,15 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
   const int64_t S = (int64_t)(C / G) * HW;
   BPK_REQUIRE(S < (1ll << 31), "group_norm_bwd: slab too large");
   hipStream_t st = bpk::as_stream(stream);
-  const bool al = is_aligned16(x) && is_aligned16(dy) && is_aligned16(dx);
+  const bool al = is_aligned16(x) && is_aligned16(dy) && is_aligned16(dx) &&
+                  (!addend || is_aligned16(addend));
   const Plan p = make_plan(S, HW, al, kBwdResidentMax);
   if (p.resident) {
     if (p.W == 4)
       return bwd_resident_dispatch<4>(S, dy, x, bias_nc, gamma, beta, mean, rstd, dx, dgamma_nc,
-                                      dbeta_nc, N, C, (int)HW, G, act, st);
+                                      dbeta_nc, N, C, (int)HW, G, act, addend, st);
     return bwd_resident_dispatch<1>(S, dy, x, bias_nc, gamma, beta, mean, rstd, dx, dgamma_nc,
-                                    dbeta_nc, N, C, (int)HW, G, act, st);
+                                    dbeta_nc, N, C, (int)HW, G, act, addend, st);
   }
   BPK_REQUIRE(workspace != nullptr, "group_norm_bwd: split path needs a workspace");
   const int cpg = C / G;
@@ -751,14 +775,14 @@ extern "C" int bpk_group_norm_bwd_f32(const float* dy, const float* x, const flo
     BPK_LAUNCH_CHECK("group_norm_bwd_partial");
     hipLaunchKernelGGL(gn_bwd_apply2<4>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
                        mean, rstd, part_ab, part_c, dx, dgamma_nc, dbeta_nc, C, (int)HW, G, CH,
-                       act);
+                       act, addend);
   } else {
     hipLaunchKernelGGL(gn_bwd_partial2<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
                        mean, rstd, part_ab, part_c, want_c, C, (int)HW, G, CH, act);
     BPK_LAUNCH_CHECK("group_norm_bwd_partial");
     hipLaunchKernelGGL(gn_bwd_apply2<1>, grid, dim3(256), 0, st, dy, x, bias_nc, gamma, beta,
                        mean, rstd, part_ab, part_c, dx, dgamma_nc, dbeta_nc, C, (int)HW, G, CH,
-                       act);
+                       act, addend);
   }
   BPK_LAUNCH_CHECK("group_norm_bwd_apply");
   return BPK_OK;

@@ -183,7 +183,7 @@ def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=N
 
 
 def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act, bias_nc=None,
-                    conv_bias=None, skip=None, div=1.0):
+                    conv_bias=None, skip=None, div=1.0, give=None, take=None):
     """gn_silu_conv under autograd for an eval-mode block (DPS: gradients of the score w.r.t.
     the input through the net): conv(SiLU(GroupNorm(x + bias_nc))) [+ residual tail] with the
     normalization inside the Winograd conv's input load and a backward that recomputes it
@@ -199,7 +199,18 @@ def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act
         return None
     return conv_op.gn_silu_conv3x3_ad(x, gn.num_groups, gn.weight if gn.affine else None,
                                       gn.bias if gn.affine else None, gn.eps, conv.weight,
-                                      conv_bias, skip, div, bias_nc)
+                                      conv_bias, skip, div, bias_nc, give, take)
+
+
+def skip_link(module: nn.Module, identity_skip: bool):
+    """A conv_op.SkipLink for a residual block whose skip is its input itself, when the block
+    is about to take the fused autograd path for both convs: the second conv then hands its
+    skip gradient to the first conv's GroupNorm backward (no separate accumulation launch)."""
+    return conv_op.SkipLink() if (_SKIP_LINK and identity_skip and not module.training
+                                  and torch.is_grad_enabled()) else None
+
+
+_SKIP_LINK = os.environ.get("BPK_SKIP_LINK", "1") == "1"  # A/B switch
 
 
 def _dropout_off(m: nn.Dropout) -> bool:
@@ -409,8 +420,10 @@ class ResnetBlockDDPM(nn.Module):
             if h is None:
                 h = conv_nobias(gn_act(x, self.GroupNorm_0, self.act), self.Conv_0)
             return self._fused_tail(h, x, None, temb)
-        h = gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act)
+        link = skip_link(self, self.in_ch == self.out_ch and _dropout_off(self.Dropout_0))
+        h = gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act, take=link)
         if h is None:
+            link = None
             h = gn_act(x, self.GroupNorm_0, self.act)
             h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
@@ -420,7 +433,7 @@ class ResnetBlockDDPM(nn.Module):
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
         if _dropout_off(self.Dropout_0):
             out = gn_silu_conv_ad(self, h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
-                                  self.Conv_1.bias, x, 1.0)
+                                  self.Conv_1.bias, x, 1.0, give=link)
             if out is not None:
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)

@@ -293,9 +293,15 @@ class ResnetBlockBigGANpp(nn.Module):
         if fused and not (self.up or self.down):
             # GroupNorm_0 + SiLU applied inside Conv_0's input load (inference)
             h = layers.gn_silu_conv(x, self.GroupNorm_0, self.Conv_0)
+        link = None
         if h is None and not (self.up or self.down):
             # eval-mode autograd (DPS): the same fusion, its backward recomputing the normalization
-            h = layers.gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act)
+            link = layers.skip_link(self, self.in_ch == self.out_ch
+                                    and layers._dropout_off(self.Dropout_0))
+            h = layers.gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act,
+                                       take=link)
+            if h is None:
+                link = None
         if h is None:
             h = gn_act(x, self.GroupNorm_0, self.act)
             h = self._resample(h)
@@ -318,7 +324,7 @@ class ResnetBlockBigGANpp(nn.Module):
                 return out
         elif layers._dropout_off(self.Dropout_0):
             out = layers.gn_silu_conv_ad(self, h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
-                                         bias, x, div)
+                                         bias, x, div, give=link)
             if out is not None:
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)

@@ -951,12 +951,21 @@ class _GNSiLUConv3x3(torch.autograd.Function):
     statistics; the weight gradient (only when the engine wants it: DPS differentiates
     w.r.t. the input alone) applies the same (s, t) in its own patch load (or, for shapes the
     Winograd weight gradient does not take, runs on the activation recomputed from them).
-    First order only (the score nets are differentiated once)."""
+    First order only (the score nets are differentiated once).
+
+    `give` / `take` (SkipLink or None): a residual block whose identity skip is the first
+    conv's input x hands the skip gradient of its second conv (`give`) to the first conv's
+    backward (`take`), which adds it in the GroupNorm backward's pass -- instead of the
+    autograd engine accumulating it into x's gradient with a separate full-size add.  The
+    engine runs the second conv's backward first (the first conv's output feeds it)."""
 
     @staticmethod
-    def forward(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats):
+    def forward(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats, give=None,
+                take=None):
         from .norm_act import group_norm_affine_stats
-        mark_inputs(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats)
+        mark_inputs(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats, give,
+                    take)
+        ctx.give, ctx.take = give, take
         ss, mean, rstd = group_norm_affine_stats(x, G, gamma, beta, eps, bias_nc)
         x = x.detach()
         if gn_partials(x) is None:
@@ -976,6 +985,8 @@ class _GNSiLUConv3x3(torch.autograd.Function):
         if ctx.div != 1.0:
             gy = gy / ctx.div
         gskip = gy if ctx.has_skip and want_grad(ctx, 6) else None
+        if gskip is not None and ctx.give is not None:
+            ctx.give.g, gskip = gskip, None  # added by the first conv's GroupNorm backward
         want_w, want_cb = want_grad(ctx, 4), ctx.has_bias and want_grad(ctx, 5)
         gw = gcb = None
         if want_w and wgrad_supported(x, tuple(w.shape)) and not _small_img(x):
@@ -991,11 +1002,17 @@ class _GNSiLUConv3x3(torch.autograd.Function):
         want_x, want_bnc = want_grad(ctx, 0), bnc is not None and want_grad(ctx, 1)
         want_g = gamma is not None and want_grad(ctx, 2)
         want_b = beta is not None and want_grad(ctx, 3)
+        addend = None
+        if ctx.take is not None:
+            addend, ctx.take.g = ctx.take.g, None
+            if not want_x:
+                addend = None  # x wants no gradient: neither did the skip that sent it
         if want_x or want_bnc or want_g or want_b:
             ga = _fwd_ft_impl(gy, w)
             dx, d_bnc, dgamma, dbeta = group_norm_act_backward(
-                ga, x, bnc, gamma, beta, mean, rstd, ctx.G, ACT_SILU, want_bnc, want_g, want_b)
-        return dx, d_bnc, dgamma, dbeta, gw, gcb, gskip, None, None, None, None
+                ga, x, bnc, gamma, beta, mean, rstd, ctx.G, ACT_SILU, want_bnc, want_g, want_b,
+                addend=addend if want_x else None)
+        return dx, d_bnc, dgamma, dbeta, gw, gcb, gskip, None, None, None, None, None, None
 
 
 def gn_silu_conv3x3_ad_supported(x, weight):
@@ -1009,8 +1026,17 @@ def gn_silu_conv3x3_ad_supported(x, weight):
                                          and 2 * weight.shape[1] <= 1024)
 
 
+class SkipLink:
+    """the gradient a residual block's second fused conv hands to its first (see
+    _GNSiLUConv3x3): one per block call"""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
 def gn_silu_conv3x3_ad(x, num_groups, gamma, beta, eps, weight, bias=None, skip=None, div=1.0,
-                       bias_nc=None):
+                       bias_nc=None, give=None, take=None):
     """(skip + conv3x3(SiLU(GroupNorm(x + bias_nc)), weight) + bias) / div, differentiable
     (first order), the normalization inside the conv's input load; the output carries
     GroupNorm partial statistics for the next GroupNorm when the 16-cin kernel runs.  None
@@ -1022,7 +1048,7 @@ def gn_silu_conv3x3_ad(x, num_groups, gamma, beta, eps, weight, bias=None, skip=
         return None
     stats = bool(wino_supported(x, weight))
     return _GNSiLUConv3x3.apply(x, bias_nc, gamma, beta, weight, bias, skip, num_groups,
-                                float(eps), float(div), stats)
+                                float(eps), float(div), stats, give, take)
 
 
 def up2_supported(x, weight):

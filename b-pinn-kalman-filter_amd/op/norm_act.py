@@ -61,9 +61,11 @@ class _GroupNormAct(Function):
 
 
 def group_norm_act_backward(dy, x, bnc, weight, bias, mean, rstd, G, act, want_bnc, want_w,
-                            want_b):
+                            want_b, addend=None):
     """(dx, d bias_nc, d gamma, d beta) of y = act(GroupNorm(x + bias_nc)) for the output
-    gradient dy, from the forward's group statistics (None where not wanted)."""
+    gradient dy, from the forward's group statistics (None where not wanted).  `addend`: another
+    consumer's gradient of x, added into dx by the same kernel (d bias_nc stays the GroupNorm
+    part alone)."""
     dy = dy.contiguous()
     N, C = x.shape[:2]
     HW = x.numel() // max(N * C, 1)
@@ -72,10 +74,19 @@ def group_norm_act_backward(dy, x, bnc, weight, bias, mean, rstd, G, act, want_b
     dg = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
     db = torch.empty((N, C), device=x.device, dtype=torch.float32) if need_affine else None
     ws = _ws(N, C, HW, G, x.device)
-    check(lib.bpk_group_norm_bwd_f32(
+    late = None  # d bias_nc sums the GroupNorm part of dx: with it, the addend comes after
+    if addend is not None:
+        addend = addend.contiguous()
+        if addend.shape != x.shape or addend.dtype != x.dtype:
+            raise RuntimeError(f"group_norm_act_backward: addend {tuple(addend.shape)} vs x "
+                               f"{tuple(x.shape)}")
+        if bnc is not None and want_bnc:
+            late, addend = addend, None
+    check(lib.bpk_group_norm_bwd_add_f32(
         dy.data_ptr(), x.data_ptr(), bnc.data_ptr() if bnc is not None else None,
         weight.data_ptr() if weight is not None else None,
         bias.data_ptr() if bias is not None else None, mean.data_ptr(), rstd.data_ptr(),
+        addend.data_ptr() if addend is not None else None,
         dx.data_ptr(), dg.data_ptr() if dg is not None else None,
         db.data_ptr() if db is not None else None, ws.data_ptr() if ws is not None else None,
         N, C, HW, G, act, stream_ptr(x.device)), "group_norm_act_bwd")
@@ -93,6 +104,8 @@ def group_norm_act_backward(dy, x, bnc, weight, bias, mean, rstd, G, act, want_b
             dw.data_ptr() if dw is not None else None,
             dbeta.data_ptr() if dbeta is not None else None, N, C, HW, stream_ptr(x.device)),
             "group_norm_param_grads")
+    if late is not None:
+        dx = late + dx
     return dx, d_bnc, dw, dbeta
 
 

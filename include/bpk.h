@@ -269,6 +269,14 @@ int bpk_group_norm_bwd_f32(const float* dy, const float* x, const float* bias_nc
                            const float* rstd, float* dx, float* dgamma_nc, float* dbeta_nc,
                            void* workspace, int N, int C, int64_t HW, int G, int act,
                            void* stream);
+/* The same backward with dx = addend + (the GroupNorm backward) when addend [N, C, HW] is not
+ * NULL: another consumer's gradient of x (a residual block's identity skip) added in the same
+ * pass instead of by a separate accumulation -- the same fp32 sum the autograd engine forms. */
+int bpk_group_norm_bwd_add_f32(const float* dy, const float* x, const float* bias_nc,
+                               const float* gamma, const float* beta, const float* mean,
+                               const float* rstd, const float* addend, float* dx, float* dgamma_nc,
+                               float* dbeta_nc, void* workspace, int N, int C, int64_t HW, int G,
+                               int act, void* stream);
 /* The parameter gradients behind that backward in one launch (NULL outputs skipped):
  * d_bias_nc [N, C] = sum over the plane of dx [N, C, HW]; dgamma / dbeta [C] = sum over n of
  * its dgamma_nc / dbeta_nc [N, C].  Fixed summation order. */

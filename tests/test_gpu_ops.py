@@ -860,6 +860,54 @@ def _count_gn_conv_ad():
     return calls
 
 
+@pytest.mark.parametrize("kind", ["biggan", "ddpm"])
+def test_skip_link_hands_the_skip_gradient_to_the_groupnorm_backward(hip, kind):
+    """A residual block with an identity skip in eval mode under autograd (DPS): with the skip
+    link (models.layers.skip_link) the second conv's skip gradient is added inside the first
+    conv's GroupNorm backward -- d/dx bit-identical to the engine's accumulation (the same fp32
+    add), one full-size add launch fewer per block."""
+    from torch.utils._python_dispatch import TorchDispatchMode
+    import models.layers as layers
+    import models.layerspp as lpp
+    torch.manual_seed(1)
+    if kind == "biggan":
+        blk = lpp.ResnetBlockBigGANpp(act=torch.nn.SiLU(), in_ch=128, out_ch=128, temb_dim=64,
+                                      skip_rescale=True, init_scale=0., dropout=0.0)
+    else:
+        blk = layers.ResnetBlockDDPM(act=torch.nn.SiLU(), in_ch=128, out_ch=128, temb_dim=64,
+                                     dropout=0.0)
+    blk = blk.to(hip).eval()
+    g = torch.Generator().manual_seed(7)
+    x0 = torch.randn(4, 128, 32, 32, generator=g).to(hip)
+    temb = torch.randn(4, 64, generator=g).to(hip)
+    gout = torch.randn(4, 128, 32, 32, generator=g).to(hip)
+
+    class Adds(TorchDispatchMode):
+        n = 0
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            if func.overloadpacket.__name__ in ("add", "add_"):
+                Adds.n += 1
+            return func(*args, **(kwargs or {}))
+
+    def dx(link):
+        old = layers._SKIP_LINK
+        layers._SKIP_LINK = link
+        try:
+            x = x0.clone().requires_grad_()
+            y = blk(x, temb)
+            Adds.n = 0
+            with Adds():
+                (gx,) = torch.autograd.grad(y, x, gout)
+            return gx, Adds.n
+        finally:
+            layers._SKIP_LINK = old
+    gl, nl = dx(True)
+    gu, nu = dx(False)
+    assert torch.equal(gl, gu)
+    assert nl == nu - 1, (nl, nu)
+
+
 @pytest.mark.parametrize("kind,cin,cout,hw", [("biggan", 128, 128, 32), ("biggan", 128, 256, 8),
                                               ("ddpm", 128, 128, 32), ("ddpm", 256, 128, 16)])
 def test_gn_silu_conv_under_autograd_matches_unfused(hip, kind, cin, cout, hw):
