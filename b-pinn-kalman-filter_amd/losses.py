@@ -335,7 +335,10 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
     step starts with zero_grad).  Under batch sharding the averaged gradient carries any
     rank's NaN, so every rank takes the same decision."""
 
+    from pinn_kalman import pinn as _pinn
+
     def loss_fn(model, operator, batch, noise=(None, None)):
+        _pinn._mark("forward")
         f1, f2, x, y, t, target = batch
         f1 = _observe(config, operator, f1, noise[0])
         f2 = _observe(config, operator, f2, noise[1])
@@ -347,10 +350,15 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
             residual = model.equation_mse_fd
         pinn_loss = (residual(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
                      * config.training.pinn_loss_weight)
+        _pinn._mark("backward")
         return pinn_loss + data_loss, pinn_loss, data_loss
 
     if graph and train:
-        return _PinnGraphStep(loss_fn, optimize_fn, ctx, config.optim.grad_clip)
+        from op import _hipenv
+        # replays are only trusted with the runtime setting of op/_hipenv.py proven in effect;
+        # otherwise (warned once) the eager step below runs instead
+        if _hipenv.graphs_allowed("get_pinn_step_fn(graph=True)"):
+            return _PinnGraphStep(loss_fn, optimize_fn, ctx, config.optim.grad_clip)
 
     bucketer = [None]  # eager + sharded: gradient buckets all-reduced during backward
 
@@ -441,9 +449,7 @@ class _PinnGraphStep:
         self.key = None
 
     def _capture(self, model, operator, batch):
-        from op import _hipenv
         from op import conv as conv_op
-        _hipenv.warn_if_unsafe("get_pinn_step_fn(graph=True)")
         dev = batch[0].device
         self.static = [b.detach().clone() for b in batch]
         for i, b in enumerate(batch):
@@ -518,15 +524,23 @@ class _PinnGraphStep:
         self.graph = g
         self.graph_b = gb_
         self.params = params
-        self.key = (id(model), tuple((b.shape, b.dtype) for b in batch))
+        # the graph recorded raw pointers: the parameters' storage and the FilterBatch's job
+        # table / transform buffers (kept alive here; a replaced weight changes the key below
+        # and forces a recapture instead of replaying into freed memory -- ADVICE r05)
+        self.filter_batch = conv_op.filter_batch_for(model)
+        self.key = self._key(model, batch)
+
+    @staticmethod
+    def _key(model, batch):
+        return (id(model), tuple((b.shape, b.dtype) for b in batch),
+                tuple(p.data_ptr() for p in model.parameters()))
 
     def __call__(self, state, operator, batch):
         model = state["model"]
         operator.next()
         opt_flow, opt_pres = state["optimizer"]
         model.train()
-        key = (id(model), tuple((b.shape, b.dtype) for b in batch))
-        if self.graph is None or key != self.key:
+        if self.graph is None or self._key(model, batch) != self.key:
             self._capture(model, operator, batch)
         # the optimizers read p.grad: point it back at the buffers the graphs write, in case a
         # caller's zero_grad(set_to_none=True) or an eager step replaced it since the last call

@@ -6,6 +6,7 @@ the fused HIP ops of `op.norm_act` (GroupNorm + bias + SiLU, residual rescale).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -120,7 +121,10 @@ _IN_FUSED = True      # InstanceNorm+ELU (+ backward, double backward) as one ke
 _GN_STATS = True      # GroupNorm partial statistics from the producing conv's epilogue
 _GEMM1X1 = True       # 1x1 convs on the MFMA GEMM kernels
 _DDPM_FUSED = True    # ResnetBlockDDPM inference on the GroupNorm-prologue Winograd convs
-_GN_CONV_AD = True    # eval-mode autograd (DPS): GroupNorm+SiLU inside the conv's input load
+# eval-mode autograd (DPS): GroupNorm+SiLU inside the conv's input load.  Its backward is
+# first-order only (once_differentiable): create_graph=True / higher derivatives through an
+# eval-mode score net need BPK_GN_CONV_AD=0 or the `higher_order_autograd()` block below
+_GN_CONV_AD = os.environ.get("BPK_GN_CONV_AD", "1") == "1"
 # the same under training (A/B switch, BPK_GN_CONV_AD_TRAIN=1)
 _GN_CONV_AD_TRAIN = os.environ.get("BPK_GN_CONV_AD_TRAIN", "0") == "1"
 
@@ -200,6 +204,21 @@ def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act
     return conv_op.gn_silu_conv3x3_ad(x, gn.num_groups, gn.weight if gn.affine else None,
                                       gn.bias if gn.affine else None, gn.eps, conv.weight,
                                       conv_bias, skip, div, bias_nc, give, take)
+
+
+@contextlib.contextmanager
+def higher_order_autograd():
+    """Inside this block eval-mode blocks record the unfused composition (every op
+    differentiable to any order) instead of the first-order-only fused GroupNorm+SiLU conv and
+    skip link: for create_graph=True / double backward through a score net (the DPS and
+    likelihood paths of the reference are first-order and do not need it)."""
+    global _GN_CONV_AD, _SKIP_LINK
+    prev = _GN_CONV_AD, _SKIP_LINK
+    _GN_CONV_AD, _SKIP_LINK = False, False
+    try:
+        yield
+    finally:
+        _GN_CONV_AD, _SKIP_LINK = prev
 
 
 def skip_link(module: nn.Module, identity_skip: bool):

@@ -25,34 +25,63 @@ shown vulnerable, covered by the setting all the same.
 from __future__ import annotations
 
 import os
-import sys
 
 GRAPH_PACKET_CAPTURE = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+
+
+def _runtime_started() -> bool:
+    """True when the ROCm runtime of this process has already initialized, i.e. holds the KFD
+    device node open.  The HIP runtime reads its DEBUG_CLR_* settings in its init, which opens
+    /dev/kfd (hipInit -> ROCr hsa_init) -- so an environment setting made while no descriptor
+    of this process points at /dev/kfd is in effect.  torch.cuda.is_initialized() is not
+    enough: torch.cuda.is_available() / device_count() start the HIP runtime without
+    initializing torch's CUDA state.  Unknowable (no /proc): assume started."""
+    try:
+        fds = os.listdir("/proc/self/fd")
+    except OSError:
+        return True
+    for fd in fds:
+        try:
+            if os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd":
+                return True
+        except OSError:
+            continue
+    return False
+
+
 _PRESET = os.environ.get(GRAPH_PACKET_CAPTURE)
+_STARTED = _runtime_started()
 os.environ.setdefault(GRAPH_PACKET_CAPTURE, "0")
-# HIP was already initialized when this module was first imported (too late for the setting to
-# take effect) -- only knowable through torch, if it is loaded
-_torch = sys.modules.get("torch")
-_LATE = _PRESET is None and _torch is not None and _torch.cuda.is_initialized()
+# the setting is proven in effect only if it was in the environment before the runtime started:
+# preset by the caller, or set here while the runtime was not yet up
+_PROVEN = _PRESET == "0" or (_PRESET is None and not _STARTED)
 
 
 def graph_replays_safe() -> bool:
-    """True when this process's hipGraph replays do not read kernel arguments from the eager
-    launch ring (the setting above is in effect)."""
-    return os.environ.get(GRAPH_PACKET_CAPTURE) == "0" and not _LATE
+    """True when this process's hipGraph replays provably do not read kernel arguments from the
+    eager launch ring (the setting above was in the environment before the runtime started)."""
+    return _PROVEN and os.environ.get(GRAPH_PACKET_CAPTURE) == "0"
 
 
-_WARNED = [False]
+_WARNED = set()
 
 
-def warn_if_unsafe(what: str) -> None:
-    if graph_replays_safe() or _WARNED[0]:
-        return
-    _WARNED[0] = True
-    import warnings
-    warnings.warn(f"{what}: this process's HIP runtime captures graph kernel packets with their "
-                  f"arguments in the eager launch ring ({GRAPH_PACKET_CAPTURE} is not 0 when the "
-                  "runtime initialized); replays may read other launches' arguments once eager "
-                  "work has filled the ring.  Import `op` (or set "
-                  f"{GRAPH_PACKET_CAPTURE}=0) before the first device call.", RuntimeWarning,
-                  stacklevel=3)
+def graphs_allowed(what: str) -> bool:
+    """The hipGraph paths (PCEngine(use_graph=True), get_pinn_step_fn(graph=True)) ask this
+    before capturing: False -- with one RuntimeWarning per caller -- when replays are not proven
+    safe, and the caller then runs its eager step instead.  Never capture-and-hope: the failure
+    the setting prevents is silently wrong results."""
+    if graph_replays_safe():
+        return True
+    if what not in _WARNED:
+        _WARNED.add(what)
+        import warnings
+        why = (f"{GRAPH_PACKET_CAPTURE}={os.environ.get(GRAPH_PACKET_CAPTURE)!r} was preset"
+               if _PRESET not in (None, "0") else
+               "the HIP runtime had started before `op` was imported")
+        warnings.warn(f"{what}: running the eager step instead of hipGraph replays ({why}; "
+                      "with graph packet capture on, replays can read other launches' kernel "
+                      "arguments from the eager launch ring).  Import `op` (or set "
+                      f"{GRAPH_PACKET_CAPTURE}=0) before the first device call -- "
+                      "INTEGRATION.md section 1.", RuntimeWarning, stacklevel=3)
+    return False

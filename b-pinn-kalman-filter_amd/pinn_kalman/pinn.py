@@ -18,6 +18,15 @@ import torch.nn as nn
 
 from models.flownet import FlowNet, PressureNet, project
 
+# diagnostics hook (tools/prof_pinn_phases.py): called with a phase name between the residual's
+# derivative passes; None in normal use
+PHASE_MARK = None
+
+
+def _mark(name):
+    if PHASE_MARK is not None:
+        PHASE_MARK(name)
+
 
 def fd_residual_mse(u, v, p, u_t, v_t, h, Re):
     """MSEs of the x/y momentum and mass residuals with spatial derivatives on the ns_step
@@ -83,13 +92,18 @@ class PINN(nn.Module):
         v = (self.mask_v * flow).sum(dim=1).unsqueeze(1)
         p = pres
         grad = torch.autograd.grad
+        _mark("d1_u")
         u_x, u_y, u_t = grad(u.sum(), (x, y, t), create_graph=True, retain_graph=True)
+        _mark("d1_v")
         v_x, v_y, v_t = grad(v.sum(), (x, y, t), create_graph=True, retain_graph=True)
+        _mark("d1_p")
         p_x, p_y = grad(p.sum(), (x, y), create_graph=True, retain_graph=True)
+        _mark("d2")
         u_xx = grad(u_x.sum(), x, retain_graph=True)[0]
         u_yy = grad(u_y.sum(), y, retain_graph=True)[0]
         v_xx = grad(v_x.sum(), x, retain_graph=True)[0]
         v_yy = grad(v_y.sum(), y, retain_graph=True)[0]
+        _mark("residual")
         u_t = u_t[:, None, None, None]
         v_t = v_t[:, None, None, None]
         nu = 1.0 / Re

@@ -428,7 +428,11 @@ class PCEngine:
         self.snr, self.n_steps = float(snr), int(n_steps)
         self.continuous, self.denoise, self.eps = continuous, denoise, eps
         self.device = torch.device(device)
-        self.use_graph = use_graph and noise_fn is None
+        from op import _hipenv
+        # hipGraph replays only with the runtime setting of op/_hipenv.py proven in effect
+        # (else, warned once, the eager step runs)
+        self.use_graph = (use_graph and noise_fn is None
+                          and _hipenv.graphs_allowed("PCEngine(use_graph=True)"))
         self.noise_fn = noise_fn
         self.dist = dist_ctx
         self.world = dist_ctx.world_size if dist_ctx is not None else 1
@@ -589,8 +593,6 @@ class PCEngine:
             self._capture_graphs(model, x, x_mean)
 
     def _capture_graphs(self, model, x, x_mean):
-        from op import _hipenv
-        _hipenv.warn_if_unsafe("PCEngine(use_graph=True)")
         # static buffers owned by the graph
         self._gx = x.clone()
         self._gxm = x_mean.clone()

@@ -1794,3 +1794,38 @@ def test_filter_batch_matches_per_weight_transforms(hip):
         y1 = conv_op.conv3x3(x, m[0].weight, m[0].bias)
     y0 = conv_op.conv3x3(x, m[0].weight, m[0].bias)
     assert torch.equal(y1, y0)
+
+
+@pytest.mark.gpu
+def test_eval_block_higher_order_autograd_opt_out(hip):
+    """The fused GroupNorm+SiLU conv of eval-mode blocks is first-order only: a double
+    backward through it raises; inside models.layers.higher_order_autograd() the block records
+    the unfused composition and the second derivative (d/dx of |d/dx|^2) matches the unfused
+    path bit for bit (same ops)."""
+    import models.layers as layers
+    import models.layerspp as lpp
+    torch.manual_seed(0)
+    blk = lpp.ResnetBlockBigGANpp(act=torch.nn.SiLU(), in_ch=64, out_ch=64, temb_dim=32,
+                                  skip_rescale=True, init_scale=0., dropout=0.0).to(hip).eval()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    x0 = torch.randn(2, 64, 16, 16, device=hip)
+    temb = torch.randn(2, 32, device=hip)
+
+    def second():
+        x = x0.clone().requires_grad_()
+        g = torch.autograd.grad(blk(x, temb).square().sum(), x, create_graph=True)[0]
+        return torch.autograd.grad(g.square().sum(), x)[0]
+    with pytest.raises(RuntimeError):
+        second()
+    with layers.higher_order_autograd():
+        a = second()
+    old = layers._GN_CONV_AD, layers._SKIP_LINK
+    layers._GN_CONV_AD, layers._SKIP_LINK = False, False
+    try:
+        b = second()
+    finally:
+        layers._GN_CONV_AD, layers._SKIP_LINK = old
+    assert torch.isfinite(a).all() and torch.equal(a, b)
+    assert layers._GN_CONV_AD  # restored
