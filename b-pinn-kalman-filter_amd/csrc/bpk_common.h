@@ -26,6 +26,16 @@ __host__ __device__ inline int floormod(int a, int b) { return a - floordiv(a, b
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// XCD-aware block order for stencil kernels: blocks are observed to be dealt round-robin over
+// the 8 XCDs (b and b + 8 share one, MI355X_MICROARCH.md), so neighbouring tiles b, b + 1 land
+// on different L2s and each XCD fetches the other's halo rows from HBM.  This bijection on
+// [0, nb) gives the blocks sharing an XCD one contiguous run of logical tiles (any nb; speed
+// only -- every tile is still processed exactly once).
+__device__ inline int64_t xcd_tile(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, xcd = b % 8, slot = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
 }  // namespace bpk
 
 #define BPK_REQUIRE(cond, ...)           \

@@ -331,7 +331,9 @@ __global__ __launch_bounds__(256) void k_fused_velocity_lds(const float* __restr
   const NsConst c(dt, dx);
   const int tid = threadIdx.x;
   const int64_t tiles_per_sample = (int64_t)tiles_x * tiles_y;
-  for (int64_t tile = blockIdx.x; tile < (int64_t)B * tiles_per_sample; tile += gridDim.x) {
+  // consecutive tiles on one XCD (shared halo rows hit its L2): bpk::xcd_tile
+  const int64_t first = bpk::xcd_tile(blockIdx.x, gridDim.x);
+  for (int64_t tile = first; tile < (int64_t)B * tiles_per_sample; tile += gridDim.x) {
     const int b = (int)(tile / tiles_per_sample);
     const int tr = (int)(tile - (int64_t)b * tiles_per_sample);
     const int x0 = (tr % tiles_x) * kTX, y0 = (tr / tiles_x) * kTY;
@@ -412,7 +414,9 @@ __global__ __launch_bounds__(256) void k_fused_pres_dens(const float* __restrict
   const float r8dt = 1.0f / (8 * dt);
   const bool ok8 = denom_ok(8 * dt);
   const int64_t total = (int64_t)B * g.hw;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+  // rows y-2 .. y+2 of a block's sites are read by its neighbours too: keep those on one XCD
+  const int64_t lb = bpk::xcd_tile(blockIdx.x, gridDim.x);
+  for (int64_t i = lb * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = i / g.hw;
     const int s = (int)(i - b * g.hw);

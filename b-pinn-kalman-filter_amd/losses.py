@@ -16,6 +16,7 @@ The PINN step functions live in pinn_kalman/.
 """
 from __future__ import annotations
 
+import os
 
 import numpy as np
 import torch
@@ -321,6 +322,22 @@ def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
     return step_fn
 
 
+# Copies of the batch the PINN residual's derivative passes run on (PINN.forward_residual_copies):
+# "auto" picks by the per-GPU batch, or a fixed 1 / 2 / 4 (1: the reference's seven passes).
+# Measured on configs[3]'s graph step (profiles/r06_pinn_copies.txt): B = 8 (a rank of the 8-GPU
+# point) 26.3 / 32.1 / 33.9 steps/s with 1 / 2 / 4 copies; B = 64 14.3 / 15.5 / 13.8.
+_COPIES = os.environ.get("BPK_PINN_COPIES", "auto")
+_COPIES_AUTO = ((16, 4), (64, 2))  # (largest per-GPU batch, copies); larger batches: 1
+
+
+def residual_copies(batch, on_gpu=True):
+    if _COPIES != "auto":
+        return int(_COPIES)
+    if not on_gpu:
+        return 1
+    return next((k for b, k in _COPIES_AUTO if batch <= b), 1)
+
+
 def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
     """Schedule 2: data losses + pinn_loss_weight * Navier-Stokes residual (Re = 1e7), both
     nets trained together; a NaN gradient on PressureNet's last 1x1 conv skips the update
@@ -342,14 +359,21 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
         f1, f2, x, y, t, target = batch
         f1 = _observe(config, operator, f1, noise[0])
         f2 = _observe(config, operator, f2, noise[1])
-        flow_pred, pres_pred = model(f1, f2, x, y, t)
+        stencil = getattr(config.training, "pinn_residual", "autograd") == "stencil"
+        copies = 1 if stencil else residual_copies(x.shape[0], f1.is_cuda)
+        if copies > 1:
+            # forward + residual with the derivative passes batched over input copies (same
+            # values and gradients, ~half the launches: PINN.forward_residual_copies)
+            flow_pred, pres_pred, res = model.forward_residual_copies(
+                f1, f2, x, y, t, 10000000.0, copies)
+        else:
+            flow_pred, pres_pred = model(f1, f2, x, y, t)
+            residual = model.equation_mse_fd if stencil else model.equation_mse
         data_loss = (model.flownet.multiscale_data_mse(flow_pred, target)
                      + model.pressurenet.data_mse(pres_pred, target))
-        residual = model.equation_mse
-        if getattr(config.training, "pinn_residual", "autograd") == "stencil":
-            residual = model.equation_mse_fd
-        pinn_loss = (residual(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
-                     * config.training.pinn_loss_weight)
+        if copies == 1:
+            res = residual(x, y, t, flow_pred[-1], pres_pred, 10000000.0)
+        pinn_loss = res * config.training.pinn_loss_weight
         _pinn._mark("backward")
         return pinn_loss + data_loss, pinn_loss, data_loss
 

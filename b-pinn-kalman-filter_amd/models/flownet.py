@@ -17,6 +17,7 @@ Call sites of the native ops: `project` -> op.grid_sample.grid_sample_2d
 from __future__ import annotations
 
 import functools
+import os
 
 import torch
 import torch.nn as nn
@@ -28,6 +29,8 @@ from op.fused_act import LeakyReLU, leaky_relu
 from . import layers
 
 _BASE_GRIDS: dict = {}
+# FlowNet: the two frames' feature pyramids as one batch (A/B switch; tests flip it)
+_PAIR_FRAMES = os.environ.get("BPK_PAIR_FRAMES", "1") == "1"
 
 
 def _base_grid(shape, device):
@@ -136,6 +139,21 @@ class FeatureExtractor(nn.Module):
             pyramid.append(f)
         return pyramid
 
+    def forward_frames(self, frames, emb):
+        """The pyramids of k frames [k, B, C, H, W] (stacked along the batch) in one pass per
+        level: the same weights and embeddings for every frame, so each conv / activation runs
+        once at batch k*B instead of k times at B -- in the forward and in every derivative
+        pass of the PINN residual.  Per-sample arithmetic and the reference's add order
+        ((f + semb) + temb, broadcast over the frames); returns k pyramids."""
+        k, B = frames.shape[0], frames.shape[1]
+        f = frames.reshape((k * B,) + tuple(frames.shape[2:]))
+        levels = []
+        for level, (semb, temb) in zip(self.feature_extractors, emb):
+            h = f.view((k, B) + tuple(f.shape[1:])) + semb[None] + temb[None]
+            f = level(h.view((k * B,) + tuple(f.shape[1:])))
+            levels.append(channels.split(f, (B,) * k, 0))
+        return [list(p) for p in zip(*levels)]
+
 
 class Matching(nn.Module):
     """Cost-volume flow estimate at one level (reference flownet.py:93-121)."""
@@ -208,8 +226,12 @@ class FlowNet(nn.Module):
 
     def forward(self, f1, f2, x, y, t, size=None):
         emb = self.feature_extractor.embeddings(x, y, t, f1.shape[1])
-        p1 = self.feature_extractor(f1, x, y, t, emb)
-        p2 = self.feature_extractor(f2, x, y, t, emb)
+        if _PAIR_FRAMES and f1.is_cuda:
+            # both frames through the shared extractor as one batch (forward_frames)
+            p1, p2 = self.feature_extractor.forward_frames(torch.stack([f1, f2]), emb)
+        else:
+            p1 = self.feature_extractor(f1, x, y, t, emb)
+            p2 = self.feature_extractor(f2, x, y, t, emb)
         flows, flow = [], None
         for unit in self.inference_units:
             flow = unit(p1[unit.level], p2[unit.level], flow)

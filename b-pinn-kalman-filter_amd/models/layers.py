@@ -304,10 +304,38 @@ def get_timestep_embedding(timesteps, embedding_dim, max_positions=10000):
     return emb
 
 
+_SPATIAL_GROUPS = 1  # batch = this many independent copies (spatial_groups)
+
+
+@contextlib.contextmanager
+def spatial_groups(k):
+    """Inside this block the batch of get_spatial_embedding is k stacked copies of one batch
+    (pinn.PINN.forward_residual_copies): x.max() / y.max() -- which couple the samples of a
+    batch -- are taken per copy, so every copy computes (and differentiates) exactly what the
+    single batch would."""
+    global _SPATIAL_GROUPS
+    prev, _SPATIAL_GROUPS = _SPATIAL_GROUPS, int(k)
+    try:
+        yield
+    finally:
+        _SPATIAL_GROUPS = prev
+
+
+def _max_minus(v):
+    """v.max() - v, the max per copy under spatial_groups(k) (ties share the gradient evenly
+    within a copy, as max() does over one batch)."""
+    k = _SPATIAL_GROUPS
+    if k == 1:
+        return v.max() - v
+    g = v.reshape((k, v.shape[0] // k) + tuple(v.shape[1:]))
+    m = g.reshape(k, -1).amax(1).view((k,) + (1,) * (g.dim() - 1))
+    return (m - g).reshape(v.shape)
+
+
 def get_spatial_embedding(x, y, omega, s=1.0):
     """Spatial embedding of the PINN nets (reference layers.py:517-521)."""
     e1 = torch.sin(omega * torch.sqrt(x ** 2 + y ** 2))
-    e2 = torch.sin(omega * torch.sqrt((x.max() - x) ** 2 + (y.max() - y) ** 2))
+    e2 = torch.sin(omega * torch.sqrt(_max_minus(x) ** 2 + _max_minus(y) ** 2))
     return (e1 + e2) / s
 
 

@@ -54,6 +54,14 @@ def cat(tensors, dim=0):
     return _Cat.apply(dim % tensors[0].dim(), *tensors)
 
 
+def split(x, sizes, dim=0):
+    """torch.split(x, sizes, dim) whose backward is one cat (and that cat's backward a split)."""
+    sizes = tuple(int(v) for v in sizes)
+    if not torch.is_grad_enabled() or not x.requires_grad:
+        return tuple(torch.split(x, list(sizes), dim))
+    return _Split.apply(x, dim % x.dim(), sizes)
+
+
 class _SwapScale(Function):
     """out[:, 0] = u[:, 1] / c0, out[:, 1] = u[:, 0] / c1 for u [B, 2, ...]: a linear map whose
     adjoint is the same map with the divisors exchanged."""

@@ -31,8 +31,10 @@ def test_hip_runtime_setting_in_effect():
     assert _hipenv.graph_replays_safe()
 
 
-def test_pinn_graph_step_with_eval_steps_and_reductions_matches_eager_b64(hip):
-    """The bench configuration (configs[3], B = 64): 5 train steps as hipGraph replays with, after
+@pytest.mark.parametrize("B", [64, 8])
+def test_pinn_graph_step_with_eval_steps_and_reductions_matches_eager_b64(hip, B):
+    """The bench configuration (configs[3], B = 64; B = 8: a rank of the 8-GPU point, whose
+    step batches the residual's derivative passes over input copies): 5 train steps as hipGraph replays with, after
     each, an eager eval step (get_pinn_step_fn(train=False): EMA store / copy_to / restore and a
     forward with the residual), device reductions of every gradient, a large-argument launch
     flood and zero_grad(set_to_none=True) -- vs the same loop with the eager train step: train
@@ -48,7 +50,7 @@ def test_pinn_graph_step_with_eval_steps_and_reductions_matches_eager_b64(hip):
     c.device = hip
     torch.manual_seed(0)
     m0 = PINN(c)
-    B, n, steps = 64, c.data.image_size, 5
+    n, steps = c.data.image_size, 5
     g = torch.Generator().manual_seed(2)
     lin = torch.linspace(0.05, 1.0, n)
 

@@ -13,7 +13,11 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO, os.path.join(REPO, "tools")]
 
-PHASES = ["forward", "d1_u", "d1_v", "d1_p", "d2", "residual", "backward"]
+# the residual's derivative passes: the reference's seven (BPK_PINN_COPIES=1) or batched over
+# input copies (PINN.forward_residual_copies: one first-order pass, one / two second-order)
+PHASES = (["forward", "d1_u", "d1_v", "d1_p", "d2", "residual", "backward"]
+          if os.environ.get("BPK_PINN_COPIES") == "1" else
+          ["forward", "d1", "d2", "residual", "backward"])
 
 if len(sys.argv) > 2 and sys.argv[1] == "--split":
     from trace_steps import short

@@ -10,6 +10,7 @@ import traceback
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
+from op import _hipenv  # noqa: E402,F401
 import torch  # noqa: E402
 from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
 
@@ -51,8 +52,9 @@ def counted(fn, dev):
 
 bench.counted = counted
 which = sys.argv[1]
+extra = sys.argv[2:]  # e.g. --per-rank-of 8
 sys.argv = ["bench.py", "--cifar-steps", "1", "--pinn-steps", "1", "--pinn-warmup", "1",
-            "--dps-steps", "1"]
+            "--dps-steps", "1"] + extra
 args = bench.parse()
 ctx = dist.init_from_env()
 dev = torch.device("cuda", 0)
