@@ -123,11 +123,12 @@ class FeatureExtractor(nn.Module):
         both frames, so FlowNet computes them once (the reference builds them per frame:
         identical values, and every derivative pass of the PINN residual then runs through
         one copy of the sin / sqrt / pool chain instead of two)."""
-        out, semb, c = [], self.spatial_emb(x, y), channels_in
-        for level in self.feature_extractors:
-            out.append((semb, layers.get_timestep_embedding(t, c)[:, :, None, None]))
+        dims = [channels_in] + [level[-2].out_channels for level in self.feature_extractors][:-1]
+        tembs = layers.get_timestep_embeddings(t, dims)  # every level's in one chain
+        out, semb = [], self.spatial_emb(x, y)
+        for temb in tembs:
+            out.append((semb, temb[:, :, None, None]))
             semb = self.semb_down(semb)
-            c = level[-2].out_channels
         return out
 
     def forward(self, f, x, y, t, emb=None):

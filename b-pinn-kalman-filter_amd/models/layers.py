@@ -291,12 +291,27 @@ def conv_nobias(x, conv: nn.Conv2d):
     return conv2d(x, conv, bias=False)
 
 
+_FREQS: dict = {}
+
+
+def _freqs(half, max_positions, device):
+    """exp(arange(half) * -log(max_positions) / (half - 1)) as the reference computes it, once per
+    (half, device): a constant of the net (three launches per call otherwise, recorded into the
+    PINN step's graph at every level)."""
+    key = (half, max_positions, str(device))
+    f = _FREQS.get(key)
+    if f is None:
+        rate = math.log(max_positions) / (half - 1)
+        f = torch.exp(torch.arange(half, dtype=torch.float32, device=device) * -rate)
+        _FREQS[key] = f
+    return f
+
+
 def get_timestep_embedding(timesteps, embedding_dim, max_positions=10000):
     """Sinusoidal embedding (reference layers.py:500-514)."""
     assert timesteps.ndim == 1
     half = embedding_dim // 2
-    rate = math.log(max_positions) / (half - 1)
-    freqs = torch.exp(torch.arange(half, dtype=torch.float32, device=timesteps.device) * -rate)
+    freqs = _freqs(half, max_positions, timesteps.device)
     arg = timesteps.float()[:, None] * freqs[None, :]
     emb = channels.cat([torch.sin(arg), torch.cos(arg)], dim=1)  # = torch.cat, any derivative order
     if embedding_dim % 2 == 1:
@@ -332,8 +347,46 @@ def _max_minus(v):
     return (m - g).reshape(v.shape)
 
 
+_SEMB_FUSED = os.environ.get("BPK_SEMB_FUSED", "1") == "1"  # A/B switch
+_RES_TAIL = os.environ.get("BPK_RES_TAIL", "1") == "1"  # ResidualBlock: skip add in conv2
+
+
+def get_timestep_embeddings(timesteps, dims, max_positions=10000):
+    """[get_timestep_embedding(timesteps, d) for d in dims] (the same values) with one product,
+    one sin and one cos for all of them: FlowNet embeds t at every pyramid level, and the PINN
+    residual differentiates each embedding w.r.t. t (u_t, v_t) -- per level a chain of
+    launches in every pass, here one."""
+    assert timesteps.ndim == 1
+    halves = [d // 2 for d in dims]
+    parts = [h for h in halves if h > 0]
+    out = [None] * len(dims)
+    if parts:
+        key = ("cat", tuple(parts), max_positions, str(timesteps.device))
+        freqs = _FREQS.get(key)
+        if freqs is None:
+            freqs = torch.cat([_freqs(h, max_positions, timesteps.device) for h in parts])
+            _FREQS[key] = freqs
+        arg = timesteps.float()[:, None] * freqs[None, :]
+        sins = iter(channels.split(torch.sin(arg), parts, 1))
+        coss = iter(channels.split(torch.cos(arg), parts, 1))
+    for i, (d, h) in enumerate(zip(dims, halves)):
+        if h > 0:
+            emb = channels.cat([next(sins), next(coss)], dim=1)
+        else:
+            emb = timesteps.new_zeros((timesteps.shape[0], 0), dtype=torch.float32)
+        if d % 2 == 1:
+            emb = F.pad(emb, (0, 1), mode="constant")
+        out[i] = emb
+    return out
+
+
 def get_spatial_embedding(x, y, omega, s=1.0):
-    """Spatial embedding of the PINN nets (reference layers.py:517-521)."""
+    """Spatial embedding of the PINN nets (reference layers.py:517-521).  On HIP tensors: one
+    native op with its first and second derivatives (op.embedding; the same forward bits)."""
+    if _SEMB_FUSED and x.is_cuda:
+        from op import embedding
+        if embedding.supported(x, y, _SPATIAL_GROUPS):
+            return embedding.spatial_embedding(x, y, omega, s, _SPATIAL_GROUPS)
     e1 = torch.sin(omega * torch.sqrt(x ** 2 + y ** 2))
     e2 = torch.sin(omega * torch.sqrt(_max_minus(x) ** 2 + _max_minus(y) ** 2))
     return (e1 + e2) / s
@@ -596,6 +649,10 @@ class ResidualBlock(nn.Module):
 
     def forward(self, x):
         h = self.conv1(self._norm_act(self.normalize1, x))
-        h = self.conv2(self._norm_act(self.normalize2, h))
         skip = x if self.output_dim == self.input_dim else self.shortcut(x)
-        return skip + h
+        a = self._norm_act(self.normalize2, h)
+        if _RES_TAIL and _is_3x3(a, self.conv2):
+            # skip + conv2(a) with the add in the conv's epilogue (same rounding: the kernel
+            # forms conv + bias, then skip + that); its gradient w.r.t. skip is gy itself
+            return conv_op.conv3x3(a, self.conv2.weight, self.conv2.bias, skip=skip)
+        return skip + self.conv2(a)

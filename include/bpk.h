@@ -296,6 +296,28 @@ int bpk_swap_scale_f32(const float* u, float* out, int64_t N, int64_t P, float c
  * autograd -- the input gradient of bpk_conv3x3_wino_up2_f32's fused upsample + conv). */
 int bpk_sum2x2_f32(const float* x, float* y, int64_t planes, int H, int W, void* stream);
 
+/* The PINN nets' spatial embedding f = (sin(w |(x, y)|) + sin(w |(mx - x, my - y)|)) / s,
+ * mx / my the max of x / y over each of k copies of the batch (reference models/layers.py:
+ * 517-521, get_spatial_embedding; copies: pinn.PINN.forward_residual_copies), with its first
+ * (vjp: (g f_x, g f_y) + the max's evenly shared gradient) and second derivatives (vjp2: the
+ * cotangent (hx, hy) of the vjp's outputs mapped to (dg, dx, dy); hx / hy / dg / dx / dy may be
+ * NULL) -- one reduction launch + one elementwise launch each, the forward bit-identical to the
+ * reference's aten op sequence.  x, y, out, g, ... hold n floats; n / k must be a multiple of
+ * 256 (bpk_spatial_emb_supported); mxy [k][2] is written by the forward and read by the
+ * derivatives; workspace: bpk_spatial_emb_workspace_bytes(n, k). */
+int bpk_spatial_emb_supported(int64_t n, int k);
+int64_t bpk_spatial_emb_workspace_bytes(int64_t n, int k);
+int bpk_spatial_emb_fwd_f32(const float* x, const float* y, float* out, float* mxy,
+                            float* workspace, int64_t n, int k, float omega, float s,
+                            void* stream);
+int bpk_spatial_emb_vjp_f32(const float* x, const float* y, const float* mxy, const float* g,
+                            float* gx, float* gy, float* workspace, int64_t n, int k, float omega,
+                            float s, void* stream);
+int bpk_spatial_emb_vjp2_f32(const float* x, const float* y, const float* mxy, const float* g,
+                             const float* hx, const float* hy, float* dg, float* dx, float* dy,
+                             float* workspace, int64_t n, int k, float omega, float s,
+                             void* stream);
+
 /* out[n,c,:] = (x + (h + bias[c])) / div -- the skip_rescale residual of the
  * BigGAN / DDPM++ blocks with Conv_1's bias folded in (models/layerspp.py:266-274,
  * :200-209).  bias may be NULL.  x, h, out: [N, C, HW]. */

@@ -342,3 +342,45 @@ def test_pinn_step_hip_graph_replays_match_eager(hip):
     # every parameter by O(lr) per step
     for a, b in zip(pg + eg, pe + ee):
         assert (a - b).abs().max().item() <= 4e-3
+
+
+@pytest.mark.parametrize("k,ties", [(1, False), (2, False), (4, True)])
+def test_spatial_embedding_native_matches_aten_chain(hip, k, ties):
+    """op.embedding (the PINN nets' spatial embedding with its first and second derivatives as
+    native launches) vs the reference's aten op chain (layers.get_spatial_embedding with the
+    fused path off), k stacked copies with a per-copy max (layers.spatial_groups): forward bit
+    for bit; then the residual's derivative pattern -- first derivatives w.r.t. x, y with
+    create_graph, second derivatives w.r.t. x, y of a weighted sum of them, and that sum's
+    gradient w.r.t. an upstream weight W (the path the final backward takes to the
+    parameters) -- within 2e-5 of each tensor's max.  ties: the max repeated inside a copy
+    (its gradient is shared evenly, as max() does)."""
+    import models.layers as layers
+    g = torch.Generator().manual_seed(10 * k + ties)
+    B, n = 2 * k, 64
+    lin = torch.linspace(0.05, 1.0, n)
+    x0 = lin.view(1, 1, 1, n) + 0.01 * torch.rand(B, 1, n, n, generator=g)
+    y0 = lin.view(1, 1, n, 1) + 0.01 * torch.rand(B, 1, n, n, generator=g)
+    if ties:
+        x0[0, 0, 3, 5] = x0[0, 0, 7, 9] = x0.view(k, -1)[0].max() + 0.01
+    w0 = torch.randn(B, 1, n, n, generator=g)
+    a0, b0 = torch.randn(B, 1, n, n, generator=g), torch.randn(B, 1, n, n, generator=g)
+    x0, y0, w0, a0, b0 = (v.to(hip) for v in (x0, y0, w0, a0, b0))
+
+    def run(fused):
+        old = layers._SEMB_FUSED
+        layers._SEMB_FUSED = fused
+        try:
+            x, y, W = (v.clone().requires_grad_() for v in (x0, y0, w0))
+            with layers.spatial_groups(k):
+                e = layers.get_spatial_embedding(x, y, 3.0, 2.5)
+            gx, gy = torch.autograd.grad((e * W).sum(), (x, y), create_graph=True)
+            l2 = (gx * a0 + gy * b0).sum()
+            d2x, d2y, dW = torch.autograd.grad(l2, (x, y, W))
+        finally:
+            layers._SEMB_FUSED = old
+        return [t.detach() for t in (e, gx, gy, d2x, d2y, dW)]
+    fz, ref = run(True), run(False)
+    assert torch.equal(fz[0], ref[0]), "forward not bit-identical"
+    for name, a, b in zip(("gx", "gy", "d2x", "d2y", "dW"), fz[1:], ref[1:]):
+        err = (a - b).abs().max().item() / b.abs().max().item()
+        assert err <= 2e-5, f"{name}: {err:.3e}"

@@ -104,3 +104,32 @@ def test_inpaint_operator_gather_matches_dense_selection():
     np.testing.assert_array_equal(back.numpy(), (masks[0] * x).numpy())
     op.next()
     assert op.mask is masks[1]
+
+
+def test_batched_timestep_embeddings_equal_per_level_calls():
+    """layers.get_timestep_embeddings (FlowNet's per-level embeddings as one product / sin / cos)
+    == get_timestep_embedding per level as the reference computes it (models/layers.py:500-514),
+    bit for bit, odd and one-channel dims included; and the same gradient w.r.t. t."""
+    import math
+
+    import models.layers as L
+    t = torch.tensor([300., 512., 899., 301.], requires_grad=True)
+    dims = [1, 16, 32, 64, 96, 7]
+    got = L.get_timestep_embeddings(t, dims)
+    ref = []
+    for d in dims:
+        half = d // 2
+        rate = math.log(10000) / (half - 1)
+        fr = torch.exp(torch.arange(half, dtype=torch.float32) * -rate)
+        arg = t.float()[:, None] * fr[None, :]
+        r = torch.cat([torch.sin(arg), torch.cos(arg)], 1)
+        if d % 2:
+            r = torch.nn.functional.pad(r, (0, 1))
+        ref.append(r)
+        assert torch.equal(L.get_timestep_embedding(t, d), r)
+    w = [torch.randn(r.shape, generator=torch.Generator().manual_seed(i)) for i, r in enumerate(ref)]
+    for a, b in zip(got, ref):
+        assert a.shape == b.shape and torch.equal(a, b)
+    ga = torch.autograd.grad(sum((a * v).sum() for a, v in zip(got, w)), t)[0]
+    gb = torch.autograd.grad(sum((b * v).sum() for b, v in zip(ref, w)), t)[0]
+    torch.testing.assert_close(ga, gb, rtol=1e-6, atol=1e-6)

@@ -20,7 +20,14 @@ PHASES = (["forward", "d1_u", "d1_v", "d1_p", "d2", "residual", "backward"]
           ["forward", "d1", "d2", "residual", "backward"])
 
 if len(sys.argv) > 2 and sys.argv[1] == "--split":
-    from trace_steps import short
+    import re
+
+    def short(n):  # as tools/trace_steps.py
+        n = n.replace("(anonymous namespace)::", "")
+        if "at::native" in n:
+            m = re.search(r"at::native::(?:\(anonymous namespace\)::)?(\w+)<[^,]*,\s*at::native::([\w:]+)", n)
+            return "aten:" + (m.group(2) if m else n[:60])
+        return n.split("(")[0][:70]
     rows = list(csv.DictReader(open(sys.argv[2])))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     marks = [i for i, e in enumerate(ev) if "sleep" in e[2].lower() or "spin" in e[2].lower()]
