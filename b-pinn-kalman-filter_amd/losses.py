@@ -325,9 +325,10 @@ def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
 # Copies of the batch the PINN residual's derivative passes run on (PINN.forward_residual_copies):
 # "auto" picks by the per-GPU batch, or a fixed 1 / 2 / 4 (1: the reference's seven passes).
 # Measured on configs[3]'s graph step (profiles/r06_pinn_copies.txt): B = 8 (a rank of the 8-GPU
-# point) 26.3 / 32.1 / 33.9 steps/s with 1 / 2 / 4 copies; B = 64 14.3 / 15.5 / 13.8.
+# point) 26.3 / 32.1 / 33.9 steps/s with 1 / 2 / 4 copies; B = 32 20.7 / 21.4 with 2 / 4;
+# B = 64 14.3 / 15.5 / 13.8 with 1 / 2 / 4 (profiles/r06_pinn_copies.txt).
 _COPIES = os.environ.get("BPK_PINN_COPIES", "auto")
-_COPIES_AUTO = ((16, 4), (64, 2))  # (largest per-GPU batch, copies); larger batches: 1
+_COPIES_AUTO = ((32, 4), (64, 2))  # (largest per-GPU batch, copies); larger batches: 1
 
 
 def residual_copies(batch, on_gpu=True):
