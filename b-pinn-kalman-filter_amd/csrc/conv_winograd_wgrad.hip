@@ -416,7 +416,15 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
   if (db && blockIdx.x == 0) {  // db[cout] = sum over splits, fixed order
     for (int i = threadIdx.x; i < Cout; i += blockDim.x) {
       float acc = 0.f;
-      for (int sp = 0; sp < splits; ++sp) acc += part_b[(int64_t)sp * Cout + i];
+      int sp = 0;
+      for (; sp + 7 < splits; sp += 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = part_b[(int64_t)(sp + u) * Cout + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += t[u];
+      }
+      for (; sp < splits; ++sp) acc += part_b[(int64_t)sp * Cout + i];
       db[i] = acc;
     }
   }
@@ -424,9 +432,20 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_kernel(const float* __r
   const int64_t i = (int64_t)blockIdx.x * 16 + (col >> 2);  // pair
   const int q = col & 3;
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-  if (i < pairs)
-    for (int s = grp; s < splits; s += 4)
+  if (i < pairs) {
+    // eight loads in flight per thread, added in split order (the same sum)
+    int s = grp;
+    for (; s + 28 < splits; s += 32) {
+      f4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = *reinterpret_cast<const f4*>(part + ((int64_t)(s + 4 * u) * pairs + i) * 16 + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; s < splits; s += 4)
       acc += *reinterpret_cast<const f4*>(part + ((int64_t)s * pairs + i) * 16 + 4 * q);
+  }
   red[grp][col] = acc;
   __syncthreads();
   if (grp == 0) red[0][col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
@@ -476,7 +495,10 @@ WgradGeo make_geo(int N, int Cin, int Cout, int H, int W) {
   const int64_t tiles = (int64_t)g.cin_blocks * g.cout_blocks;
   const int64_t target = nb == 1 ? 512 : 256;
   const int64_t want = std::max<int64_t>(1, (target + tiles - 1) / tiles);
-  g.splits = (int)std::min<int64_t>(want, g.chunks);
+  // at least 8 chunks per split: with 1-2 per split the small-image shapes (the PINN's 64^2
+  // levels at 8 samples per GPU) were all prologue and partial-slab traffic -- round 6,
+  // tools/bench_wgrad3x3.py: B = 8 shapes 776 -> 654 us in sum, B = 64 unchanged
+  g.splits = (int)std::max<int64_t>(1, std::min<int64_t>(want, g.chunks / 8));
   return g;
 }
 

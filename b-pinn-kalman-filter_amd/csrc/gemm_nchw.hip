@@ -314,15 +314,34 @@ __global__ __launch_bounds__(256) void gemm_wgrad_reduce_kernel(
   const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + col;
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-  if (i < n4)
-    for (int s = grp; s < splits; s += 4) acc += part[(int64_t)s * n4 + i];
+  if (i < n4) {
+    // eight loads in flight per thread (the adds stay in split order: the same sum); one at a
+    // time, hundreds of splits made this kernel latency-bound (~90 us on PressureNet shapes)
+    int s = grp;
+    for (; s + 28 < splits; s += 32) {
+      f4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(s + 4 * u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; s < splits; s += 4) acc += part[(int64_t)s * n4 + i];
+  }
   red[grp][col] = acc;
   __syncthreads();
   if (grp == 0 && i < n4) out[i] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
   if (ob != nullptr && blockIdx.x == 0)
     for (int m = threadIdx.x; m < M; m += 256) {
       float v = 0.f;
-      for (int s = 0; s < splits; ++s) v += part_b[(int64_t)s * M + m];
+      int s = 0;
+      for (; s + 7 < splits; s += 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = part_b[(int64_t)(s + u) * M + m];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += t[u];
+      }
+      for (; s < splits; ++s) v += part_b[(int64_t)s * M + m];
       ob[m] = v;
     }
 }
@@ -331,9 +350,12 @@ WgGeo wgrad_geo(int N, int M, int K, int P) {
   WgGeo g{N, M, K, P, (M + kBM - 1) / kBM, (K + kBM - 1) / kBM, 1, 0};
   const int64_t chunks = (int64_t)N * (P / kKC);
   const int tiles = g.tiles_m * g.tiles_k;
-  // ~1024 workgroups (4 per CU), at least 64 chunks (1024 pixels) per split
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(bpk::ceil_div(1024, tiles),
-                                                          chunks / 64));
+  // ~1024 workgroups (4 per CU), at least 8 chunks (128 pixels) per split, at most 256 splits
+  // (PressureNet's 1x1 shortcuts, tools/bench_wgrad1x1.py, round 6: 64 chunks per split left
+  // 32-128 workgroups on the chip at B = 8, ~95 us a call; now 20-34 us; B = 64 1.66 -> ~1.0
+  // ms over the shapes)
+  int64_t splits = std::max<int64_t>(
+      1, std::min<int64_t>(std::min<int64_t>(bpk::ceil_div(1024, tiles), 256), chunks / 8));
   g.cps = (int)bpk::ceil_div(chunks, splits);
   g.splits = (int)bpk::ceil_div(chunks, (int64_t)g.cps);  // every split non-empty
   return g;
