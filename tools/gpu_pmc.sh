@@ -4,11 +4,14 @@
 # tools/pmc_summary.py gpurun_out/pmc_$TAG $TAG on the same tree: it records the kernel
 # sources' sha1, which bench.py checks before it uses an entry).
 # $1 = kernels (single-kernel passes) | steps (whole-step traffic; $2 = modes)
-TAG=${TAG:-r04}
+TAG=${TAG:-r06}
 D=gpurun_out/pmc_$TAG
-# the kernel-argument pool at 64 MB: with the default pool rocprofv3 --pmc died with SIGSEGV
-# inside a launch at a pool boundary on the PINN and DPS steps (rounds 4-5)
-export HSA_KERNARG_POOL_SIZE=${HSA_KERNARG_POOL_SIZE:-67108864}
+# the profiler's preloaded library starts the HIP runtime before Python runs: the graph
+# packet-capture setting must come from the environment (op/_hipenv.py is too late there).
+# Rounds 4-5 ran without it and needed a 64 MB kernel-argument pool to keep the PINN / DPS
+# passes from dying with SIGSEGV inside a launch; with the setting in effect the DPS pass runs
+# at the default pool (round 6, profiles/r06_pmc_dps_default_pool.txt)
+export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
 mkdir -p $D; export TMPDIR=/tmp
 run() {  # script mode group counters...
   local script=$1 mode=$2 grp=$3; shift 3

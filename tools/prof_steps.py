@@ -5,14 +5,18 @@ marker dispatch of fused_bias_act_kernel<double> on 256 values (an instance no b
 launches: FlowNet's LeakyReLU runs the float one).
 tools/pmc_summary.py sums FETCH_SIZE / WRITE_SIZE over the dispatches between the markers.
 The PINN phase runs its eager step (--pinn-eager): the counted step is eager in either mode.
-Run the passes with HSA_KERNARG_POOL_SIZE=67108864: round 4's PINN / DPS passes died with
-SIGSEGV inside a kernel launch at a kernel-argument-pool boundary (rocprofv3 copying a launch's
-arguments; the 64 MB pool moved past it in round 5)."""
+Under rocprofv3 --pmc the profiler's preloaded library starts the HIP runtime before Python
+runs, so DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 must be exported by the shell (op/_hipenv.py cannot set
+it in time, and with it unset the graph phases fall back to their eager steps).  Rounds 4-5
+ran without it and their PINN / DPS passes died with SIGSEGV inside a kernel launch at a
+kernel-argument-pool boundary, sidestepped with HSA_KERNARG_POOL_SIZE=67108864 (DESIGN.md
+section 6 for what round 6 found)."""
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "b-pinn-kalman-filter_amd"), REPO]
+from op import _hipenv  # noqa: E402,F401
 import torch  # noqa: E402
 
 import bench  # noqa: E402
