@@ -98,7 +98,7 @@ class DDPM(nn.Module):
         else:
             temb = None
         fused = layers._DDPM_FUSED and layers.fused_inference_ok(self, x, self.act)
-        if temb is not None and fused:
+        if temb is not None and x.is_cuda and (fused or layers._TEMB_BANK_AD):
             # every block's Dense_0 projection of act(temb) as one GEMM (layers.TembBank)
             temb = layers.TembBank(temb, self.act, [m.Dense_0 for m in mods
                                                     if isinstance(m, layers.ResnetBlockDDPM)])

@@ -41,27 +41,37 @@ def dense(m: nn.Linear, x):
     return m(x)
 
 
+# the bank under autograd too (training, DPS); A/B switch
+_TEMB_BANK_AD = os.environ.get("BPK_TEMB_BANK_AD", "1") == "1"
+
+
 class TembBank:
-    """act(temb) projected by every residual block's Dense_0 at once (inference): one
-    concatenation of the weights and one GEMM per forward instead of ~34 latency-bound
-    [B, 4 nf] x [4 nf, C] Linear launches.  Built per forward from the live weights (no
-    cache to go stale when EMA / load_state_dict rewrite them)."""
+    """act(temb) projected by every residual block's Dense_0 at once: one concatenation of the
+    weights and one GEMM per forward instead of ~34 latency-bound [B, 4 nf] x [4 nf, C] Linear
+    launches (and one SiLU instead of one per block).  Under autograd the backward is then
+    one GEMM per gradient too (the weight gradients of all blocks in one launch, split back
+    into each Dense_0's as views), instead of three launches and an add per block.  Built per
+    forward from the live weights (no cache to go stale when EMA / load_state_dict / an
+    optimizer step rewrite them).  The same values as per-block Linear calls: each output is
+    the same dot product over the same K order."""
 
     def __init__(self, temb, act, denses):
-        self._off = {}
-        off = 0
-        for d in denses:
-            self._off[id(d)] = (off, d.out_features)
-            off += d.out_features
-        w = torch.cat([d.weight for d in denses], 0)
-        b = torch.cat([d.bias for d in denses], 0)
+        self._idx = {}
+        sizes = []
+        for i, d in enumerate(denses):
+            self._idx[id(d)] = i
+            sizes.append(d.out_features)
+        w = channels.cat([d.weight for d in denses], 0)
+        b = channels.cat([d.bias for d in denses], 0)
         a = act(temb)
-        self.all = (matmul_op.linear(a, w, b) if a.is_cuda and matmul_op.supported(a, w, b)
-                    else torch.addmm(b, a, w.t()))
+        allp = (matmul_op.linear(a, w, b) if a.is_cuda and matmul_op.supported(a, w, b)
+                else torch.addmm(b, a, w.t()))
+        # per-block views; under autograd one split (its backward: one concatenation) rather
+        # than a slice per block (a zero-filled full-size gradient per slice, then the adds)
+        self.parts = channels.split(allp, sizes, 1)
 
     def proj(self, dense):
-        off, n = self._off[id(dense)]
-        return self.all[:, off:off + n]
+        return self.parts[self._idx[id(dense)]]
 
 
 def temb_proj(dense_m: nn.Linear, act, temb):

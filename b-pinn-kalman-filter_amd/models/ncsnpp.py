@@ -214,7 +214,8 @@ class NCSNpp(nn.Module):
     def forward(self, x, time_cond):
         mods = self.all_modules
         temb, used_sigmas = self._time_embedding(time_cond)
-        if temb is not None and _TEMB_BANK and layers.fused_inference_ok(self, x, self.act):
+        if temb is not None and _TEMB_BANK and x.is_cuda and (
+                layers._TEMB_BANK_AD or layers.fused_inference_ok(self, x, self.act)):
             if self._denses is None:
                 self._denses = [m.Dense_0 for m in self.all_modules
                                 if hasattr(m, "Dense_0") and isinstance(m.Dense_0, nn.Linear)]
