@@ -1,6 +1,7 @@
 """Per-step kernel count and busy time of the timed graph replays in a rocprofv3 kernel trace
-of tools/prof_pinn.py (segments separated by > 2 ms of idle; the longest segment holds the
-replays): python tools/trace_steps.py TRACE.csv REPLAYS [TOP]"""
+of tools/prof_pinn.py: the periods between the step's FilterBatch launches (else: segments
+separated by > 2 ms of idle, the longest holding the replays): python tools/trace_steps.py
+TRACE.csv REPLAYS [TOP]"""
 import collections
 import csv
 import re
@@ -28,6 +29,12 @@ for e in ev[1:]:
     last = max(last, e[1])
 segs.append(cur)
 s = max(segs, key=len)
+# the graph step starts with the one FilterBatch launch (every Winograd filter of the step):
+# when present, a step is the period between two of them (the replay plus the eager optimizer
+# / EMA launches after it); the last nrep periods are the timed replays
+marks = [i for i, e in enumerate(ev) if "wino_filter_batch_kernel" in e[2]]
+if len(marks) > nrep:
+    s = ev[marks[-nrep - 1]:marks[-1]]
 t, c = collections.Counter(), collections.Counter()
 for e in s:
     k = short(e[2])
