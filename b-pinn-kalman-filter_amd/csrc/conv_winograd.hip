@@ -843,11 +843,12 @@ __global__ __launch_bounds__(64 * WG, WG == 8 ? 1 : (NB == 1 ? 2 : 1)) void wino
 // and the patch is 10 x 20 (each image with its own one-pixel halo: columns 0-9 and 10-19), so
 // the 3x3 convs of 8 x 8 feature maps run at the full 32-tile region instead of on the
 // implicit GEMM.
-template <bool PRE, bool PAIR = false>
-__global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
-    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
-    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
-    float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2) {
+template <bool PRE, bool PAIR>
+__device__ __forceinline__ void k16_item(
+    unsigned b, const float* __restrict__ x, const float* __restrict__ U,
+    const float* __restrict__ bias, const float* __restrict__ skip,
+    const float2* __restrict__ pre, float* __restrict__ y, float2* __restrict__ stats,
+    const WinoGeo& g, const float* __restrict__ x2) {
   constexpr int CK = 16;
   constexpr int kPatch = CK * kPR * kPCp;
   __shared__ __attribute__((aligned(16))) float s_patch_raw[2][kPatch];
@@ -858,9 +859,6 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   WINO_TS(0);
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const unsigned nblk = gridDim.x;
-  unsigned b = blockIdx.x;
-  if (xcd_remap) b = (b & 7u) * (nblk >> 3) + (b >> 3);
   unsigned cb, rx, ry;
   unsigned r = udivmod(b, (unsigned)g.cout_blocks, cb);
   r = udivmod(r, (unsigned)g.regions_x, rx);
@@ -1136,6 +1134,30 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
   WINO_TS(5);
 }
 
+// Persistent form (round 6): gridDim.x workgroups (one per CU, k16_grid) walk the items, so the
+// dispatcher's workgroup turnaround (~1 us between one workgroup's exit and the next one's start
+// on a CU, the round-4 timeline) is paid once per CU instead of once per item.  Round r runs
+// items [r G, r G + G); within a round the workgroups sharing an XCD (b, b + 8, ...) take one
+// contiguous run (the cout blocks of a region, neighbouring regions: their patches shared in
+// that XCD's L2).  Items do not overlap inside a workgroup (the register-staged overlap spilled,
+// DESIGN.md section 4); the barrier between items keeps the next prologue's LDS stores behind
+// every wave's last reads of the previous item.
+template <bool PRE, bool PAIR = false>
+__global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
+    const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
+    const float* __restrict__ skip, const float2* __restrict__ pre, float* __restrict__ y,
+    float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2,
+    unsigned items) {
+  const unsigned G = gridDim.x, w = blockIdx.x;
+  const unsigned slot = xcd_remap ? (w & 7u) * (G >> 3) + (w >> 3) : w;
+  for (unsigned base = 0; base < items; base += G) {
+    const unsigned b = base + slot;
+    if (b >= items) break;  // the last round's remap may leave this workgroup without an item
+    if (base) __syncthreads();
+    k16_item<PRE, PAIR>(b, x, U, bias, skip, pre, y, stats, g, x2);
+  }
+}
+
 // Split-K epilogue: y = sum_s part[s] + bias, or (skip + that) / div, and the GroupNorm partial
 // statistics of the stored values, as the 16-cin kernel's own epilogue (the partial slabs are
 // summed in a fixed order: deterministic).  One workgroup = 8 channels x one 8 x 16 region of
@@ -1189,6 +1211,21 @@ __global__ __launch_bounds__(256) void wino_splitk_reduce_kernel(
 }  // namespace
 
 static int cout_padded(int Cout) { return (Cout + 63) / 64 * 64; }
+
+// grid of the persistent 16-cin kernel: one workgroup per CU (its launch bound), at most one
+// per item; WINO_PERSIST=0 builds launch one workgroup per item (the round-5 form, for A/B)
+#ifndef WINO_PERSIST
+#define WINO_PERSIST 1
+#endif
+static unsigned k16_grid(int64_t items) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return (unsigned)(WINO_PERSIST ? std::min<int64_t>(items, cus) : items);
+}
 
 extern "C" int64_t bpk_conv3x3_wino_filter_bytes(int Cin, int Cout) {
   return (int64_t)16 * Cin * cout_padded(Cout) * (int64_t)sizeof(float);
@@ -1251,15 +1288,16 @@ static int wino_pair_launch(const float* x, const float* pre, const float* U, co
   BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino pair form: grid too large");
   const float2* kpre = reinterpret_cast<const float2*>(pre);
   hipStream_t st = bpk::as_stream(stream);
-  const int remap = (items % 8 == 0) ? 1 : 0;
+  const unsigned kg = k16_grid(items);
+  const int remap = (kg % 8 == 0) ? 1 : 0;
   const float* kb = S > 1 ? nullptr : bias;
   const float* ks = S > 1 ? nullptr : skip;
   if (pre)
-    hipLaunchKernelGGL((wino_f23_k16_kernel<true, true>), dim3((unsigned)items), dim3(512), 0, st,
-                       x, U, kb, ks, kpre, y, nullptr, gk, remap, nullptr);
+    hipLaunchKernelGGL((wino_f23_k16_kernel<true, true>), dim3(kg), dim3(512), 0, st,
+                       x, U, kb, ks, kpre, y, nullptr, gk, remap, nullptr, (unsigned)items);
   else
-    hipLaunchKernelGGL((wino_f23_k16_kernel<false, true>), dim3((unsigned)items), dim3(512), 0, st,
-                       x, U, kb, ks, kpre, y, nullptr, gk, remap, nullptr);
+    hipLaunchKernelGGL((wino_f23_k16_kernel<false, true>), dim3(kg), dim3(512), 0, st,
+                       x, U, kb, ks, kpre, y, nullptr, gk, remap, nullptr, (unsigned)items);
   BPK_LAUNCH_CHECK("conv3x3_wino_pair");
   return BPK_OK;
 }
@@ -1312,14 +1350,14 @@ extern "C" int bpk_conv3x3_wino_ex_f32(const float* x, const float* x2, int C1, 
       BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino: grid too large");
       const float2* kpre = reinterpret_cast<const float2*>(pre);
       hipStream_t kst = bpk::as_stream(stream);
-      const int64_t kblocks = items;
-      const int kremap = (kblocks % 8 == 0) ? 1 : 0;
+      const unsigned kg = k16_grid(items);
+      const int kremap = (kg % 8 == 0) ? 1 : 0;
       if (pre)
-        hipLaunchKernelGGL((wino_f23_k16_kernel<true>), dim3((unsigned)kblocks), dim3(512), 0, kst,
-                           x, U, bias, skip, kpre, y, stats2, gk, kremap, x2);
+        hipLaunchKernelGGL((wino_f23_k16_kernel<true>), dim3(kg), dim3(512), 0, kst,
+                           x, U, bias, skip, kpre, y, stats2, gk, kremap, x2, (unsigned)items);
       else
-        hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3((unsigned)kblocks), dim3(512), 0, kst,
-                           x, U, bias, skip, kpre, y, stats2, gk, kremap, x2);
+        hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3(kg), dim3(512), 0, kst,
+                           x, U, bias, skip, kpre, y, stats2, gk, kremap, x2, (unsigned)items);
       BPK_LAUNCH_CHECK("conv3x3_wino_k16");
       return BPK_OK;
     }
@@ -1429,13 +1467,14 @@ extern "C" int bpk_conv3x3_wino_splitk_f32(const float* x, const float* x2, int 
   BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino_splitk: grid too large");
   const float2* kpre = reinterpret_cast<const float2*>(pre);
   hipStream_t st = bpk::as_stream(stream);
-  const int remap = (items % 8 == 0) ? 1 : 0;
+  const unsigned kg = k16_grid(items);
+  const int remap = (kg % 8 == 0) ? 1 : 0;
   if (pre)
-    hipLaunchKernelGGL((wino_f23_k16_kernel<true>), dim3((unsigned)items), dim3(512), 0, st, x, U,
-                       nullptr, nullptr, kpre, workspace, nullptr, gk, remap, x2);
+    hipLaunchKernelGGL((wino_f23_k16_kernel<true>), dim3(kg), dim3(512), 0, st, x, U,
+                       nullptr, nullptr, kpre, workspace, nullptr, gk, remap, x2, (unsigned)items);
   else
-    hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3((unsigned)items), dim3(512), 0, st, x,
-                       U, nullptr, nullptr, kpre, workspace, nullptr, gk, remap, x2);
+    hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3(kg), dim3(512), 0, st, x,
+                       U, nullptr, nullptr, kpre, workspace, nullptr, gk, remap, x2, (unsigned)items);
   BPK_LAUNCH_CHECK("conv3x3_wino_splitk");
   const int64_t rblocks = (int64_t)N * (Cout / 8) * gk.regions_x * gk.regions_y;
   BPK_REQUIRE(Cout % 8 == 0 && rblocks < (1LL << 31), "conv3x3_wino_splitk: reduce grid");
@@ -1463,9 +1502,10 @@ extern "C" int bpk_conv3x3_wino_up2_f32(const float* x, const float* U, const fl
   WinoGeo gk{N, Cin, CoutP, H, W, W / kOutCols, H / kOutRows, CoutP / 128, 1.0f, Cin, Cout, 1};
   const int64_t items = (int64_t)N * gk.regions_x * gk.regions_y * gk.cout_blocks;
   BPK_REQUIRE(items < (1LL << 31), "conv3x3_wino_up2: grid too large");
-  hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3((unsigned)items), dim3(512), 0,
+  const unsigned kg = k16_grid(items);
+  hipLaunchKernelGGL((wino_f23_k16_kernel<false>), dim3(kg), dim3(512), 0,
                      bpk::as_stream(stream), x, U, bias, nullptr, nullptr, y, nullptr, gk,
-                     (items % 8 == 0) ? 1 : 0, nullptr);
+                     (kg % 8 == 0) ? 1 : 0, nullptr, (unsigned)items);
   BPK_LAUNCH_CHECK("conv3x3_wino_up2");
   return BPK_OK;
 }
