@@ -1136,12 +1136,13 @@ __device__ __forceinline__ void k16_item(
 
 // Persistent form (round 6): gridDim.x workgroups (one per CU, k16_grid) walk the items, so the
 // dispatcher's workgroup turnaround (~1 us between one workgroup's exit and the next one's start
-// on a CU, the round-4 timeline) is paid once per CU instead of once per item.  Round r runs
-// items [r G, r G + G); within a round the workgroups sharing an XCD (b, b + 8, ...) take one
-// contiguous run (the cout blocks of a region, neighbouring regions: their patches shared in
-// that XCD's L2).  Items do not overlap inside a workgroup (the register-staged overlap spilled,
-// DESIGN.md section 4); the barrier between items keeps the next prologue's LDS stores behind
-// every wave's last reads of the previous item.
+// on a CU, the round-4 timeline) is paid once per CU instead of once per item.  With xcd_remap
+// the workgroups sharing an XCD (w, w + 8, ...: blocks are dealt round-robin over the 8 XCDs)
+// walk one contiguous eighth of the items together, in order -- the order the dispatcher gave
+// the one-workgroup-per-item launch: the cout blocks of a region and the neighbouring regions
+// (their patch halos) are processed close in time on one XCD's L2.  Items do not overlap inside
+// a workgroup (the register-staged overlap spilled); the barrier between
+// items keeps the next prologue's LDS stores behind every wave's last reads of the previous one.
 template <bool PRE, bool PAIR = false>
 __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
     const float* __restrict__ x, const float* __restrict__ U, const float* __restrict__ bias,
@@ -1149,11 +1150,16 @@ __global__ __launch_bounds__(512, 1) void wino_f23_k16_kernel(
     float2* __restrict__ stats, WinoGeo g, int xcd_remap, const float* __restrict__ x2,
     unsigned items) {
   const unsigned G = gridDim.x, w = blockIdx.x;
-  const unsigned slot = xcd_remap ? (w & 7u) * (G >> 3) + (w >> 3) : w;
-  for (unsigned base = 0; base < items; base += G) {
-    const unsigned b = base + slot;
-    if (b >= items) break;  // the last round's remap may leave this workgroup without an item
-    if (base) __syncthreads();
+  unsigned first = w, stride = G, end = items;
+  if (xcd_remap) {  // G % 8 == 0: XCD label w % 8 owns items [start, start + count)
+    const unsigned xc = w & 7u, q = items >> 3, r = items & 7u;
+    const unsigned start = xc * q + min(xc, r);
+    first = start + (w >> 3);
+    stride = G >> 3;
+    end = start + q + (xc < r ? 1u : 0u);
+  }
+  for (unsigned b = first; b < end; b += stride) {
+    if (b != first) __syncthreads();
     k16_item<PRE, PAIR>(b, x, U, bias, skip, pre, y, stats, g, x2);
   }
 }
