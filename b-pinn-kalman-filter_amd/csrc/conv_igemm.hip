@@ -72,6 +72,9 @@ struct IgGeo {
   // K-chunk is 16 channels of ONE tap
   int tap, Cc;
   FDiv f_cc;
+  // split-K combined in-launch (bpk::splitk_last): one zeroed counter per output tile, else
+  // nullptr and a reduce kernel follows
+  unsigned* cnt;
 };
 
 // k -> (co, r, s) of a MODE 3 class sub-filter tap
@@ -102,6 +105,99 @@ __device__ inline void split_tap(int k, const IgGeo& g, int& c, int& r, int& s) 
   s = rs - r * kw;
 }
 
+// the output offset and stride (per row m) of GEMM column `col`
+template <int MODE>
+__device__ inline int64_t out_offset(int col, const IgGeo& g, int64_t& ostride) {
+  if (MODE == 0) {
+    const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
+    ostride = g.HoWo;
+    return (int64_t)n * g.Cout * g.HoWo + pix;
+  } else if (MODE == 1) {
+    const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
+    ostride = g.HW;
+    return (int64_t)n * g.Cin * g.HW + pix;
+  } else if (MODE == 3) {
+    ostride = g.HW;
+    return class_pixel_offset(col, g);
+  }
+  ostride = g.wcols;
+  return col;
+}
+
+// split-K, combined in the launch: the workgroup that draws its tile's last ticket sums the S
+// partial slabs of the tile in slab order (igemm_reduce_kernel's sum) and writes the output
+// (+ bias, or the weight gradient's bias column), 16 elements per thread per pass with 4 x 16
+// loads in flight; out-of-range elements load element 0 and are not stored (no branch around
+// the loads).
+template <int MODE, int TM, int TN>
+__device__ void splitk_tail(const IgGeo& g, const float* __restrict__ ws,
+                            const float* __restrict__ bias, float* __restrict__ out,
+                            float* __restrict__ out2, int* flag) {
+  if (!bpk::splitk_last(g.cnt + blockIdx.y * gridDim.x + blockIdx.x, (unsigned)g.splits, flag))
+    return;
+  constexpr int EPT = 16;                     // elements per thread per pass
+  constexpr int PASSES = TM * TN / (256 * EPT);  // 1 (64 x 64, 16 x 256) or 4 (128 x 128)
+  constexpr int ZU = 4;                          // slabs in flight per element
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
+  const int64_t total = (int64_t)g.M * g.Ncol;
+#pragma unroll 1
+  for (int pass = 0; pass < PASSES; ++pass) {
+    int off[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = threadIdx.x + 256 * (pass * EPT + i);
+      const int m = m0 + e / TN, col = n0 + e % TN;
+      off[i] = (m < g.M && col < g.Ncol) ? m * g.Ncol + col : 0;
+    }
+    float v[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) v[i] = ws[off[i]];
+    int z = 1;
+    for (; z + ZU <= g.splits; z += ZU) {
+      float t[ZU][EPT];
+#pragma unroll
+      for (int u = 0; u < ZU; ++u) {
+        const float* wz = ws + (int64_t)(z + u) * total;
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) t[u][i] = wz[off[i]];
+      }
+#pragma unroll
+      for (int u = 0; u < ZU; ++u)
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) v[i] += t[u][i];
+    }
+    for (; z < g.splits; ++z) {
+      const float* wz = ws + (int64_t)z * total;
+      float t[EPT];
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) t[i] = wz[off[i]];
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) v[i] += t[i];
+    }
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = threadIdx.x + 256 * (pass * EPT + i);
+      const int m = m0 + e / TN, col = n0 + e % TN;
+      if (m >= g.M || col >= g.Ncol) continue;
+      if (MODE == 2 && col == g.wcols) {
+        out2[m] = v[i];
+        continue;
+      }
+      int64_t ostride;
+      const int64_t ob = out_offset<MODE>(col, g, ostride);
+      out[ob + (int64_t)m * ostride] = (MODE == 0 && bias) ? v[i] + bias[m] : v[i];
+    }
+  }
+}
+
+// the tiles whose kernels carry the in-launch split-K tail: 64 x 64, and 16 x 256 except the
+// strided backward-data classes and the weight gradient of a filter size without its own
+// instantiation (there, and in the 128 x 128 kernels, it made the compiler spill; those
+// launches keep the reduce kernel)
+__host__ __device__ constexpr bool fuse_tail(int mode, int tm, bool generic_taps) {
+  return tm == 64 || (tm == 16 && mode != 3 && !(mode == 2 && generic_taps));
+}
+
 // TM x TN outputs per workgroup of 4 waves (WMW along M x 4 / WMW along N; each wave
 // NBM x NBN MFMA blocks of 16 x 16), K chunks of 16 through double-buffered LDS
 template <int MODE, int KH_, int KW_, int TM, int TN, int WMW, bool TAP>
@@ -113,6 +209,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
                                                     float* __restrict__ ws, IgGeo g) {
   constexpr int WNW = 4 / WMW;
   constexpr int WTM = TM / WMW, WTN = TN / WNW;  // wave tile
+  constexpr bool kFuseTail = fuse_tail(MODE, TM, KH_ == 0);
   constexpr int NBM = WTM / 16, NBN = WTN / 16;  // MFMA blocks per wave
   constexpr int NLA = TM / 16, NLB = TN / 16;    // A / B elements each thread stages per chunk
   constexpr int kAP = BK + 1;                    // LDS pitch of the A tile [m][k]
@@ -426,6 +523,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
           dst[obase + (int64_t)m * ostride] = acc[mb][nb][i] + bbv[mb][i];
         }
     }
+    if (kFuseTail && g.splits > 1 && g.cnt)
+      splitk_tail<MODE, TM, TN>(g, ws, bias, out, out2, reinterpret_cast<int*>(&s_a[0][0]));
     return;
   }
 #pragma unroll
@@ -472,6 +571,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
         }
       }
   }
+  if (kFuseTail && g.splits > 1 && g.cnt)
+    splitk_tail<MODE, TM, TN>(g, ws, bias, out, out2, reinterpret_cast<int*>(&s_a[0][0]));
 }
 
 // Many splits (a weight gradient over a long pixel sum into few outputs: the PINN's 1-32
@@ -685,9 +786,19 @@ void launch_tile(const IgGeo& g, const float* A0, const float* B0, const float* 
 }
 
 template <int MODE>
-int launch(const IgGeo& g, const float* A0, const float* B0, const float* bias, float* out,
+int launch(const IgGeo& g0, const float* A0, const float* B0, const float* bias, float* out,
            float* out2, float* ws, hipStream_t st) {
+  IgGeo g = g0;
   float* wsp = g.splits > 1 ? ws : nullptr;
+  g.cnt = nullptr;
+  const int tm = g.tile == 1 ? 128 : g.tile == 2 ? 16 : 64;
+  const bool own_taps = g.KH == g.KW && g.KH >= 1 && g.KH <= 4;  // launch_tile's instantiations
+  // (beyond kRedG slices the reduce runs in two levels, a different summation order)
+  if (g.splits > 1 && g.splits <= std::min(bpk::splitk_fuse_max(), kRedG) &&
+      fuse_tail(MODE, tm, !own_taps)) {
+    const int tn = g.tile == 1 ? 128 : g.tile == 2 ? 256 : 64;
+    g.cnt = bpk::splitk_tickets(bpk::ceil_div(g.M, tm) * bpk::ceil_div(g.Ncol, tn));
+  }
   if (g.tile == 1)
     launch_tile<MODE, 128, 128, 2>(g, A0, B0, bias, out, out2, wsp, st);
   else if (g.tile == 2)
@@ -695,7 +806,7 @@ int launch(const IgGeo& g, const float* A0, const float* B0, const float* bias, 
   else
     launch_tile<MODE, 64, 64, 2>(g, A0, B0, bias, out, out2, wsp, st);
   BPK_LAUNCH_CHECK("conv2d_igemm");
-  if (g.splits > 1) {
+  if (g.splits > 1 && !g.cnt) {
     const int64_t total = (int64_t)g.M * g.Ncol;
     const float* src = ws;
     int S = g.splits;

@@ -42,6 +42,14 @@ const char* bpk_last_error(void);
 /* Returns BPK_ABI_VERSION. */
 int bpk_abi_version(void);
 
+/* Split-K launches (implicit-GEMM convs, Winograd / 1x1 weight gradients at small batches)
+ * with at most this many K-slices combine their partials inside the launch: the workgroup that
+ * finishes a tile's last slice sums the slices in slice order (the same sum as the separate
+ * reduce kernel, bit for bit) and writes the tile, so no reduce launch follows.  Default
+ * BPK_SPLITK_FUSE_MAX (environment) or 16; 0 = always launch the reduce kernel.  Returns the
+ * previous value.  Not a reference interface: a tuning / A-B switch of this library. */
+int bpk_splitk_set_fuse_max(int max_splits);
+
 /* ------------------------------------------------------------------------- *
  * upfirdn2d: zero-insert upsample by (up_x, up_y), pad (negative = crop),
  * true 2-D convolution with `kernel` [kernel_h, kernel_w] (i.e. correlation with

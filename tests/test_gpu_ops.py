@@ -1250,6 +1250,50 @@ def test_conv2d_igemm_fwd_dgrad_wgrad_vs_fp64(hip, case):
     assert none is None and torch.equal(dw2, dw)
 
 
+@pytest.fixture
+def splitk_fuse(hip):
+    """Set the in-launch split-K limit (bpk_splitk_set_fuse_max) for a test; restored after."""
+    from op._lib import lib
+    prev = lib.bpk_splitk_set_fuse_max(16)
+    lib.bpk_splitk_set_fuse_max(prev)
+    yield lambda v: lib.bpk_splitk_set_fuse_max(v)
+    lib.bpk_splitk_set_fuse_max(prev)
+
+
+@pytest.mark.parametrize("case", _IG_CASES + [
+    (8, 16, 8, 8, 32, 3, 1, 1),      # PINN pyramid level 8^2 at B = 8: forward / dgrad split
+    (8, 128, 4, 4, 96, 3, 1, 1),     # 4^2 level, 64 x 64 tiles with a ragged M
+    (16, 96, 2, 2, 2, 3, 1, 1),      # 2-channel head at 2^2: 16 x 256 tiles, long K
+    (8, 32, 16, 16, 16, 4, 2, 1),    # ConvTranspose2d(k4, s2)-class shapes
+])
+def test_conv2d_igemm_splitk_in_launch_matches_reduce_kernel(hip, splitk_fuse, case):
+    """The in-launch split-K combine (the workgroup drawing a tile's last ticket sums the
+    slices, bpk_common.h splitk_last) gives results bit-identical to the separate reduce
+    kernel, for every product of the conv, and stays so over repeated launches (every launch
+    must leave its tile counters at zero for the next)."""
+    from op.conv import conv2d_igemm_raw, conv2d_input_igemm_raw, conv2d_weight_igemm_raw
+    N, C, H, W, Co, k, s, p = case
+    g = torch.Generator().manual_seed(7 + sum(case))
+    x = torch.randn(N, C, H, W, generator=g).to(hip)
+    w = (torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5).to(hip)
+    b = torch.randn(Co, generator=g).to(hip)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    gy = torch.randn(N, Co, Ho, Wo, generator=g).to(hip)
+
+    def run():
+        return (conv2d_igemm_raw(x, w, b, s, p), conv2d_input_igemm_raw(x.shape, w, gy, s, p),
+                *conv2d_weight_igemm_raw(x, w.shape, gy, s, p, bias_grad=True))
+
+    splitk_fuse(0)
+    ref = run()
+    splitk_fuse(4096)  # every split count in-launch
+    for _ in range(6):
+        got = run()
+        for a, r, name in zip(got, ref, ("forward", "dgrad", "wgrad", "bias grad")):
+            assert torch.equal(a, r), name
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("case", [
     # N, Cin, H, W, Cout, K
     (2, 5, 9, 13, 1, 3),       # odd sizes, bands ragged
