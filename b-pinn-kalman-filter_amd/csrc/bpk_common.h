@@ -36,43 +36,6 @@ __device__ inline int64_t xcd_tile(int64_t b, int64_t nb) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
-// In-launch split-K combine (cdna_hip_programming.md §6 Guideline 16, counter form): each
-// K-slice workgroup stores its partial slab with plain stores, then draws a ticket on its
-// output tile's counter; the workgroup drawing the last ticket reads every slab and writes the
-// tile -- the separate reduce launch (and its kernel boundary, ~1.5-1.9 us) is gone, the sum
-// order (slab 0, 1, ..., S - 1) and with it the result are unchanged.  Correct for any
-// placement of a tile's slices over CUs / XCDs: agent-scope release before the ticket,
-// agent-scope acquire in the last arriver.  `flag` is a word of the kernel's own LDS array
-// (a second __shared__ object can de-pipeline the main loop, ibid. item 4a), free by now.
-// The last arriver resets the counter, so the tickets are zero again when the launch ends.
-__device__ inline bool splitk_last(unsigned* cnt, unsigned splits, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == splits - 1;
-    if (last) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-// host: n zeroed tile counters for one launch (a ring over a device array that every launch
-// leaves zeroed; consecutive launches take different slots, so kernels running concurrently on
-// different streams do not share counters), or nullptr when the in-launch combine is off
-// (BPK_SPLITK_FUSE_MAX=0) or unavailable -- callers then launch their reduce kernel
-unsigned* splitk_tickets(int64_t n);
-// largest split count combined in-launch (the last arriver reads S partial slabs of its tile
-// serially; BPK_SPLITK_FUSE_MAX, default 16; 0 = never)
-int splitk_fuse_max();
-
 }  // namespace bpk
 
 #define BPK_REQUIRE(cond, ...)           \

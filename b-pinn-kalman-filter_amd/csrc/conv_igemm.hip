@@ -72,9 +72,12 @@ struct IgGeo {
   // K-chunk is 16 channels of ONE tap
   int tap, Cc;
   FDiv f_cc;
-  // split-K combined in-launch (bpk::splitk_last): one zeroed counter per output tile, else
-  // nullptr and a reduce kernel follows
-  unsigned* cnt;
+  // MODE 2 over two (x, gy) sources: images n < N1 of the K range come from (B0, A0), the
+  // others from (B1, A1) as image n - N1 (the weight gradient of one weight used by two convs
+  // in one launch); the bias column counts images n < Nb only
+  const float* A1;
+  const float* B1;
+  int N1, Nb;
 };
 
 // k -> (co, r, s) of a MODE 3 class sub-filter tap
@@ -105,99 +108,6 @@ __device__ inline void split_tap(int k, const IgGeo& g, int& c, int& r, int& s) 
   s = rs - r * kw;
 }
 
-// the output offset and stride (per row m) of GEMM column `col`
-template <int MODE>
-__device__ inline int64_t out_offset(int col, const IgGeo& g, int64_t& ostride) {
-  if (MODE == 0) {
-    const int n = fdiv(col, g.f_howo), pix = col - n * g.HoWo;
-    ostride = g.HoWo;
-    return (int64_t)n * g.Cout * g.HoWo + pix;
-  } else if (MODE == 1) {
-    const int n = fdiv(col, g.f_hw), pix = col - n * g.HW;
-    ostride = g.HW;
-    return (int64_t)n * g.Cin * g.HW + pix;
-  } else if (MODE == 3) {
-    ostride = g.HW;
-    return class_pixel_offset(col, g);
-  }
-  ostride = g.wcols;
-  return col;
-}
-
-// split-K, combined in the launch: the workgroup that draws its tile's last ticket sums the S
-// partial slabs of the tile in slab order (igemm_reduce_kernel's sum) and writes the output
-// (+ bias, or the weight gradient's bias column), 16 elements per thread per pass with 4 x 16
-// loads in flight; out-of-range elements load element 0 and are not stored (no branch around
-// the loads).
-template <int MODE, int TM, int TN>
-__device__ void splitk_tail(const IgGeo& g, const float* __restrict__ ws,
-                            const float* __restrict__ bias, float* __restrict__ out,
-                            float* __restrict__ out2, int* flag) {
-  if (!bpk::splitk_last(g.cnt + blockIdx.y * gridDim.x + blockIdx.x, (unsigned)g.splits, flag))
-    return;
-  constexpr int EPT = 16;                     // elements per thread per pass
-  constexpr int PASSES = TM * TN / (256 * EPT);  // 1 (64 x 64, 16 x 256) or 4 (128 x 128)
-  constexpr int ZU = 4;                          // slabs in flight per element
-  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
-  const int64_t total = (int64_t)g.M * g.Ncol;
-#pragma unroll 1
-  for (int pass = 0; pass < PASSES; ++pass) {
-    int off[EPT];
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int e = threadIdx.x + 256 * (pass * EPT + i);
-      const int m = m0 + e / TN, col = n0 + e % TN;
-      off[i] = (m < g.M && col < g.Ncol) ? m * g.Ncol + col : 0;
-    }
-    float v[EPT];
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) v[i] = ws[off[i]];
-    int z = 1;
-    for (; z + ZU <= g.splits; z += ZU) {
-      float t[ZU][EPT];
-#pragma unroll
-      for (int u = 0; u < ZU; ++u) {
-        const float* wz = ws + (int64_t)(z + u) * total;
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) t[u][i] = wz[off[i]];
-      }
-#pragma unroll
-      for (int u = 0; u < ZU; ++u)
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) v[i] += t[u][i];
-    }
-    for (; z < g.splits; ++z) {
-      const float* wz = ws + (int64_t)z * total;
-      float t[EPT];
-#pragma unroll
-      for (int i = 0; i < EPT; ++i) t[i] = wz[off[i]];
-#pragma unroll
-      for (int i = 0; i < EPT; ++i) v[i] += t[i];
-    }
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int e = threadIdx.x + 256 * (pass * EPT + i);
-      const int m = m0 + e / TN, col = n0 + e % TN;
-      if (m >= g.M || col >= g.Ncol) continue;
-      if (MODE == 2 && col == g.wcols) {
-        out2[m] = v[i];
-        continue;
-      }
-      int64_t ostride;
-      const int64_t ob = out_offset<MODE>(col, g, ostride);
-      out[ob + (int64_t)m * ostride] = (MODE == 0 && bias) ? v[i] + bias[m] : v[i];
-    }
-  }
-}
-
-// the tiles whose kernels carry the in-launch split-K tail: 64 x 64, and 16 x 256 except the
-// strided backward-data classes and the weight gradient of a filter size without its own
-// instantiation (there, and in the 128 x 128 kernels, it made the compiler spill; those
-// launches keep the reduce kernel)
-__host__ __device__ constexpr bool fuse_tail(int mode, int tm, bool generic_taps) {
-  return tm == 64 || (tm == 16 && mode != 3 && !(mode == 2 && generic_taps));
-}
-
 // TM x TN outputs per workgroup of 4 waves (WMW along M x 4 / WMW along N; each wave
 // NBM x NBN MFMA blocks of 16 x 16), K chunks of 16 through double-buffered LDS
 template <int MODE, int KH_, int KW_, int TM, int TN, int WMW, bool TAP>
@@ -209,7 +119,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
                                                     float* __restrict__ ws, IgGeo g) {
   constexpr int WNW = 4 / WMW;
   constexpr int WTM = TM / WMW, WTN = TN / WNW;  // wave tile
-  constexpr bool kFuseTail = fuse_tail(MODE, TM, KH_ == 0);
   constexpr int NBM = WTM / 16, NBN = WTN / 16;  // MFMA blocks per wave
   constexpr int NLA = TM / 16, NLB = TN / 16;    // A / B elements each thread stages per chunk
   constexpr int kAP = BK + 1;                    // LDS pitch of the A tile [m][k]
@@ -343,7 +252,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
           } else if (MODE == 3) {  // m = ci, k = (co, class tap)
             v = A0[((int64_t)a_co * g.Cin + m) * g.KHW + a_rs];
           } else {  // m = co, k = pixel
-            v = A0[((int64_t)a_n * g.Cout + m) * g.HoWo + a_pix];
+            const bool s2 = a_n >= g.N1;
+            v = (s2 ? g.A1 : A0)[((int64_t)(s2 ? a_n - g.N1 : a_n) * g.Cout + m) * g.HoWo + a_pix];
           }
         }
         ra[j] = v;
@@ -400,13 +310,15 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
       for (int q = 0; q < KW_; ++q) sm |= (unsigned)((unsigned)(ix0 + q) < (unsigned)g.W) << q;
 #pragma unroll
       for (int r = 0; r < KH_; ++r) vm |= ((rm >> r) & 1u) ? sm << (r * KW_) : 0u;
-      vm = kv ? vm | (1u << 16) : 0u;
+      vm = kv ? vm | (n < g.Nb ? 1u << 16 : 0u) : 0u;
       // the tap origin's element offset; negative only where the mask excludes the tap
-      const int pb = n * g.Cin * g.HW + iy0 * g.W + ix0;
+      const bool s2 = n >= g.N1;
+      const float* bsrc = s2 ? g.B1 : B0;
+      const int pb = (s2 ? n - g.N1 : n) * g.Cin * g.HW + iy0 * g.W + ix0;
 #pragma unroll
       for (int j = 0; j < NLB; ++j) {
         float v = 0.f;
-        if (vm & bbit[j]) v = bcol_one[j] ? 1.f : B0[(unsigned)(pb + boff[j])];
+        if (vm & bbit[j]) v = bcol_one[j] ? 1.f : bsrc[(unsigned)(pb + boff[j])];
         rb[j] = v;
       }
     } else {
@@ -416,17 +328,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
       const int n = fdiv(kk, g.f_howo), pix = kk - n * g.HoWo;
       const int oy = fdiv(pix, g.f_wo), ox = pix - oy * g.Wo;
       const int iy0 = oy * g.sh - g.ph, ix0 = ox * g.sw - g.pw;
-      const int64_t xb = (int64_t)n * g.Cin * g.HW;
+      const bool s2 = n >= g.N1;
+      const float* bsrc = s2 ? g.B1 : B0;
+      const int64_t xb = (int64_t)(s2 ? n - g.N1 : n) * g.Cin * g.HW;
 #pragma unroll
       for (int j = 0; j < NLB; ++j) {
         float v = 0.f;
         if (kv && bcol_ok[j]) {
           if (bcol_one[j]) {
-            v = 1.f;
+            v = n < g.Nb ? 1.f : 0.f;
           } else {
             const int iy = iy0 + br[j], ix = ix0 + bs[j];
             if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
-              v = B0[xb + ((int64_t)bc[j] * g.H + iy) * g.W + ix];
+              v = bsrc[xb + ((int64_t)bc[j] * g.H + iy) * g.W + ix];
           }
         }
         rb[j] = v;
@@ -523,8 +437,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
           dst[obase + (int64_t)m * ostride] = acc[mb][nb][i] + bbv[mb][i];
         }
     }
-    if (kFuseTail && g.splits > 1 && g.cnt)
-      splitk_tail<MODE, TM, TN>(g, ws, bias, out, out2, reinterpret_cast<int*>(&s_a[0][0]));
     return;
   }
 #pragma unroll
@@ -571,8 +483,6 @@ __global__ __launch_bounds__(256) void igemm_kernel(const float* __restrict__ A0
         }
       }
   }
-  if (kFuseTail && g.splits > 1 && g.cnt)
-    splitk_tail<MODE, TM, TN>(g, ws, bias, out, out2, reinterpret_cast<int*>(&s_a[0][0]));
 }
 
 // Many splits (a weight gradient over a long pixel sum into few outputs: the PINN's 1-32
@@ -678,6 +588,7 @@ bool make_geo(int mode, int N, int Cin, int H, int W, int Cout, int KH, int KW, 
   } else {
     g.M = Cout; g.Ncol = g.wcols + (bias_col ? 1 : 0); g.K = N * Ho * Wo;
   }
+  g.N1 = g.Nb = N;
   g.Cc = mode == 0 ? Cin : Cout;
   g.tap = (mode == 0 || (mode == 1 && sh == 1 && sw == 1)) && KH == 3 && KW == 3 &&
           g.Cc % BK == 0;
@@ -786,19 +697,9 @@ void launch_tile(const IgGeo& g, const float* A0, const float* B0, const float* 
 }
 
 template <int MODE>
-int launch(const IgGeo& g0, const float* A0, const float* B0, const float* bias, float* out,
+int launch(const IgGeo& g, const float* A0, const float* B0, const float* bias, float* out,
            float* out2, float* ws, hipStream_t st) {
-  IgGeo g = g0;
   float* wsp = g.splits > 1 ? ws : nullptr;
-  g.cnt = nullptr;
-  const int tm = g.tile == 1 ? 128 : g.tile == 2 ? 16 : 64;
-  const bool own_taps = g.KH == g.KW && g.KH >= 1 && g.KH <= 4;  // launch_tile's instantiations
-  // (beyond kRedG slices the reduce runs in two levels, a different summation order)
-  if (g.splits > 1 && g.splits <= std::min(bpk::splitk_fuse_max(), kRedG) &&
-      fuse_tail(MODE, tm, !own_taps)) {
-    const int tn = g.tile == 1 ? 128 : g.tile == 2 ? 256 : 64;
-    g.cnt = bpk::splitk_tickets(bpk::ceil_div(g.M, tm) * bpk::ceil_div(g.Ncol, tn));
-  }
   if (g.tile == 1)
     launch_tile<MODE, 128, 128, 2>(g, A0, B0, bias, out, out2, wsp, st);
   else if (g.tile == 2)
@@ -806,7 +707,7 @@ int launch(const IgGeo& g0, const float* A0, const float* B0, const float* bias,
   else
     launch_tile<MODE, 64, 64, 2>(g, A0, B0, bias, out, out2, wsp, st);
   BPK_LAUNCH_CHECK("conv2d_igemm");
-  if (g.splits > 1 && !g.cnt) {
+  if (g.splits > 1) {
     const int64_t total = (int64_t)g.M * g.Ncol;
     const float* src = ws;
     int S = g.splits;
@@ -901,5 +802,27 @@ extern "C" int bpk_conv2d_igemm_wgrad_f32(const float* x, const float* gy, float
   BPK_REQUIRE((H + 2 * ph - KH) / sh + 1 == Ho && (W + 2 * pw - KW) / sw + 1 == Wo,
               "conv2d_igemm_wgrad: output %dx%d inconsistent with input %dx%d", Ho, Wo, H, W);
   BPK_REQUIRE(x && gy && dw && (g.splits == 1 || ws), "conv2d_igemm_wgrad: null pointer");
+  return launch<2>(g, gy, x, nullptr, dw, db, ws, bpk::as_stream(stream));
+}
+
+extern "C" int bpk_conv2d_igemm_wgrad2_f32(const float* x, const float* gy, const float* x2,
+                                           const float* gy2, int N2, float* dw, float* db,
+                                           void* wsv, int N, int Cin, int H, int W, int Cout,
+                                           int KH, int KW, int sh, int sw, int ph, int pw,
+                                           int Ho, int Wo, void* stream) {
+  IgGeo g;
+  float* ws = static_cast<float*>(wsv);
+  BPK_REQUIRE(N > 0 && N2 >= 0, "conv2d_igemm_wgrad2: bad image counts %d, %d", N, N2);
+  BPK_REQUIRE(make_geo(2, N + N2, Cin, H, W, Cout, KH, KW, sh, sw, ph, pw, Ho, Wo,
+                       db != nullptr, g),
+              "conv2d_igemm_wgrad2: bad shape N=%d+%d Cin=%d %dx%d Cout=%d k=%dx%d", N, N2, Cin,
+              H, W, Cout, KH, KW);
+  BPK_REQUIRE((H + 2 * ph - KH) / sh + 1 == Ho && (W + 2 * pw - KW) / sw + 1 == Wo,
+              "conv2d_igemm_wgrad2: output %dx%d inconsistent with input %dx%d", Ho, Wo, H, W);
+  BPK_REQUIRE(x && gy && dw && (N2 == 0 || (x2 && gy2)) && (g.splits == 1 || ws),
+              "conv2d_igemm_wgrad2: null pointer");
+  g.N1 = g.Nb = N;
+  g.A1 = gy2;
+  g.B1 = x2;
   return launch<2>(g, gy, x, nullptr, dw, db, ws, bpk::as_stream(stream));
 }

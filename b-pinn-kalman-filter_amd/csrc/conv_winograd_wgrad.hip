@@ -39,6 +39,7 @@ struct WgradGeo {
   int strips_x, strips_y;  // W / 16, H / 2 (PAIR: 1, H / 2; a strip = 2 rows of two images)
   int cin_blocks, cout_blocks, splits;
   int64_t chunks;          // N * strips_y * strips_x
+  int N1;                  // TWO: images n >= N1 are image n - N1 of (x2, gy2)
 };
 
 // Software-pipelined weight gradient (workgroup = 32 cin x 64 cout over a K-range of 8-tile
@@ -71,10 +72,14 @@ constexpr int kVT = kCB * kRec + 4;          // per-tile stride of the V records
 // PRE: the convolved input is silu(x * s + t) with pre[n][cin] = (s, t) -- the GroupNorm+SiLU
 // the forward conv applied in its input load (op.conv.gn_silu_conv3x3_ad) -- applied here in
 // the patch store with the forward prologue's arithmetic; the zero padding stays zero.
-template <int NB, bool PAIR = false, bool PRE = false>
+// TWO: the K range runs over the images of two (x, gy) sources (x2, gy2 from image N1 on; PAIR
+// needs N1 even) -- the weight gradient of one weight used by two convs in one launch; the
+// bias gradient sums the first source's gradient tiles only.
+template <int NB, bool PAIR = false, bool PRE = false, bool TWO = false>
 __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const float* __restrict__ x, const float* __restrict__ gy, float* __restrict__ part,
-    float* __restrict__ part_b, WgradGeo g, int xcd_remap, const float2* __restrict__ pre) {
+    float* __restrict__ part_b, WgradGeo g, int xcd_remap, const float2* __restrict__ pre,
+    const float* __restrict__ x2, const float* __restrict__ gy2) {
   __shared__ __attribute__((aligned(16))) float s_x[2][kCB * kXCS];   // 2 x 14.3 KB
   __shared__ __attribute__((aligned(16))) float s_v[2][kT * kVT];     // 2 x 24.7 KB
 
@@ -163,8 +168,13 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
     const Strip s = xcur;
     advance(xcur);
     const int oy0 = 2 * s.sy, ox0 = PAIR ? -8 * xh : 16 * s.sx;  // PAIR: half xh = image 2n + xh
-    const int img = PAIR ? 2 * s.n + xh : s.n;
-    const float* base = x + ((int64_t)img * g.Cin + cin0) * plane;
+    int img = PAIR ? 2 * s.n + xh : s.n;
+    const float* xsrc = x;
+    if (TWO && img >= g.N1) {
+      xsrc = x2;
+      img -= g.N1;
+    }
+    const float* base = xsrc + ((int64_t)img * g.Cin + cin0) * plane;
     if (PRE) xst = pre[(int64_t)img * g.Cin + cin0 + xc];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(base), 0, kCB * plane * 4, 0x00020000);
@@ -250,16 +260,23 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
   // fixed 32-bit voffset: no per-chunk 64-bit address arithmetic on the vector unit
   const int gwave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gvo0 = (jj * plane + 2 * kq) * 4;  // + 16 nb planes; + W floats for row 1
+  bool g_src1 = true;  // TWO: the gradient tiles in gq are the first source's (bias gradient)
   auto load_g = [&](float2 (&dst)[NB][2][2]) {  // gradient tiles of chunk gcur, then advance
     const Strip s = gcur;
     advance(gcur);
+    if (TWO) g_src1 = (PAIR ? 2 * s.n : s.n) < g.N1;
     if (!wvalid) return;  // past Cout: its MFMAs run on stale registers, never stored
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       {
         // tile 4 ks + kq; PAIR: k-step ks is image 2n + ks, tile column kq
-        const int img = PAIR ? 2 * s.n + ks : s.n;
-        const float* base = gy + ((int64_t)img * g.Cout + cout0 + 16 * NB * gwave) * plane;
+        int img = PAIR ? 2 * s.n + ks : s.n;
+        const float* gsrc = gy;
+        if (TWO && img >= g.N1) {
+          gsrc = gy2;
+          img -= g.N1;
+        }
+        const float* base = gsrc + ((int64_t)img * g.Cout + cout0 + 16 * NB * gwave) * plane;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(base), 0, 16 * NB * plane * 4, 0x00020000);
         const int so = (2 * s.sy * g.W + (PAIR ? 0 : 16 * s.sx + 8 * ks)) * 4;
@@ -342,7 +359,7 @@ __global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void wino_wgrad_pipe_kernel(
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         gbar(gq[nb][ks], bq[nb]);
-        if (want_b)
+        if (want_b && (!TWO || g_src1))
           bsum[nb] += (gq[nb][ks][0].x + gq[nb][ks][0].y) + (gq[nb][ks][1].x + gq[nb][ks][1].y);
       }
       if (ks == 1) load_g(gq);  // chunk j + 1 (both k-steps' tiles consumed)
@@ -530,28 +547,60 @@ extern "C" int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, 
                                         stream);
 }
 
+namespace {
+
+int wgrad_launch(const float* x, const float* pre, const float* gy, const float* x2,
+                 const float* gy2, int N2, float* dw, float* db, float* workspace, int N, int Cin,
+                 int Cout, int H, int W, void* stream);
+
+}  // namespace
+
 extern "C" int bpk_conv3x3_wino_wgrad_pre_f32(const float* x, const float* pre, const float* gy,
                                               float* dw, float* db, float* workspace, int N,
                                               int Cin, int Cout, int H, int W, void* stream) {
+  return wgrad_launch(x, pre, gy, nullptr, nullptr, 0, dw, db, workspace, N, Cin, Cout, H, W,
+                      stream);
+}
+
+extern "C" int bpk_conv3x3_wino_wgrad2_f32(const float* x, const float* gy, const float* x2,
+                                           const float* gy2, int N2, float* dw, float* db,
+                                           float* workspace, int N, int Cin, int Cout, int H,
+                                           int W, void* stream) {
+  BPK_REQUIRE(N > 0 && N2 > 0 && x2 && gy2, "conv3x3_wino_wgrad2: second source missing (N2=%d)",
+              N2);
+  BPK_REQUIRE(!wgrad_pair(N + N2, W) || N % 2 == 0,
+              "conv3x3_wino_wgrad2: 8-wide images need an even first source (N=%d)", N);
+  return wgrad_launch(x, nullptr, gy, x2, gy2, N2, dw, db, workspace, N, Cin, Cout, H, W, stream);
+}
+
+namespace {
+
+int wgrad_launch(const float* x, const float* pre, const float* gy, const float* x2,
+                 const float* gy2, int N2, float* dw, float* db, float* workspace, int N1, int Cin,
+                 int Cout, int H, int W, void* stream) {
+  const int N = N1 + N2;
   BPK_REQUIRE(bpk_conv3x3_wino_wgrad_supported(N, Cin, Cout, H, W),
               "conv3x3_wino_wgrad: unsupported shape N=%d Cin=%d Cout=%d H=%d W=%d (need Cin "
               "%% 32, Cout %% 16, H %% 2, W %% 16 == 0 or W == 8 with N even)", N, Cin, Cout,
               H, W);
   BPK_REQUIRE(workspace != nullptr, "conv3x3_wino_wgrad: workspace is NULL");
-  const WgradGeo g = make_geo(N, Cin, Cout, H, W);
+  WgradGeo g = make_geo(N, Cin, Cout, H, W);
+  g.N1 = N1;
   const int64_t blocks = (int64_t)g.splits * g.cin_blocks * g.cout_blocks;
   BPK_REQUIRE(blocks < (1LL << 31), "conv3x3_wino_wgrad: grid too large");
   hipStream_t st = bpk::as_stream(stream);
   const int remap = (blocks % 8 == 0) ? 1 : 0;
   float* part_b = db ? workspace + (int64_t)g.splits * Cin * Cout * 16 : nullptr;
   const float2* kp = reinterpret_cast<const float2*>(pre);
-#define BPK_WG(PAIR_, PRE_)                                                                      \
-  hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, PAIR_, PRE_>), dim3((unsigned)blocks),        \
-                     dim3(256), 0, st, x, gy, workspace, part_b, g, remap, kp)
-  if (wgrad_pair(N, W)) {
-    if (pre) BPK_WG(true, true); else BPK_WG(true, false);
+#define BPK_WG(PAIR_, PRE_, TWO_)                                                                \
+  hipLaunchKernelGGL((wino_wgrad_pipe_kernel<kNB, PAIR_, PRE_, TWO_>), dim3((unsigned)blocks),  \
+                     dim3(256), 0, st, x, gy, workspace, part_b, g, remap, kp, x2, gy2)
+  if (N2 > 0) {  // two sources (no prologue)
+    if (wgrad_pair(N, W)) BPK_WG(true, false, true); else BPK_WG(false, false, true);
+  } else if (wgrad_pair(N, W)) {
+    if (pre) BPK_WG(true, true, false); else BPK_WG(true, false, false);
   } else {
-    if (pre) BPK_WG(false, true); else BPK_WG(false, false);
+    if (pre) BPK_WG(false, true, false); else BPK_WG(false, false, false);
   }
 #undef BPK_WG
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad");
@@ -562,3 +611,5 @@ extern "C" int bpk_conv3x3_wino_wgrad_pre_f32(const float* x, const float* pre, 
   BPK_LAUNCH_CHECK("conv3x3_wino_wgrad_reduce");
   return BPK_OK;
 }
+
+}  // namespace

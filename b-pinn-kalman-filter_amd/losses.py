@@ -328,6 +328,9 @@ def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
 # point) 26.3 / 32.1 / 33.9 steps/s with 1 / 2 / 4 copies; B = 32 20.7 / 21.4 with 2 / 4;
 # B = 64 14.3 / 15.5 / 13.8 with 1 / 2 / 4 (profiles/r06_pinn_copies.txt).
 _COPIES = os.environ.get("BPK_PINN_COPIES", "auto")
+# the PINN backward's weight gradients deferred and run two sources per launch
+# (op.conv.deferred_weight_grads); BPK_DEFER_WGRAD=0: autograd's per-node weight gradients
+_DEFER_WGRAD = os.environ.get("BPK_DEFER_WGRAD", "1") == "1"
 _COPIES_AUTO = ((32, 4), (64, 2))  # (largest per-GPU batch, copies); larger batches: 1
 
 
@@ -400,7 +403,11 @@ def get_pinn_step_fn(config, train, optimize_fn, ctx=None, graph=False):
             from op import conv as conv_op
             with conv_op.batched_filters(model, enabled=batch[0].is_cuda):
                 loss, pinn_loss, data_loss = loss_fn(model, operator, batch)
-                loss.backward()
+                # weight gradients two sources per launch (op.conv.deferred_weight_grads);
+                # not under the bucketer, whose all-reduces ride the accumulation hooks
+                with conv_op.deferred_weight_grads(_DEFER_WGRAD and bucketer[0] is None
+                                                   and batch[0].is_cuda):
+                    loss.backward()
             # the values only: a returned loss that still carries the spent autograd graph
             # keeps the parameters' AccumulateGrad nodes alive, and a hipGraph captured later
             # on another stream (get_pinn_step_fn(graph=True)) then accumulates through them
@@ -493,7 +500,8 @@ class _PinnGraphStep:
                         p.grad = None
                     with conv_op.batched_filters(model):
                         loss, _pl, _dl = self.loss_fn(model, sop, self.static, self.noise)
-                        loss.backward(inputs=params)
+                        with conv_op.deferred_weight_grads(_DEFER_WGRAD):
+                            loss.backward(inputs=params)
             # nothing of the warm-up may be freed while the capture runs: a block released
             # mid-capture went back to the general pool and could be handed to the graph, which
             # then shared it with eager allocations after the capture (replays read garbage a
@@ -519,7 +527,8 @@ class _PinnGraphStep:
                 # table and the transform buffers were built by the warm-up)
                 with conv_op.batched_filters(model):
                     loss, pl, dl = self.loss_fn(model, sop, self.static, self.noise)
-                    loss.backward(inputs=params)
+                    with conv_op.deferred_weight_grads(_DEFER_WGRAD):
+                        loss.backward(inputs=params)
                 live = [(gb, p.grad) for gb, p in zip(gbufs, params) if p.grad is not None]
                 torch._foreach_copy_([a for a, _ in live], [b for _, b in live])
                 obuf[:3].copy_(torch.stack([loss.detach(), pl.detach(), dl.detach()]))

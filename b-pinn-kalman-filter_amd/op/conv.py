@@ -820,7 +820,7 @@ class _Conv3x3FT(torch.autograd.Function):
         if want_grad(ctx, 1):
             if torch.is_grad_enabled():
                 gw = _Wgrad3x3.apply(gy, x, tuple(w.shape))
-            else:
+            elif not _defer_wgrad(w, gy, x, ("3x3",)):
                 gw = _wgrad_impl(gy, x, tuple(w.shape), False)[0]
         return gx, gw
 
@@ -845,6 +845,7 @@ class _Conv3x3(torch.autograd.Function):
         mark_inputs(ctx, x, weight, bias, skip, div)
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.bias_leaf = bias if bias is not None and bias.is_leaf else None
         ctx.div = float(div)
         return _fwd_impl(x, weight, bias, skip, div)
 
@@ -864,6 +865,9 @@ class _Conv3x3(torch.autograd.Function):
                 gw = _Wgrad3x3.apply(x, gy, tuple(weight.shape))
             if want_b:
                 gb = gy.sum((0, 2, 3))
+        elif (want_grad(ctx, 1) and (not want_b or ctx.bias_leaf is not None)
+              and _defer_wgrad(weight, x, gy, ("3x3",), ctx.bias_leaf if want_b else None)):
+            pass  # weight (and bias) gradients deferred to the end of the backward pass
         elif want_grad(ctx, 1) or want_b:
             dw, gb = _wgrad_impl(x, gy, tuple(weight.shape), want_b)
             gw = dw if want_grad(ctx, 1) else None
@@ -890,6 +894,183 @@ class _Wgrad3x3(torch.autograd.Function):
         if want_grad(ctx, 1):
             ggy = _conv_any(x, ggw)
         return gx, ggy, None
+
+
+# ---------------------------------------------------------------- deferred weight gradients
+# The PINN step's final backward (losses.get_pinn_step_fn) reaches almost every conv weight
+# twice: through the conv of the forward and through its backward-data conv recorded by the
+# residual's first-order pass (create_graph).  Each contribution is a weight-gradient launch
+# (plus, at small batches, its split-K reduce), and autograd adds the two in the weight's input
+# buffer -- three to five launches per weight, ~130 weights.  Inside
+# `deferred_weight_grads()` the backward nodes only record the (input, output-gradient) pair of
+# a leaf weight (and of its bias); when the block ends, each weight's pairs run as ONE
+# weight-gradient launch over both sources (bpk_conv3x3_wino_wgrad2_f32 /
+# bpk_conv2d_igemm_wgrad2_f32: the K sum runs over the images of both pairs) and the result is
+# written to .grad (added when .grad already holds a gradient).  Per distinct shape the
+# two-source launch is timed once against the two separate launches + add, and the faster kept.
+# Same sums as autograd's up to the order of the additions (one K sum instead of two plus an
+# add); the bias gradient comes from the forward conv's pair alone, as before.
+_DEFER = [None]
+
+
+class _Deferral:
+    def __init__(self):
+        self.entries = {}  # id(weight) -> [weight, bias leaf or None, kind, [(X, GY, has_b)]]
+
+
+@contextlib.contextmanager
+def deferred_weight_grads(enabled=True):
+    """Weight (and bias) gradients of the convs' backward nodes are recorded while this block
+    runs a backward pass and computed -- two sources per launch -- when it ends.  Only for
+    backward passes whose result is read from .grad (loss.backward(), not autograd.grad),
+    and not with gradient hooks on the parameters (they would not fire)."""
+    if not enabled or _DEFER[0] is not None:
+        yield
+        return
+    d = _Deferral()
+    _DEFER[0] = d
+    try:
+        yield
+    finally:
+        _DEFER[0] = None
+    _flush_deferred(d)
+
+
+def _defer_wgrad(weight, X, GY, kind, bias=None) -> bool:
+    """Record the pair (X, GY) -- dW += wgrad(X, GY) -- of a leaf `weight` (and, with `bias`,
+    that pair's bias gradient sum(GY)) for the end of the active deferred_weight_grads()
+    block; False when no block is active or the weight is not a leaf."""
+    d = _DEFER[0]
+    if d is None or not weight.is_leaf or not weight.requires_grad or not X.is_cuda:
+        return False
+    e = d.entries.get(id(weight))
+    if e is None:
+        e = d.entries[id(weight)] = [weight, None, kind, []]
+    elif e[2] != kind:
+        return False
+    if bias is not None:
+        if e[1] is not None:
+            return False  # a second bias-bearing use: keep the plain path for this one
+        e[1] = bias
+    e[3].append((X.detach(), GY.detach(), bias is not None))
+    return True
+
+
+def _accum_grad(p, g):
+    if p.grad is None:
+        p.grad = g
+    else:
+        p.grad.add_(g)
+
+
+def _flush_deferred(d):
+    with torch.no_grad():
+        for w, b, kind, pairs in d.entries.values():
+            pairs = sorted(pairs, key=lambda t: not t[2])  # the bias-bearing pair first
+            dw, db = _wgrad_pairs(kind, tuple(w.shape), pairs)
+            _accum_grad(w, dw)
+            if b is not None:
+                _accum_grad(b, db)
+
+
+def _wgrad_one(kind, wshape, X, GY, want_b):
+    if kind[0] == "3x3":
+        return _wgrad_impl(X, GY, wshape, want_b)
+    return _wgrad_fn(X, GY, wshape, kind[1], bool(want_b))
+
+
+def _wgrad_separate(kind, wshape, pairs):
+    dw = db = None
+    for X, GY, hb in pairs:
+        w_, b_ = _wgrad_one(kind, wshape, X, GY, hb)
+        dw = w_ if dw is None else dw.add_(w_)
+        if hb:
+            db = b_
+    return dw, db
+
+
+def _two_source_ok(kind, wshape, p1, p2):
+    (X1, G1, _), (X2, G2, _) = p1, p2
+    if X1.shape[1:] != X2.shape[1:] or G1.shape[1:] != G2.shape[1:]:
+        return None
+    if X1.dtype != torch.float32 or X2.dtype != torch.float32:
+        return None
+    N1, C, H, W = X1.shape
+    N = N1 + X2.shape[0]
+    if kind[0] == "3x3":
+        if (_WGRAD and bool(lib.bpk_conv3x3_wino_wgrad_supported(N, C, wshape[0], H, W))
+                and (W != 8 or N1 % 2 == 0)):
+            return "wino"
+        if _IGEMM and _igemm_shape_ok((N, C, H, W), tuple(wshape), (1, 1), (1, 1)):
+            return "igemm"
+        return None
+    cfg = kind[1]
+    if _IGEMM and int(cfg[3]) == 1 and _pair(cfg[2]) == (1, 1) and _igemm_shape_ok(
+            (N, C, H, W), tuple(wshape), _pair(cfg[0]), _pair(cfg[1])):
+        return "igemm"
+    return None
+
+
+def _wgrad_pairs(kind, wshape, pairs):
+    if len(pairs) != 2:
+        return _wgrad_separate(kind, wshape, pairs)
+    how = _two_source_ok(kind, wshape, pairs[0], pairs[1])
+    if how is None:
+        return _wgrad_separate(kind, wshape, pairs)
+    (X1, G1, hb), (X2, G2, _) = pairs
+    if how == "wino":
+        two = lambda: conv3x3_wgrad2_raw(X1, G1, X2, G2, wshape, hb)  # noqa: E731
+    else:
+        s, p = ((1, 1), (1, 1)) if kind[0] == "3x3" else (_pair(kind[1][0]), _pair(kind[1][1]))
+        two = lambda: conv2d_weight_igemm2_raw(X1, G1, X2, G2, wshape, s, p, hb)  # noqa: E731
+    key = ("w2", kind[0], tuple(X1.shape), tuple(X2.shape), tuple(G1.shape), tuple(wshape),
+           None if kind[0] == "3x3" else kind[1], bool(hb))
+    return _pick_any(key, [two, lambda: _wgrad_separate(kind, wshape, pairs)])
+
+
+def conv3x3_wgrad2_raw(x, gy, x2, gy2, wshape, bias_grad=False):
+    """(dw, db or None): the 3x3 weight gradient summed over two (x, gy) sources in one
+    Winograd launch (db: the first source's); == conv3x3_wgrad_raw(x, gy) + (x2, gy2)."""
+    x, gy, x2, gy2 = (t.detach().contiguous() for t in (x, gy, x2, gy2))
+    N, C, H, W = x.shape
+    N2 = x2.shape[0]
+    Cout = wshape[0]
+    if (tuple(gy.shape) != (N, Cout, H, W) or tuple(x2.shape) != (N2, C, H, W)
+            or tuple(gy2.shape) != (N2, Cout, H, W)):
+        raise RuntimeError("conv3x3_wgrad2: mismatched sources")
+    nbytes = lib.bpk_conv3x3_wino_wgrad_workspace_bytes(N + N2, C, Cout, H, W)
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
+    dw = torch.empty((Cout, C, 3, 3), dtype=torch.float32, device=x.device)
+    db = torch.empty((Cout,), dtype=torch.float32, device=x.device) if bias_grad else None
+    check(lib.bpk_conv3x3_wino_wgrad2_f32(
+        x.data_ptr(), gy.data_ptr(), x2.data_ptr(), gy2.data_ptr(), N2, dw.data_ptr(),
+        None if db is None else db.data_ptr(), ws.data_ptr(), N, C, Cout, H, W,
+        stream_ptr(x.device)), "conv3x3_wgrad2")
+    flops.wino3x3("wino_wgrad", N + N2, C, Cout, H, W)
+    return dw, db
+
+
+def conv2d_weight_igemm2_raw(x, gy, x2, gy2, wshape, stride=1, padding=0, bias_grad=False):
+    """(dw, db or None) of a general conv summed over two (x, gy) sources in one implicit-GEMM
+    launch (db: the first source's)."""
+    s, p = _pair(stride), _pair(padding)
+    x, gy, x2, gy2 = (t.detach().contiguous() for t in (x, gy, x2, gy2))
+    N, C, H, W = x.shape
+    N2 = x2.shape[0]
+    Co, _, KH, KW = (int(v) for v in wshape)
+    Ho, Wo = gy.shape[2], gy.shape[3]
+    if tuple(x2.shape[1:]) != (C, H, W) or tuple(gy2.shape) != (N2, Co, Ho, Wo):
+        raise RuntimeError("conv2d_igemm_wgrad2: mismatched sources")
+    dw = torch.empty((Co, C, KH, KW), dtype=torch.float32, device=x.device)
+    db = torch.empty((Co,), dtype=torch.float32, device=x.device) if bias_grad else None
+    ws = _igemm_ws(2, N + N2, C, H, W, Co, KH, KW, s, p, Ho, Wo, bias_grad, x.device)
+    check(lib.bpk_conv2d_igemm_wgrad2_f32(x.data_ptr(), gy.data_ptr(), x2.data_ptr(),
+                                          gy2.data_ptr(), N2, dw.data_ptr(),
+                                          None if db is None else db.data_ptr(), ws.data_ptr(),
+                                          N, C, H, W, Co, KH, KW, s[0], s[1], p[0], p[1], Ho, Wo,
+                                          stream_ptr(x.device)), "conv2d_igemm_wgrad2")
+    flops.add("igemm_wgrad", 2.0 * (N + N2) * Co * C * KH * KW * Ho * Wo)
+    return dw, db
 
 
 def _needs_grad(*ts):
@@ -1352,6 +1533,7 @@ class _ConvG(torch.autograd.Function):
             ctx.save_for_backward(x, w)
             ctx.cfg = cfg
             ctx.has_b = b is not None
+            ctx.bias_leaf = b if b is not None and b.is_leaf else None
         if _ig_ok(x, w, cfg):
             return conv2d_select(x, w, b, cfg[0], cfg[1])
         with torch.no_grad():
@@ -1363,7 +1545,11 @@ class _ConvG(torch.autograd.Function):
         gx = _convt_fn(gy, w, tuple(x.shape), ctx.cfg) if want_grad(ctx, 0) else None
         gw = gb = None
         want_b = ctx.has_b and want_grad(ctx, 2)
-        if want_grad(ctx, 1) or want_b:
+        if (not torch.is_grad_enabled() and want_grad(ctx, 1)
+                and (not want_b or ctx.bias_leaf is not None)
+                and _defer_wgrad(w, x, gy, ("gen", ctx.cfg), ctx.bias_leaf if want_b else None)):
+            pass  # deferred to the end of the backward pass
+        elif want_grad(ctx, 1) or want_b:
             gw, gb = _wgrad_fn(x, gy, tuple(w.shape), ctx.cfg, bool(want_b))
             if not want_grad(ctx, 1):
                 gw = None
@@ -1391,7 +1577,10 @@ class _ConvTG(torch.autograd.Function):
     def backward(ctx, gz):
         u, w = ctx.saved_tensors
         gu = _conv_fn(gz, w, ctx.cfg) if want_grad(ctx, 0) else None
-        gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg)[0] if want_grad(ctx, 1) else None
+        gw = None
+        if want_grad(ctx, 1) and (torch.is_grad_enabled()
+                                  or not _defer_wgrad(w, gz, u, ("gen", ctx.cfg))):
+            gw = _wgrad_fn(gz, u, tuple(w.shape), ctx.cfg)[0]
         return gu, gw, None, None
 
 

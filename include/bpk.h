@@ -42,13 +42,6 @@ const char* bpk_last_error(void);
 /* Returns BPK_ABI_VERSION. */
 int bpk_abi_version(void);
 
-/* Split-K launches (implicit-GEMM convs, Winograd / 1x1 weight gradients at small batches)
- * with at most this many K-slices combine their partials inside the launch: the workgroup that
- * finishes a tile's last slice sums the slices in slice order (the same sum as the separate
- * reduce kernel, bit for bit) and writes the tile, so no reduce launch follows.  Default
- * BPK_SPLITK_FUSE_MAX (environment) or 16; 0 = always launch the reduce kernel.  Returns the
- * previous value.  Not a reference interface: a tuning / A-B switch of this library. */
-int bpk_splitk_set_fuse_max(int max_splits);
 
 /* ------------------------------------------------------------------------- *
  * upfirdn2d: zero-insert upsample by (up_x, up_y), pad (negative = crop),
@@ -506,6 +499,15 @@ int bpk_conv3x3_wino_wgrad_bias_f32(const float* x, const float* gy, float* dw, 
 int bpk_conv3x3_wino_wgrad_pre_f32(const float* x, const float* pre, const float* gy, float* dw,
                                    float* db, float* workspace, int N, int Cin, int Cout, int H,
                                    int W, void* stream);
+/* The weight gradient summed over two (x, gy) sources in one launch: dw = wgrad(x, gy) +
+ * wgrad(x2, gy2) with x2 [N2, Cin, H, W], gy2 [N2, Cout, H, W]; db (optional) = the FIRST
+ * source's bias gradient.  Workspace: bpk_conv3x3_wino_wgrad_workspace_bytes(N + N2, ...).
+ * 8-wide images need N even.  The deferred weight gradients of the PINN backward (a conv and
+ * its first-order backward-data conv share the weight): one launch and one reduce instead of
+ * two each plus autograd's accumulation add -- no reference interface of its own. */
+int bpk_conv3x3_wino_wgrad2_f32(const float* x, const float* gy, const float* x2, const float* gy2,
+                                int N2, float* dw, float* db, float* workspace, int N, int Cin,
+                                int Cout, int H, int W, void* stream);
 
 /* 3x3 / stride 1 / pad 1 conv with a small channel count on one side (VALU, HBM-bound):
  * the score networks' conv_in (Cin = image channels, models/ncsnpp.py) and output_skip
@@ -619,6 +621,17 @@ int bpk_conv2d_igemm_wgrad_f32(const float* x, const float* gy, float* dw, float
                                void* workspace, int N, int Cin, int H, int W, int Cout, int KH,
                                int KW, int sh, int sw, int ph, int pw, int Ho, int Wo,
                                void* stream);
+/* The weight gradient summed over two (x, gy) sources of the same geometry in one launch:
+ * dw = wgrad(x, gy) + wgrad(x2, gy2), x [N, Cin, H, W], x2 [N2, Cin, H, W] (gy, gy2 likewise);
+ * db (optional) = the bias gradient of the FIRST source only.  The K sum runs over the images
+ * of x then x2 (workspace: bpk_conv2d_igemm_workspace_bytes(2, N + N2, ...)).  Replaces the
+ * second weight-gradient launch, its reduce and autograd's accumulation add for a weight that
+ * two convs of one backward pass use (the PINN residual: each conv and its backward-data conv
+ * of the first-order pass) -- no reference interface of its own. */
+int bpk_conv2d_igemm_wgrad2_f32(const float* x, const float* gy, const float* x2, const float* gy2,
+                                int N2, float* dw, float* db, void* workspace, int N, int Cin,
+                                int H, int W, int Cout, int KH, int KW, int sh, int sw, int ph,
+                                int pw, int Ho, int Wo, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * InstanceNorm2d (affine=False) + activation, forward / backward / double backward:

@@ -1250,48 +1250,85 @@ def test_conv2d_igemm_fwd_dgrad_wgrad_vs_fp64(hip, case):
     assert none is None and torch.equal(dw2, dw)
 
 
-@pytest.fixture
-def splitk_fuse(hip):
-    """Set the in-launch split-K limit (bpk_splitk_set_fuse_max) for a test; restored after."""
-    from op._lib import lib
-    prev = lib.bpk_splitk_set_fuse_max(16)
-    lib.bpk_splitk_set_fuse_max(prev)
-    yield lambda v: lib.bpk_splitk_set_fuse_max(v)
-    lib.bpk_splitk_set_fuse_max(prev)
-
-
-@pytest.mark.parametrize("case", _IG_CASES + [
-    (8, 16, 8, 8, 32, 3, 1, 1),      # PINN pyramid level 8^2 at B = 8: forward / dgrad split
-    (8, 128, 4, 4, 96, 3, 1, 1),     # 4^2 level, 64 x 64 tiles with a ragged M
-    (16, 96, 2, 2, 2, 3, 1, 1),      # 2-channel head at 2^2: 16 x 256 tiles, long K
-    (8, 32, 16, 16, 16, 4, 2, 1),    # ConvTranspose2d(k4, s2)-class shapes
+@pytest.mark.parametrize("case", [
+    # kind, N1, N2, Cin, H, W, Cout, k, stride, pad
+    ("wino", 8, 8, 32, 16, 16, 32, 3, 1, 1),      # PINN pyramid conv, both sources B = 8
+    ("wino", 4, 6, 64, 8, 8, 48, 3, 1, 1),        # 8-wide images (pair form), uneven sources
+    ("wino", 3, 5, 32, 32, 32, 16, 3, 1, 1),      # odd first source, 32^2
+    ("igemm", 8, 8, 16, 64, 64, 16, 3, 1, 1),     # PINN 16-channel conv at 64^2 (16 x 256 tiles)
+    ("igemm", 5, 3, 49, 8, 8, 128, 3, 1, 1),      # corr_conv first conv (Cin 49)
+    ("igemm", 4, 4, 16, 32, 32, 32, 3, 2, 1),     # stride-2 pyramid conv
+    ("igemm", 2, 3, 6, 9, 9, 4, 4, 2, 1),         # k4 s2 (ConvTranspose class)
 ])
-def test_conv2d_igemm_splitk_in_launch_matches_reduce_kernel(hip, splitk_fuse, case):
-    """The in-launch split-K combine (the workgroup drawing a tile's last ticket sums the
-    slices, bpk_common.h splitk_last) gives results bit-identical to the separate reduce
-    kernel, for every product of the conv, and stays so over repeated launches (every launch
-    must leave its tile counters at zero for the next)."""
-    from op.conv import conv2d_igemm_raw, conv2d_input_igemm_raw, conv2d_weight_igemm_raw
-    N, C, H, W, Co, k, s, p = case
-    g = torch.Generator().manual_seed(7 + sum(case))
-    x = torch.randn(N, C, H, W, generator=g).to(hip)
-    w = (torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5).to(hip)
-    b = torch.randn(Co, generator=g).to(hip)
+def test_wgrad_two_sources_match_sum_vs_fp64(hip, case):
+    """bpk_conv3x3_wino_wgrad2_f32 / bpk_conv2d_igemm_wgrad2_f32 (the deferred weight gradients
+    of op.conv.deferred_weight_grads): dw = wgrad(x1, gy1) + wgrad(x2, gy2) in one launch, db =
+    the first source's bias gradient -- vs float64 autograd on the CPU, within 2e-5 of the
+    gradient's magnitude (an image of the wrong source, or the second source's bias column,
+    shows up as O(1))."""
+    from op.conv import conv2d_weight_igemm2_raw, conv3x3_wgrad2_raw
+    kind, N1, N2, C, H, W, Co, k, s, p = case
+    g = torch.Generator().manual_seed(11 + sum(case[1:]))
+    x1, x2 = torch.randn(N1, C, H, W, generator=g), torch.randn(N2, C, H, W, generator=g)
+    w = (torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5).double().requires_grad_()
+    b = torch.zeros(Co, dtype=torch.float64, requires_grad=True)
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    gy = torch.randn(N, Co, Ho, Wo, generator=g).to(hip)
+    gy1, gy2 = torch.randn(N1, Co, Ho, Wo, generator=g), torch.randn(N2, Co, Ho, Wo, generator=g)
+    y1 = F.conv2d(x1.double(), w, b, s, p)
+    y2 = F.conv2d(x2.double(), w, None, s, p)
+    gw_ref, gb_ref = torch.autograd.grad((y1 * gy1.double()).sum() + (y2 * gy2.double()).sum(),
+                                         (w, b))
+    d = [t.to(hip) for t in (x1, gy1, x2, gy2)]
+    if kind == "wino":
+        dw, db = conv3x3_wgrad2_raw(*d, tuple(w.shape), bias_grad=True)
+    else:
+        dw, db = conv2d_weight_igemm2_raw(*d, tuple(w.shape), s, p, bias_grad=True)
+    for got, ref, what in ((dw, gw_ref, "dw"), (db, gb_ref, "db")):
+        tol = 2e-5 * max(1.0, float(ref.abs().max()))
+        err = float((got.double().cpu() - ref).abs().max())
+        assert err <= tol, f"{what}: {err} > {tol}"
 
-    def run():
-        return (conv2d_igemm_raw(x, w, b, s, p), conv2d_input_igemm_raw(x.shape, w, gy, s, p),
-                *conv2d_weight_igemm_raw(x, w.shape, gy, s, p, bias_grad=True))
 
-    splitk_fuse(0)
-    ref = run()
-    splitk_fuse(4096)  # every split count in-launch
-    for _ in range(6):
-        got = run()
-        for a, r, name in zip(got, ref, ("forward", "dgrad", "wgrad", "bias grad")):
-            assert torch.equal(a, r), name
-    torch.cuda.synchronize()
+def test_deferred_weight_grads_match_autograd(hip):
+    """op.conv.deferred_weight_grads around the backward of a PINN-shaped double backward
+    (a first-order input gradient with create_graph, then a loss of it and of the output):
+    every parameter's .grad matches autograd's per-node weight gradients (the same sums up to
+    the order of the additions), through Winograd 3x3 convs, a general stride-2 conv and a
+    conv transpose; non-deferred parameters (none here) and the accumulation into an existing
+    .grad keep autograd's semantics."""
+    from models import layers
+    from op import conv as conv_op
+    from op.fused_act import leaky_relu
+    torch.manual_seed(3)
+    net = torch.nn.ModuleList([
+        layers.Conv2d(16, 32, 3, padding=1), layers.Conv2d(32, 32, 3, padding=1),
+        layers.Conv2d(32, 16, 3, stride=2, padding=1),
+        layers.ConvTranspose2d(16, 16, 2, stride=2)]).to(hip)
+    x = torch.randn(8, 16, 16, 16, device=hip, requires_grad=True)
+
+    def run(defer, twice=False):
+        for q in net.parameters():
+            q.grad = None
+        for _ in range(2 if twice else 1):
+            h = x
+            for i, m in enumerate(net):
+                h = m(h)
+                if i < len(net) - 1:
+                    h = leaky_relu(h, 0.1)
+            gx, = torch.autograd.grad(h.sum(), x, create_graph=True)
+            loss = (gx ** 2).sum() + (h ** 2).sum()
+            with conv_op.deferred_weight_grads(defer):
+                loss.backward(inputs=list(net.parameters()))
+        return [q.grad.clone() for q in net.parameters()]
+
+    ref = run(False)
+    got = run(True)
+    for a, r in zip(got, ref):
+        assert torch.allclose(a, r, rtol=1e-5, atol=1e-5 * float(r.abs().max())), \
+            float((a - r).abs().max())
+    got2 = run(True, twice=True)  # .grad already set: the deferred gradients add into it
+    for a, r in zip(got2, ref):
+        assert torch.allclose(a, 2 * r, rtol=1e-5, atol=2e-5 * float(r.abs().max()))
 
 
 @pytest.mark.parametrize("case", [

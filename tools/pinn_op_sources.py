@@ -49,7 +49,7 @@ class A:
 args = A()
 args.batch = None
 args.weak = False
-args.per_rank_of = None
+args.per_rank_of = int(sys.argv[1]) if len(sys.argv) > 1 else None  # 8: the B = 8 rank
 args.pinn_warmup, args.pinn_steps, args.pinn_eager = 1, 1, True
 dev = torch.device("cuda:0")
 bench.bench_pinn(args, DistContext(), dev)  # warm (conv choices, filter caches)
