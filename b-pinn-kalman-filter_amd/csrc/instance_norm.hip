@@ -82,7 +82,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void in_bwd(const T* __restrict__ dy, const T* __restrict__ x,
                                               const T* __restrict__ mean,
                                               const T* __restrict__ rstd, T* __restrict__ dx,
-                                              int64_t planes, int64_t M, int act) {
+                                              int64_t planes, int64_t M, int act,
+                                              const T* __restrict__ add) {
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (p >= planes) return;
@@ -101,7 +102,8 @@ __global__ __launch_bounds__(256) void in_bwd(const T* __restrict__ dy, const T*
   for (int64_t i = lane; i < M; i += 64) {
     const T z = (xp[i] - mu) * r;
     const T g = dp[i] * act_d1(z, act);
-    op[i] = r * (g - mg - z * mgz);
+    const T o = r * (g - mg - z * mgz);
+    op[i] = add ? o + add[p * M + i] : o;
   }
 }
 
@@ -249,7 +251,7 @@ template <typename T, int V, int W>
 __global__ __launch_bounds__(256) void in_bwd_blk(const T* __restrict__ dy, const T* __restrict__ x,
                                                   const T* __restrict__ mean,
                                                   const T* __restrict__ rstd, T* __restrict__ dx,
-                                                  int64_t M, int act) {
+                                                  int64_t M, int act, const T* __restrict__ add) {
   __shared__ T sh[4];
   const int64_t p = blockIdx.x;
   const T mu = mean[p], r = rstd[p];
@@ -283,6 +285,12 @@ __global__ __launch_bounds__(256) void in_bwd_blk(const T* __restrict__ dy, cons
     T o[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) o[j] = r * (g[k][j] - mg - z[k][j] * mgz);
+    if (add) {  // the identity-skip gradient of the residual block, added in the same pass
+      T a[W];
+      ld<T, W>(add + p * M + e, a);
+#pragma unroll
+      for (int j = 0; j < W; ++j) o[j] = o[j] + a[j];
+    }
     st<T, W>(dx + p * M + e, o);
   }
 }
@@ -423,17 +431,17 @@ int fwd_impl(const T* x, T* y, T* mean, T* rstd, int64_t planes, int64_t M, doub
 
 template <typename T>
 int bwd_impl(const T* dy, const T* x, const T* mean, const T* rstd, T* dx, int64_t planes,
-             int64_t M, int act, void* stream) {
+             int64_t M, int act, void* stream, const T* add = nullptr) {
   IN_CHECK("instance_norm_act_bwd");
   BPK_REQUIRE(dy && x && mean && rstd && dx, "instance_norm_act_bwd: null pointer");
   if (planes == 0) return BPK_OK;
   hipStream_t st = bpk::as_stream(stream);
   if (blk_runs(M, 1) && planes < (1ll << 31)) {
-    const int w = blk_w<T>(dy, x, dx, M);
-    IN_BLK(in_bwd_blk, T, w, dy, x, mean, rstd, dx, M, act)
+    const int w = blk_w<T>(dy, x, dx, M) == 4 && blk_w<T>(add, nullptr, nullptr, M) == 4 ? 4 : 1;
+    IN_BLK(in_bwd_blk, T, w, dy, x, mean, rstd, dx, M, act, add)
   } else {
     hipLaunchKernelGGL(in_bwd<T>, dim3(blocks_for(planes)), dim3(256), 0, st, dy, x, mean, rstd,
-                       dx, planes, M, act);
+                       dx, planes, M, act, add);
   }
   BPK_LAUNCH_CHECK("instance_norm_act_bwd");
   return BPK_OK;
@@ -478,6 +486,12 @@ int bpk_instance_norm_act_bwd_f64(const double* dy, const double* x, const doubl
                                   const double* rstd, double* dx, int64_t planes, int64_t M,
                                   int act, void* stream) {
   return bwd_impl(dy, x, mean, rstd, dx, planes, M, act, stream);
+}
+int bpk_instance_norm_act_bwd_add_f32(const float* dy, const float* x, const float* mean,
+                                      const float* rstd, const float* add, float* dx,
+                                      int64_t planes, int64_t M, int act, void* stream) {
+  BPK_REQUIRE(add, "instance_norm_act_bwd_add: null addend");
+  return bwd_impl(dy, x, mean, rstd, dx, planes, M, act, stream, add);
 }
 int bpk_instance_norm_act_bwd2_f32(const float* v, const float* dy, const float* x,
                                    const float* mean, const float* rstd, float* gdy, float* gx,

@@ -240,6 +240,8 @@ def skip_link(module: nn.Module, identity_skip: bool):
 
 
 _SKIP_LINK = os.environ.get("BPK_SKIP_LINK", "1") == "1"  # A/B switch
+# ResidualBlock (PressureNet): the input's two gradients added in the norm's backward kernel
+_IN_FANOUT = os.environ.get("BPK_IN_FANOUT", "1") == "1"
 
 
 def _dropout_off(m: nn.Dropout) -> bool:
@@ -644,6 +646,13 @@ class ResidualBlock(nn.Module):
             self.shortcut = ncsn_conv1x1(input_dim, output_dim)
         self.normalize1 = normalization(input_dim)
 
+    def _fused_ok(self, norm, x):
+        act = self.non_linearity
+        return (_IN_FUSED and x.is_cuda and x.dtype in (torch.float32, torch.float64)
+                and type(norm) is nn.InstanceNorm2d and not norm.affine
+                and not norm.track_running_stats and type(act) is nn.ELU
+                and act.alpha == 1.0 and not act.inplace)
+
     def _norm_act(self, norm, x):
         """act(norm(x)); InstanceNorm2d(affine=False) + ELU(1) on the fused HIP kernels
         (op.norm_act.instance_norm_act: forward, backward and double backward one launch
@@ -658,8 +667,16 @@ class ResidualBlock(nn.Module):
         return act(norm(x))
 
     def forward(self, x):
-        h = self.conv1(self._norm_act(self.normalize1, x))
-        skip = x if self.output_dim == self.input_dim else self.shortcut(x)
+        if _IN_FANOUT and self._fused_ok(self.normalize1, x) and torch.is_grad_enabled() \
+                and x.requires_grad:
+            # x feeds the first norm and the skip: one node takes both gradients and adds them
+            # in the norm's backward kernel (op.norm_act.instance_norm_act_fanout)
+            a1, xs = norm_act_op.instance_norm_act_fanout(x, self.normalize1.eps,
+                                                          norm_act_op.ACT_ELU)
+        else:
+            a1, xs = self._norm_act(self.normalize1, x), x
+        h = self.conv1(a1)
+        skip = xs if self.output_dim == self.input_dim else self.shortcut(xs)
         a = self._norm_act(self.normalize2, h)
         if _RES_TAIL and _is_3x3(a, self.conv2):
             # skip + conv2(a) with the add in the conv's epilogue (same rounding: the kernel

@@ -976,6 +976,9 @@ def _flush_deferred(d):
 def _wgrad_one(kind, wshape, X, GY, want_b):
     if kind[0] == "3x3":
         return _wgrad_impl(X, GY, wshape, want_b)
+    if kind[0] == "1x1":
+        dw, db = _wgrad1x1_raw(GY, X, bool(want_b))
+        return dw.view(wshape), db
     return _wgrad_fn(X, GY, wshape, kind[1], bool(want_b))
 
 
@@ -1004,6 +1007,9 @@ def _two_source_ok(kind, wshape, p1, p2):
         if _IGEMM and _igemm_shape_ok((N, C, H, W), tuple(wshape), (1, 1), (1, 1)):
             return "igemm"
         return None
+    if kind[0] == "1x1":
+        ok = _IGEMM and _igemm_shape_ok((N, C, H, W), tuple(wshape), (1, 1), (0, 0))
+        return "igemm" if ok else None
     cfg = kind[1]
     if _IGEMM and int(cfg[3]) == 1 and _pair(cfg[2]) == (1, 1) and _igemm_shape_ok(
             (N, C, H, W), tuple(wshape), _pair(cfg[0]), _pair(cfg[1])):
@@ -1021,10 +1027,11 @@ def _wgrad_pairs(kind, wshape, pairs):
     if how == "wino":
         two = lambda: conv3x3_wgrad2_raw(X1, G1, X2, G2, wshape, hb)  # noqa: E731
     else:
-        s, p = ((1, 1), (1, 1)) if kind[0] == "3x3" else (_pair(kind[1][0]), _pair(kind[1][1]))
+        s, p = {"3x3": ((1, 1), (1, 1)), "1x1": ((1, 1), (0, 0))}.get(kind[0]) or (
+            _pair(kind[1][0]), _pair(kind[1][1]))
         two = lambda: conv2d_weight_igemm2_raw(X1, G1, X2, G2, wshape, s, p, hb)  # noqa: E731
     key = ("w2", kind[0], tuple(X1.shape), tuple(X2.shape), tuple(G1.shape), tuple(wshape),
-           None if kind[0] == "3x3" else kind[1], bool(hb))
+           kind[1] if kind[0] == "gen" else None, bool(hb))
     return _pick_any(key, [two, lambda: _wgrad_separate(kind, wshape, pairs)])
 
 
@@ -1437,21 +1444,48 @@ class _Conv1x1(torch.autograd.Function):
     take second derivatives through the networks)."""
 
     @staticmethod
-    def forward(ctx, x, w2d, bias):
-        mark_inputs(ctx, x, w2d, bias)
+    def forward(ctx, x, w2d, bias, wref=None):
+        mark_inputs(ctx, x, w2d, bias, wref)
         ctx.save_for_backward(x, w2d)
+        # the [Cout, Cin, 1, 1] leaf parameter w2d is a view of (deferred weight gradients)
+        ctx.wref = wref
+        ctx.bias_leaf = bias if bias is not None and bias.is_leaf else None
         return _gemm1x1_raw(x, w2d, bias)
 
     @staticmethod
     def backward(ctx, gy):
         x, w2d = ctx.saved_tensors
-        gx = _c1_fn(gy, w2d.t()) if want_grad(ctx, 0) else None
+        gx = None
+        if want_grad(ctx, 0):
+            if ctx.wref is not None and torch.is_grad_enabled():  # the adjoint, still deferrable
+                gx = _Conv1x1.apply(gy, w2d.t(), None, _WRef(ctx.wref.t, not ctx.wref.transposed))
+            else:
+                gx = _c1_fn(gy, w2d.t())
         gw = gb = None
-        if want_grad(ctx, 1) or want_grad(ctx, 2):
+        want_b = want_grad(ctx, 2)
+        # the parameter's gradient from this node: sum gy x^T, or for the adjoint use (w2d is
+        # the parameter transposed) sum x gy^T -- the pair (X, GY) = (gy, x)
+        pair = (gy, x) if ctx.wref is not None and ctx.wref.transposed else (x, gy)
+        if (not torch.is_grad_enabled() and ctx.wref is not None and want_grad(ctx, 1)
+                and (not want_b or ctx.bias_leaf is not None)
+                and _defer_wgrad(ctx.wref.t, pair[0], pair[1], ("1x1",),
+                                 ctx.bias_leaf if want_b else None)):
+            pass  # deferred to the end of the backward pass
+        elif want_grad(ctx, 1) or want_grad(ctx, 2):
             gw, gb = _w1_fn(gy, x, bool(want_grad(ctx, 2)))
             if not want_grad(ctx, 1):
                 gw = None
-        return gx, gw, gb
+        return gx, gw, gb, None
+
+
+class _WRef:
+    """A parameter passed to a Function as a plain reference (no autograd edge); transposed:
+    the Function's weight is the parameter's transpose (the 1x1 conv's adjoint)."""
+    __slots__ = ("t", "transposed")
+
+    def __init__(self, t, transposed=False):
+        self.t = t
+        self.transposed = transposed
 
 
 class _Wgrad1x1(torch.autograd.Function):
@@ -1483,7 +1517,10 @@ def conv1x1_ad(x, weight, bias=None):
     require_hip(x, weight, bias, what="conv1x1")
     if not conv1x1_train_supported(x, weight):
         raise RuntimeError(f"conv1x1: unsupported shape {tuple(x.shape)} x {tuple(weight.shape)}")
-    return _c1_fn(x, weight.reshape(weight.shape[0], weight.shape[1]), bias)
+    w2d = weight.reshape(weight.shape[0], weight.shape[1])
+    if torch.is_grad_enabled() and weight.is_leaf and weight.dim() == 4:
+        return _Conv1x1.apply(x, w2d, bias, _WRef(weight))
+    return _c1_fn(x, w2d, bias)
 
 
 # ---------------------------------------------------------------- general convolutions

@@ -299,25 +299,35 @@ class _InstanceNormAct(Function):
 
 
 class _InstanceNormActBackward(Function):
-    """dx = d act(IN(x)) / dx applied to dy; differentiable once more (w.r.t. dy and x; mean
-    and rstd are functions of x already accounted for by the double-backward kernel)."""
+    """dx = d act(IN(x)) / dx applied to dy (+ add, the fan-out form's skip gradient, added in
+    the same kernel pass); differentiable once more (w.r.t. dy and x; mean and rstd are
+    functions of x already accounted for by the double-backward kernel; w.r.t. add: identity)."""
 
     @staticmethod
-    def forward(ctx, dy, x, mean, rstd, act):
+    def forward(ctx, dy, x, mean, rstd, act, add=None):
         P, M = _planes(x)
         dx = torch.empty_like(x)
-        check(_in_fns(x.dtype)[1](dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                                  dx.data_ptr(), P, M, act, stream_ptr(x.device)),
-              "instance_norm_act_bwd")
+        if add is not None and x.dtype == torch.float32:
+            add = add.contiguous()
+            check(lib.bpk_instance_norm_act_bwd_add_f32(
+                dy.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), add.data_ptr(),
+                dx.data_ptr(), P, M, act, stream_ptr(x.device)), "instance_norm_act_bwd_add")
+        else:
+            check(_in_fns(x.dtype)[1](dy.data_ptr(), x.data_ptr(), mean.data_ptr(),
+                                      rstd.data_ptr(), dx.data_ptr(), P, M, act,
+                                      stream_ptr(x.device)), "instance_norm_act_bwd")
+            if add is not None:  # float64 (gradcheck): the plain sum
+                dx.add_(add)
         ctx.save_for_backward(dy, x, mean, rstd)
         ctx.act = act
         return dx
 
     @staticmethod
     @once_differentiable
-    def backward(ctx, v):
+    def backward(ctx, v, *_):
         dy, x, mean, rstd = ctx.saved_tensors
         need_dy, need_x = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_add = len(ctx.needs_input_grad) > 5 and ctx.needs_input_grad[5]
         P, M = _planes(x)
         v = v.contiguous()
         gdy = torch.empty_like(x) if need_dy else None
@@ -326,7 +336,45 @@ class _InstanceNormActBackward(Function):
                                   rstd.data_ptr(), gdy.data_ptr() if gdy is not None else None,
                                   gx.data_ptr() if gx is not None else None, P, M, ctx.act,
                                   stream_ptr(x.device)), "instance_norm_act_bwd2")
-        return gdy, gx, None, None, None
+        return gdy, gx, None, None, None, (v if need_add else None)
+
+
+class _InstanceNormActFanout(Function):
+    """(act(IN(x)), x): for a residual block whose input feeds both its first norm and its
+    skip.  Both gradients reach this one node, and the skip's is added inside the norm's
+    backward kernel (bpk_instance_norm_act_bwd_add_f32) -- no accumulation launch of autograd's
+    -- in every derivative pass of the PINN residual (the first-order pass records the fused
+    backward, whose own backward hands the addend's gradient through unchanged)."""
+
+    @staticmethod
+    def forward(ctx, x, eps, act):
+        require_hip(x, what="instance_norm_act")
+        ctx.set_materialize_grads(False)
+        P, M = _planes(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(P, device=x.device, dtype=x.dtype)
+        rstd = torch.empty_like(mean)
+        check(_in_fns(x.dtype)[0](x.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                  P, M, float(eps), act, stream_ptr(x.device)),
+              "instance_norm_act_fwd")
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.act = act
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        x, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            return dskip, None, None
+        return (_InstanceNormActBackward.apply(dy.contiguous(), x, mean, rstd, ctx.act, dskip),
+                None, None)
+
+
+def instance_norm_act_fanout(x, eps=1e-5, act=ACT_ELU):
+    """(act(F.instance_norm(x, eps=eps)), x) -- the skip's gradient joins the norm's inside the
+    backward kernel (see _InstanceNormActFanout)."""
+    require_hip(x, what="instance_norm_act")
+    return _InstanceNormActFanout.apply(x.contiguous(), float(eps), int(act))
 
 
 def instance_norm_act(x, eps=1e-5, act=ACT_ELU):

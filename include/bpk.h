@@ -653,6 +653,12 @@ int bpk_instance_norm_act_bwd_f32(const float* dy, const float* x, const float* 
 int bpk_instance_norm_act_bwd_f64(const double* dy, const double* x, const double* mean,
                                   const double* rstd, double* dx, int64_t planes, int64_t M,
                                   int act, void* stream);
+/* dx = the backward above + add (same shapes): the residual block's skip gradient added in the
+ * same pass (PressureNet's ResidualBlock input feeds its first norm and its skip; autograd
+ * would add the two gradients in a separate launch). */
+int bpk_instance_norm_act_bwd_add_f32(const float* dy, const float* x, const float* mean,
+                                      const float* rstd, const float* add, float* dx,
+                                      int64_t planes, int64_t M, int act, void* stream);
 int bpk_instance_norm_act_bwd2_f32(const float* v, const float* dy, const float* x,
                                    const float* mean, const float* rstd, float* gdy, float* gx,
                                    int64_t planes, int64_t M, int act, void* stream);

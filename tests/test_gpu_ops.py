@@ -1293,9 +1293,11 @@ def test_deferred_weight_grads_match_autograd(hip):
     """op.conv.deferred_weight_grads around the backward of a PINN-shaped double backward
     (a first-order input gradient with create_graph, then a loss of it and of the output):
     every parameter's .grad matches autograd's per-node weight gradients (the same sums up to
-    the order of the additions), through Winograd 3x3 convs, a general stride-2 conv and a
-    conv transpose; non-deferred parameters (none here) and the accumulation into an existing
-    .grad keep autograd's semantics."""
+    the order of the additions), through Winograd 3x3 convs, a general stride-2 conv, a conv
+    transpose, 1x1 convs (PressureNet's shortcuts: the adjoint's transposed weight) and
+    PressureNet ResidualBlocks in their fan-out form (the skip gradient added inside the
+    InstanceNorm backward kernel); the accumulation into an existing .grad keeps autograd's
+    semantics."""
     from models import layers
     from op import conv as conv_op
     from op.fused_act import leaky_relu
@@ -1303,32 +1305,41 @@ def test_deferred_weight_grads_match_autograd(hip):
     net = torch.nn.ModuleList([
         layers.Conv2d(16, 32, 3, padding=1), layers.Conv2d(32, 32, 3, padding=1),
         layers.Conv2d(32, 16, 3, stride=2, padding=1),
-        layers.ConvTranspose2d(16, 16, 2, stride=2)]).to(hip)
+        layers.ConvTranspose2d(16, 16, 2, stride=2),
+        layers.ResidualBlock(16, 32), layers.ResidualBlock(32, 32),   # 1x1 shortcut, identity
+        layers.Conv2d(32, 8, 1)]).to(hip)
     x = torch.randn(8, 16, 16, 16, device=hip, requires_grad=True)
 
     def run(defer, twice=False):
         for q in net.parameters():
             q.grad = None
-        for _ in range(2 if twice else 1):
-            h = x
-            for i, m in enumerate(net):
-                h = m(h)
-                if i < len(net) - 1:
-                    h = leaky_relu(h, 0.1)
-            gx, = torch.autograd.grad(h.sum(), x, create_graph=True)
-            loss = (gx ** 2).sum() + (h ** 2).sum()
-            with conv_op.deferred_weight_grads(defer):
-                loss.backward(inputs=list(net.parameters()))
+        prev = layers._IN_FANOUT
+        layers._IN_FANOUT = defer  # the ResidualBlocks' fan-out form with it
+        try:
+            for _ in range(2 if twice else 1):
+                h = x
+                for i, m in enumerate(net):
+                    h = m(h)
+                    if i < 3:
+                        h = leaky_relu(h, 0.1)
+                gx, = torch.autograd.grad(h.sum(), x, create_graph=True)
+                loss = (gx ** 2).sum() + (h ** 2).sum()
+                with conv_op.deferred_weight_grads(defer):
+                    loss.backward(inputs=list(net.parameters()))
+        finally:
+            layers._IN_FANOUT = prev
         return [q.grad.clone() for q in net.parameters()]
 
     ref = run(False)
     got = run(True)
+    # absolute floor from the largest gradient: a conv bias in front of an InstanceNorm has an
+    # analytically zero gradient, whose computed value is rounding noise either way
+    scale = max(float(r.abs().max()) for r in ref)
     for a, r in zip(got, ref):
-        assert torch.allclose(a, r, rtol=1e-5, atol=1e-5 * float(r.abs().max())), \
-            float((a - r).abs().max())
+        assert torch.allclose(a, r, rtol=1e-5, atol=1e-5 * scale), float((a - r).abs().max())
     got2 = run(True, twice=True)  # .grad already set: the deferred gradients add into it
     for a, r in zip(got2, ref):
-        assert torch.allclose(a, 2 * r, rtol=1e-5, atol=2e-5 * float(r.abs().max()))
+        assert torch.allclose(a, 2 * r, rtol=1e-5, atol=2e-5 * scale)
 
 
 @pytest.mark.parametrize("case", [
@@ -1482,6 +1493,37 @@ def test_instance_norm_elu_gradgradcheck_and_third_order_refused(hip):
     (ddx,) = torch.autograd.grad((dx ** 2).sum(), x, create_graph=True)
     with pytest.raises(RuntimeError):
         ddx.sum().backward()
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 4, 5), (1, 2, 15, 20), (2, 8, 32, 32)])
+def test_instance_norm_elu_fanout(hip, shape):
+    """instance_norm_act_fanout(x) = (act(IN(x)), x) with the skip's gradient added inside the
+    backward kernel: float64 gradcheck / gradgradcheck of (y, x) -> any loss, and in float32
+    the fused add (bpk_instance_norm_act_bwd_add_f32) bit-identical to the plain backward plus
+    autograd's add, first and second order."""
+    from op.norm_act import instance_norm_act, instance_norm_act_fanout
+    torch.manual_seed(7)
+    x = torch.randn(*shape, dtype=torch.float64, device=hip, requires_grad=True)
+    w = torch.randn(*shape, dtype=torch.float64, device=hip)
+    f = lambda a: instance_norm_act_fanout(a)[0] * 2 + instance_norm_act_fanout(a)[1] * w  # noqa
+    assert torch.autograd.gradcheck(f, (x,))
+    assert torch.autograd.gradgradcheck(f, (x,))
+    xf = (torch.randn(*shape, device=hip) * 2 + 0.3).requires_grad_()
+    g1, g2 = torch.randn(*shape, device=hip), torch.randn(*shape, device=hip)
+    v = torch.randn(*shape, device=hip)
+
+    def grads(fan):
+        if fan:
+            y, xs = instance_norm_act_fanout(xf)
+        else:
+            y, xs = instance_norm_act(xf), xf
+        # one skip contribution: the fused add then sums the same two terms autograd does
+        (dx,) = torch.autograd.grad((y * g1).sum() + (xs * g2).sum(), xf, create_graph=True)
+        (ddx,) = torch.autograd.grad((dx * v).sum(), xf)
+        return dx.detach(), ddx
+
+    for a, b in zip(grads(True), grads(False)):
+        assert torch.equal(a, b)
 
 
 def test_instance_norm_elu_residual_block_matches_aten(hip, monkeypatch):
