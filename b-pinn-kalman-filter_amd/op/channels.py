@@ -37,11 +37,41 @@ class _Split(Function):
         ctx.dim = dim
         ctx.shape = tuple(g.shape)
         ctx.sizes = sizes
+        ctx.set_materialize_grads(False)
         return tuple(torch.split(g, list(sizes), dim))
 
     @staticmethod
     def backward(ctx, *gs):
-        return _Cat.apply(ctx.dim, *gs), None, None
+        if all(g is not None for g in gs):
+            return _Cat.apply(ctx.dim, *gs), None, None
+        # pieces nobody used (PINN.forward_residual_copies reads copy 0 of most splits): one
+        # zero fill and a copy per used piece, not a fill per unused piece plus a cat
+        present = tuple(g is not None for g in gs)
+        return _PadCat.apply(ctx.dim, ctx.sizes, present, ctx.shape,
+                             *[g for g in gs if g is not None]), None, None
+
+
+class _PadCat(Function):
+    """cat along `dim` of the pieces marked present, zeros for the others; backward: views of
+    the present pieces (a split)."""
+
+    @staticmethod
+    def forward(ctx, dim, sizes, present, shape, *gs):
+        ctx.dim, ctx.sizes, ctx.present = dim, sizes, present
+        out = gs[0].new_zeros(shape) if gs else torch.zeros(shape)
+        it = iter(gs)
+        off = 0
+        for sz, p in zip(sizes, present):
+            if p:
+                out.narrow(dim, off, sz).copy_(next(it))
+            off += sz
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        pieces = _Split.apply(gout, ctx.dim, ctx.sizes)
+        return (None, None, None, None) + tuple(
+            q for q, p in zip(pieces, ctx.present) if p)
 
 
 def cat(tensors, dim=0):

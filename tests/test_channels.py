@@ -2,6 +2,7 @@
 second and third derivatives equal torch's (float64 gradcheck / gradgradcheck plus an explicit
 third-order comparison), with every order one cat / split / swap op (the PINN residual
 differentiates FlowNet three times, reference pinn.py:72-111)."""
+import pytest
 import torch
 
 from op import channels
@@ -61,3 +62,27 @@ def test_sum2x2_adjoint_pair_cpu_f64():
     assert torch.autograd.gradgradcheck(_sum2x2, (x,))
     y = _sum2x2(x)
     assert torch.allclose(y, x.reshape(2, 3, 2, 2, 3, 2).sum((3, 5)))
+
+
+@pytest.mark.parametrize("used", [(0,), (1, 3), (0, 1, 2, 3), (2,)])
+def test_split_backward_with_unused_pieces(used):
+    """channels.split whose pieces are only partly used (PINN.forward_residual_copies reads
+    copy 0 of most splits): the backward fills the unused pieces' rows with zeros in one op
+    (_PadCat) -- same gradient as torch.split, and differentiable again (gradcheck /
+    gradgradcheck in float64)."""
+    torch.manual_seed(0)
+    x = torch.randn(8, 3, 2, dtype=torch.float64, requires_grad=True)
+
+    def f(split):
+        def g(x):
+            ps = split(x * 1.5)
+            return sum(((ps[i] ** 2) * (i + 1)).sum() for i in used)
+        return g
+
+    ours = f(lambda t: channels.split(t, (2, 2, 2, 2), 0))
+    ref = f(lambda t: torch.split(t, [2, 2, 2, 2], 0))
+    g1, = torch.autograd.grad(ours(x), x)
+    g2, = torch.autograd.grad(ref(x), x)
+    assert torch.equal(g1, g2)
+    assert torch.autograd.gradcheck(ours, (x,))
+    assert torch.autograd.gradgradcheck(ours, (x,))
