@@ -35,6 +35,27 @@ __global__ __launch_bounds__(256) void fused_bias_act_kernel(
   }
 }
 
+// no bias, float32, 16-B aligned, n % 4 == 0 (FlowNet's LeakyReLU(0.1) and its derivative
+// mask, 242 launches per PINN step at B = 8): four elements per thread, the act / grad case
+// resolved at compile time -- the same per-element arithmetic as above
+template <int CASE>
+__global__ __launch_bounds__(256) void lrelu4_kernel(const float4* __restrict__ x,
+                                                     const float4* __restrict__ ref,
+                                                     float4* __restrict__ out, int64_t n4,
+                                                     float alpha, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = x[i];
+    const float4 r = CASE == 31 ? ref[i] : v;
+    float4 y;
+    y.x = ((CASE == 30 ? v.x : r.x) > 0.f ? v.x : v.x * alpha) * scale;
+    y.y = ((CASE == 30 ? v.y : r.y) > 0.f ? v.y : v.y * alpha) * scale;
+    y.z = ((CASE == 30 ? v.z : r.z) > 0.f ? v.z : v.z * alpha) * scale;
+    y.w = ((CASE == 30 ? v.w : r.w) > 0.f ? v.w : v.w * alpha) * scale;
+    out[i] = y;
+  }
+}
+
 template <typename T>
 int fba_impl(const T* x, const T* bias, const T* refer, T* out, int64_t n, int64_t step_b,
              int64_t size_b, int act, int grad, T alpha, T scale, void* stream) {
@@ -44,6 +65,24 @@ int fba_impl(const T* x, const T* bias, const T* refer, T* out, int64_t n, int64
   BPK_REQUIRE(grad >= 0 && grad <= 2, "fused_bias_act: grad must be 0, 1 or 2");
   if (bias) BPK_REQUIRE(step_b > 0 && size_b > 0, "fused_bias_act: bad bias geometry");
   if (n == 0) return BPK_OK;
+  const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(refer) |
+                    reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (sizeof(T) == 4 && !bias && act == 3 && (grad == 0 || (grad == 1 && refer)) && n % 4 == 0 &&
+      al) {
+    const int64_t n4 = n / 4;
+    const int64_t blocks = std::min<int64_t>(bpk::ceil_div(n4, 256), 256 * 16);
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* r4 = reinterpret_cast<const float4*>(refer);
+    float4* o4 = reinterpret_cast<float4*>(out);
+    if (grad == 0)
+      hipLaunchKernelGGL(lrelu4_kernel<30>, dim3((unsigned)blocks), dim3(256), 0,
+                         bpk::as_stream(stream), x4, r4, o4, n4, (float)alpha, (float)scale);
+    else
+      hipLaunchKernelGGL(lrelu4_kernel<31>, dim3((unsigned)blocks), dim3(256), 0,
+                         bpk::as_stream(stream), x4, r4, o4, n4, (float)alpha, (float)scale);
+    BPK_LAUNCH_CHECK("fused_bias_act");
+    return BPK_OK;
+  }
   const int64_t blocks = std::min<int64_t>(bpk::ceil_div(n, 256), 256 * 16);
   hipLaunchKernelGGL(fused_bias_act_kernel<T>, dim3((unsigned)blocks), dim3(256), 0,
                      bpk::as_stream(stream), x, bias, refer, out, n, step_b, size_b, act, grad,

@@ -111,8 +111,9 @@ def test_fused_leaky_relu_grads_f64(hip):
     assert torch.autograd.gradgradcheck(f, (x, b))
 
 
+@pytest.mark.parametrize("shape", [(3, 5, 7, 9), (4, 8, 16, 16)])  # scalar / float4 kernel
 @pytest.mark.parametrize("slope", [0.1, 0.01])
-def test_native_leaky_relu_bit_identical_to_aten_to_third_order(hip, slope):
+def test_native_leaky_relu_bit_identical_to_aten_to_third_order(hip, slope, shape):
     """op.fused_act.leaky_relu (FlowNet's activation on the native kernel): forward, first,
     second and third derivatives bit-identical to F.leaky_relu under autograd, and f64
     gradcheck / gradgradcheck.  (The mask's derivative is not materialized: a derivative whose
@@ -120,9 +121,9 @@ def test_native_leaky_relu_bit_identical_to_aten_to_third_order(hip, slope):
     import torch.nn.functional as F
     from op.fused_act import leaky_relu
     g = torch.Generator().manual_seed(5)
-    x0 = torch.randn(3, 5, 7, 9, generator=g)
+    x0 = torch.randn(*shape, generator=g)
     x0[0, 0, 0, :3] = 0.0  # the x == 0 boundary takes the slope branch in both
-    w = torch.randn(3, 5, 7, 9, generator=g).to(hip)
+    w = torch.randn(*shape, generator=g).to(hip)
 
     def derivs(fn):
         x = x0.to(hip).requires_grad_()
