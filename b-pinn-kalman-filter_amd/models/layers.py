@@ -81,6 +81,20 @@ def temb_proj(dense_m: nn.Linear, act, temb):
     return dense(dense_m, act(temb))
 
 
+_GN_FANOUT = os.environ.get("BPK_GN_FANOUT", "0") == "1"  # A/B switch (gn_act_fanout)
+
+
+def gn_act_fanout(x, gn: nn.GroupNorm, act=None):
+    """(gn_act(x, gn, act), x) for a residual block whose input also feeds its skip: under
+    autograd the skip's gradient is added inside the GroupNorm backward kernel
+    (op.norm_act.group_norm_act_fanout) instead of by a separate accumulation launch."""
+    if (_GN_FANOUT and torch.is_grad_enabled() and x.requires_grad and x.is_cuda
+            and x.dtype == torch.float32 and (act is None or isinstance(act, nn.SiLU))):
+        from op.norm_act import group_norm_act_fanout
+        return group_norm_act_fanout(x, gn, ACT_NONE if act is None else ACT_SILU)
+    return gn_act(x, gn, act), x
+
+
 def gn_act(x, gn: nn.GroupNorm, act=None, bias_nc=None):
     """act(GroupNorm(x + bias_nc)); SiLU (and no activation) fuse into one HIP launch."""
     if act is None:
@@ -197,7 +211,7 @@ def gn_silu_conv(x, gn: nn.GroupNorm, conv: nn.Conv2d, bias_nc=None, conv_bias=N
 
 
 def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act, bias_nc=None,
-                    conv_bias=None, skip=None, div=1.0, give=None, take=None):
+                    conv_bias=None, skip=None, div=1.0, give=None, take=None, fanout=False):
     """gn_silu_conv under autograd for an eval-mode block (DPS: gradients of the score w.r.t.
     the input through the net): conv(SiLU(GroupNorm(x + bias_nc))) [+ residual tail] with the
     normalization inside the Winograd conv's input load and a backward that recomputes it
@@ -205,15 +219,28 @@ def gn_silu_conv_ad(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act
     record, another activation, a conv the kernel does not take).  Training keeps the unfused
     composition: on the DSM and CIFAR train steps the fused form measured 2.8 % and 1.5 %
     slower (the weight gradient's per-element SiLU in its patch load, the igemm choice lost
-    on small images), DPS 4.1 % faster (profiles/r05_gn_conv_ad_ab.txt)."""
+    on small images), DPS 4.1 % faster (profiles/r05_gn_conv_ad_ab.txt).
+    Returns (output, x') or None; x' is x itself, or with fanout=True (a block whose shortcut
+    conv reads x) x through the fused Function, so the shortcut's gradient joins the GroupNorm
+    backward's pass instead of an accumulation launch."""
     if not (_GN_CONV_AD and (not module.training or _GN_CONV_AD_TRAIN) and torch.is_grad_enabled()
             and isinstance(act, nn.SiLU) and _is_3x3(x, conv)):
         return None
     if skip is not None and skip.shape[1] != conv.out_channels:
         return None
-    return conv_op.gn_silu_conv3x3_ad(x, gn.num_groups, gn.weight if gn.affine else None,
-                                      gn.bias if gn.affine else None, gn.eps, conv.weight,
-                                      conv_bias, skip, div, bias_nc, give, take)
+    fanout = fanout and _GN_FANOUT and x.requires_grad
+    r = conv_op.gn_silu_conv3x3_ad(x, gn.num_groups, gn.weight if gn.affine else None,
+                                   gn.bias if gn.affine else None, gn.eps, conv.weight,
+                                   conv_bias, skip, div, bias_nc, give, take, fanout)
+    if r is None or not fanout:
+        return r if r is None else (r, x)
+    return r
+
+
+def gn_silu_conv_ad_1(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, act, **kw):
+    """gn_silu_conv_ad's output alone (or None)"""
+    r = gn_silu_conv_ad(module, x, gn, conv, act, **kw)
+    return None if r is None else r[0]
 
 
 @contextlib.contextmanager
@@ -533,19 +560,23 @@ class ResnetBlockDDPM(nn.Module):
                 h = conv_nobias(gn_act(x, self.GroupNorm_0, self.act), self.Conv_0)
             return self._fused_tail(h, x, None, temb)
         link = skip_link(self, self.in_ch == self.out_ch and _dropout_off(self.Dropout_0))
-        h = gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act, take=link)
-        if h is None:
+        r = gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act, take=link,
+                            fanout=self.in_ch != self.out_ch)
+        if r is None:
             link = None
-            h = gn_act(x, self.GroupNorm_0, self.act)
+            h, x = gn_act_fanout(x, self.GroupNorm_0, self.act)
             h = conv_nobias(h, self.Conv_0)
+        else:
+            h, x = r
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
         if temb is not None:
             bias_nc = bias_nc + temb_proj(self.Dense_0, self.act, temb)
         if self.in_ch != self.out_ch:
             x = self.Conv_2(x) if self.conv_shortcut else self.NIN_0(x)
         if _dropout_off(self.Dropout_0):
-            out = gn_silu_conv_ad(self, h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
-                                  self.Conv_1.bias, x, 1.0, give=link)
+            out = gn_silu_conv_ad_1(self, h, self.GroupNorm_1, self.Conv_1, self.act,
+                                    bias_nc=bias_nc, conv_bias=self.Conv_1.bias, skip=x, div=1.0,
+                                    give=link)
             if out is not None:
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)

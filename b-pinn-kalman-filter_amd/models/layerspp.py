@@ -203,7 +203,7 @@ class ResnetBlockDDPMpp(nn.Module):
         self.conv_shortcut = conv_shortcut
 
     def forward(self, x, temb=None):
-        h = gn_act(x, self.GroupNorm_0, self.act)
+        h, x = layers.gn_act_fanout(x, self.GroupNorm_0, self.act)
         h = conv_nobias(h, self.Conv_0)
         bias_nc = self.Conv_0.bias[None, :].expand(x.shape[0], -1)
         if temb is not None:
@@ -298,12 +298,15 @@ class ResnetBlockBigGANpp(nn.Module):
             # eval-mode autograd (DPS): the same fusion, its backward recomputing the normalization
             link = layers.skip_link(self, self.in_ch == self.out_ch
                                     and layers._dropout_off(self.Dropout_0))
-            h = layers.gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act,
-                                       take=link)
-            if h is None:
+            r = layers.gn_silu_conv_ad(self, x, self.GroupNorm_0, self.Conv_0, self.act,
+                                       take=link, fanout=self.in_ch != self.out_ch)
+            h = None
+            if r is None:
                 link = None
+            else:
+                h, x = r
         if h is None:
-            h = gn_act(x, self.GroupNorm_0, self.act)
+            h, x = layers.gn_act_fanout(x, self.GroupNorm_0, self.act)
             h = self._resample(h)
             x = self._resample(x)
             h = conv_nobias(h, self.Conv_0)
@@ -323,8 +326,9 @@ class ResnetBlockBigGANpp(nn.Module):
             if out is not None:
                 return out
         elif layers._dropout_off(self.Dropout_0):
-            out = layers.gn_silu_conv_ad(self, h, self.GroupNorm_1, self.Conv_1, self.act, bias_nc,
-                                         bias, x, div, give=link)
+            out = layers.gn_silu_conv_ad_1(self, h, self.GroupNorm_1, self.Conv_1, self.act,
+                                           bias_nc=bias_nc, conv_bias=bias, skip=x, div=div,
+                                           give=link)
             if out is not None:
                 return out
         h = gn_act(h, self.GroupNorm_1, self.act, bias_nc)

@@ -1149,11 +1149,13 @@ class _GNSiLUConv3x3(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats, give=None,
-                take=None):
+                take=None, fanout=False):
         from .norm_act import group_norm_affine_stats
         mark_inputs(ctx, x, bias_nc, gamma, beta, weight, bias, skip, G, eps, div, stats, give,
-                    take)
-        ctx.give, ctx.take = give, take
+                    take, fanout)
+        ctx.give, ctx.take, ctx.fanout = give, take, fanout
+        if fanout:
+            ctx.set_materialize_grads(False)
         ss, mean, rstd = group_norm_affine_stats(x, G, gamma, beta, eps, bias_nc)
         x = x.detach()
         if gn_partials(x) is None:
@@ -1162,13 +1164,17 @@ class _GNSiLUConv3x3(torch.autograd.Function):
         ctx.save_for_backward(x, bias_nc, gamma, beta, weight, mean, rstd, ss)
         ctx.G, ctx.div = G, float(div)
         ctx.has_bias, ctx.has_skip = bias is not None, skip is not None
-        return y
+        # fanout: (y, x) -- the block's input for its 1x1 / conv shortcut, whose gradient then
+        # arrives here with gy and joins the GroupNorm backward's pass as its addend
+        return (y, x.view_as(x)) if fanout else y
 
     @staticmethod
     @once_differentiable
-    def backward(ctx, gy):
+    def backward(ctx, gy, dskip=None):
         from .norm_act import ACT_SILU, affine_silu, group_norm_act_backward
         x, bnc, gamma, beta, w, mean, rstd, ss = ctx.saved_tensors
+        if gy is None:  # fanout: only the shortcut's gradient came back
+            return (dskip,) + (None,) * 13
         gy = gy.contiguous()
         if ctx.div != 1.0:
             gy = gy / ctx.div
@@ -1195,12 +1201,16 @@ class _GNSiLUConv3x3(torch.autograd.Function):
             addend, ctx.take.g = ctx.take.g, None
             if not want_x:
                 addend = None  # x wants no gradient: neither did the skip that sent it
+        if dskip is not None:
+            addend = dskip if addend is None else addend + dskip
         if want_x or want_bnc or want_g or want_b:
             ga = _fwd_ft_impl(gy, w)
             dx, d_bnc, dgamma, dbeta = group_norm_act_backward(
                 ga, x, bnc, gamma, beta, mean, rstd, ctx.G, ACT_SILU, want_bnc, want_g, want_b,
                 addend=addend if want_x else None)
-        return dx, d_bnc, dgamma, dbeta, gw, gcb, gskip, None, None, None, None, None, None
+        elif dskip is not None:
+            dx = dskip
+        return dx, d_bnc, dgamma, dbeta, gw, gcb, gskip, None, None, None, None, None, None, None
 
 
 def gn_silu_conv3x3_ad_supported(x, weight):
@@ -1224,11 +1234,12 @@ class SkipLink:
 
 
 def gn_silu_conv3x3_ad(x, num_groups, gamma, beta, eps, weight, bias=None, skip=None, div=1.0,
-                       bias_nc=None, give=None, take=None):
+                       bias_nc=None, give=None, take=None, fanout=False):
     """(skip + conv3x3(SiLU(GroupNorm(x + bias_nc)), weight) + bias) / div, differentiable
     (first order), the normalization inside the conv's input load; the output carries
     GroupNorm partial statistics for the next GroupNorm when the 16-cin kernel runs.  None
-    when the shape does not qualify (gn_silu_conv3x3_ad_supported)."""
+    when the shape does not qualify (gn_silu_conv3x3_ad_supported).  fanout=True: returns
+    (y, x), the x for the block's shortcut conv (its gradient is added in this backward)."""
     require_hip(x, weight, bias, skip, bias_nc, what="gn_silu_conv3x3_ad")
     if not gn_silu_conv3x3_ad_supported(x, weight):
         return None
@@ -1236,7 +1247,7 @@ def gn_silu_conv3x3_ad(x, num_groups, gamma, beta, eps, weight, bias=None, skip=
         return None
     stats = bool(wino_supported(x, weight))
     return _GNSiLUConv3x3.apply(x, bias_nc, gamma, beta, weight, bias, skip, num_groups,
-                                float(eps), float(div), stats, give, take)
+                                float(eps), float(div), stats, give, take, bool(fanout))
 
 
 def up2_supported(x, weight):

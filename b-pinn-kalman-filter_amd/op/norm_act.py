@@ -109,6 +109,41 @@ def group_norm_act_backward(dy, x, bnc, weight, bias, mean, rstd, G, act, want_b
     return dx, d_bnc, dw, dbeta
 
 
+class _GroupNormActFanout(Function):
+    """(act(GroupNorm(x)), x): a residual block's input feeds its first GroupNorm and its skip
+    (identity, 1x1 projection or resampling).  Both gradients reach this one node and the
+    skip's is added inside the GroupNorm backward kernel (bpk_group_norm_bwd_add_f32's addend)
+    instead of by an autograd accumulation launch over the block's input.  First order (the
+    training backward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, num_groups, eps, act):
+        ctx.set_materialize_grads(False)
+        y = _GroupNormAct.forward(ctx, x, None, weight, bias, num_groups, eps, act)
+        mark_inputs(ctx, x, weight, bias, num_groups, eps, act)  # this Function's positions
+        return y, x.view_as(x)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy, dskip):
+        x, bnc, weight, bias, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            return dskip, None, None, None, None, None
+        dx, _, dw, dbeta = group_norm_act_backward(
+            dy, x, None, weight, bias, mean, rstd, ctx.num_groups, ctx.act, False,
+            weight is not None and want_grad(ctx, 1), bias is not None and want_grad(ctx, 2),
+            addend=dskip)
+        return dx, dw, dbeta, None, None, None
+
+
+def group_norm_act_fanout(x, gn: torch.nn.GroupNorm, act: int = ACT_SILU):
+    """(act(GroupNorm(x)), x) with the skip's gradient joining the norm's inside the backward
+    kernel (see _GroupNormActFanout)."""
+    w = gn.weight if gn.affine else None
+    b = gn.bias if gn.affine else None
+    return _GroupNormActFanout.apply(x, w, b, gn.num_groups, gn.eps, act)
+
+
 def group_norm_act(x, gn: torch.nn.GroupNorm, act: int = ACT_SILU, bias_nc=None):
     """act(GroupNorm(x + bias_nc)) using the parameters of an nn.GroupNorm module."""
     w = gn.weight if gn.affine else None

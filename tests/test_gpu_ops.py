@@ -1953,3 +1953,81 @@ def test_eval_block_higher_order_autograd_opt_out(hip):
         layers._GN_CONV_AD, layers._SKIP_LINK = old
     assert torch.isfinite(a).all() and torch.equal(a, b)
     assert layers._GN_CONV_AD  # restored
+
+
+@pytest.mark.parametrize("kind,cin,cout,updown", [
+    ("biggan", 64, 64, None), ("biggan", 64, 128, None), ("biggan", 64, 64, "down"),
+    ("biggan", 64, 64, "up"), ("ddpmpp", 64, 64, None), ("ddpmpp", 64, 128, None)])
+def test_gn_fanout_training_block_grads_bit_identical(hip, kind, cin, cout, updown):
+    """Training-mode residual blocks with the GroupNorm fan-out (layers.gn_act_fanout: the
+    skip's gradient -- identity, 1x1 projection, FIR resampling -- added inside the GroupNorm
+    backward kernel): the block input's gradient and every parameter gradient bit-identical to
+    the plain form, whose autograd adds the two gradients of the input."""
+    from models import layers
+    from models import layerspp as lpp
+    torch.manual_seed(2)
+    if kind == "biggan":
+        blk = lpp.ResnetBlockBigGANpp(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=32,
+                                      up=updown == "up", down=updown == "down", fir=True,
+                                      dropout=0.0, skip_rescale=True).to(hip).train()
+    else:
+        blk = lpp.ResnetBlockDDPMpp(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=32,
+                                    dropout=0.0, skip_rescale=True).to(hip).train()
+    x0 = torch.randn(4, cin, 16, 16, device=hip)
+    temb = torch.randn(4, 32, device=hip)
+
+    def grads(fan):
+        prev = layers._GN_FANOUT
+        layers._GN_FANOUT = fan
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = blk(x * 1.0, temb)
+            (y * torch.linspace(-1, 1, y.numel(), device=hip).view_as(y)).sum().backward()
+        finally:
+            layers._GN_FANOUT = prev
+        return [y.detach(), x.grad] + [p.grad for p in blk.parameters()]
+
+    for a, b in zip(grads(True), grads(False)):
+        assert a is not None and b is not None and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kind,cin,cout", [("biggan", 128, 256), ("ddpm", 256, 128),
+                                           ("biggan", 128, 128)])
+def test_gn_fanout_eval_fused_block_bit_identical(hip, kind, cin, cout):
+    """Eval-mode blocks under autograd (DPS) on the fused GroupNorm+SiLU conv: with the fan-out
+    (the 1x1 / conv shortcut's gradient of the block input added in the fused conv's GroupNorm
+    backward, op.conv.gn_silu_conv3x3_ad(fanout=True)) the output, d/dx and every parameter
+    gradient are bit-identical to the accumulation by autograd; identity-skip blocks keep the
+    skip link."""
+    import models.layers as layers
+    import models.layerspp as lpp
+    torch.manual_seed(1)
+    if kind == "biggan":
+        blk = lpp.ResnetBlockBigGANpp(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=64,
+                                      skip_rescale=True, init_scale=0., dropout=0.0)
+    else:
+        blk = layers.ResnetBlockDDPM(act=torch.nn.SiLU(), in_ch=cin, out_ch=cout, temb_dim=64,
+                                     dropout=0.0)
+    blk = blk.to(hip).eval()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    x0 = torch.randn(4, cin, 16, 16, device=hip)
+    temb = torch.randn(4, 64, device=hip)
+    gout = torch.randn(4, cout, 16, 16, device=hip)
+
+    def run(fan):
+        prev = layers._GN_FANOUT
+        layers._GN_FANOUT = fan
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = blk(x * 1.0, temb)
+            (y * gout).sum().backward()
+        finally:
+            layers._GN_FANOUT = prev
+        return [y.detach(), x.grad] + [p.grad for p in blk.parameters()]
+
+    for a, b in zip(run(True), run(False)):
+        assert torch.equal(a, b)
