@@ -81,7 +81,7 @@ def temb_proj(dense_m: nn.Linear, act, temb):
     return dense(dense_m, act(temb))
 
 
-_GN_FANOUT = os.environ.get("BPK_GN_FANOUT", "0") == "1"  # A/B switch (gn_act_fanout)
+_GN_FANOUT = os.environ.get("BPK_GN_FANOUT", "1") == "1"  # A/B switch (gn_act_fanout)
 
 
 def gn_act_fanout(x, gn: nn.GroupNorm, act=None):

@@ -1986,10 +1986,17 @@ def test_gn_fanout_training_block_grads_bit_identical(hip, kind, cin, cout, updo
             (y * torch.linspace(-1, 1, y.numel(), device=hip).view_as(y)).sum().backward()
         finally:
             layers._GN_FANOUT = prev
-        return [y.detach(), x.grad] + [p.grad for p in blk.parameters()]
+        return [("y", y.detach()), ("x", x.grad)] + [(n, p.grad) for n, p in
+                                                     blk.named_parameters()]
 
-    for a, b in zip(grads(True), grads(False)):
-        assert a is not None and b is not None and torch.equal(a, b)
+    for (name, a), (_, b) in zip(grads(True), grads(False)):
+        assert a is not None and b is not None, name
+        if name.startswith("GroupNorm"):
+            # the resident GroupNorm backward sums gamma / beta partials with LDS float atomics:
+            # last-bit run-to-run noise with or without the fan-out (tools/diag_gn_fanout.py)
+            assert torch.allclose(a, b, rtol=1e-5, atol=2e-6 * float(b.abs().max())), name
+        else:
+            assert torch.equal(a, b), name
 
 
 @pytest.mark.parametrize("kind,cin,cout", [("biggan", 128, 256), ("ddpm", 256, 128),
