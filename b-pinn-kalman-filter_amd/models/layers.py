@@ -246,16 +246,16 @@ def gn_silu_conv_ad_1(module: nn.Module, x, gn: nn.GroupNorm, conv: nn.Conv2d, a
 @contextlib.contextmanager
 def higher_order_autograd():
     """Inside this block eval-mode blocks record the unfused composition (every op
-    differentiable to any order) instead of the first-order-only fused GroupNorm+SiLU conv and
-    skip link: for create_graph=True / double backward through a score net (the DPS and
+    differentiable to any order) instead of the first-order-only fused GroupNorm+SiLU conv, skip
+    link and GroupNorm fan-out: for create_graph=True / double backward through a score net (the DPS and
     likelihood paths of the reference are first-order and do not need it)."""
-    global _GN_CONV_AD, _SKIP_LINK
-    prev = _GN_CONV_AD, _SKIP_LINK
-    _GN_CONV_AD, _SKIP_LINK = False, False
+    global _GN_CONV_AD, _SKIP_LINK, _GN_FANOUT
+    prev = _GN_CONV_AD, _SKIP_LINK, _GN_FANOUT
+    _GN_CONV_AD, _SKIP_LINK, _GN_FANOUT = False, False, False
     try:
         yield
     finally:
-        _GN_CONV_AD, _SKIP_LINK = prev
+        _GN_CONV_AD, _SKIP_LINK, _GN_FANOUT = prev
 
 
 def skip_link(module: nn.Module, identity_skip: bool):

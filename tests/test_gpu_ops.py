@@ -1945,14 +1945,14 @@ def test_eval_block_higher_order_autograd_opt_out(hip):
         second()
     with layers.higher_order_autograd():
         a = second()
-    old = layers._GN_CONV_AD, layers._SKIP_LINK
-    layers._GN_CONV_AD, layers._SKIP_LINK = False, False
+    old = layers._GN_CONV_AD, layers._SKIP_LINK, layers._GN_FANOUT
+    layers._GN_CONV_AD, layers._SKIP_LINK, layers._GN_FANOUT = False, False, False
     try:
         b = second()
     finally:
-        layers._GN_CONV_AD, layers._SKIP_LINK = old
+        layers._GN_CONV_AD, layers._SKIP_LINK, layers._GN_FANOUT = old
     assert torch.isfinite(a).all() and torch.equal(a, b)
-    assert layers._GN_CONV_AD  # restored
+    assert layers._GN_CONV_AD and layers._GN_FANOUT  # restored
 
 
 @pytest.mark.parametrize("kind,cin,cout,updown", [
