@@ -297,7 +297,8 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, float* __restrict__ dx,
     float* __restrict__ dgamma_nc, float* __restrict__ dbeta_nc, int C, int HW, int G, int act,
     const float* __restrict__ addend) {
-  extern __shared__ float sdyn[];  // [T/64] reduce buffer + 2*cpg channel partials
+  // [T/64] reduce buffer + 2*cpg channel partials + 2 * VPT * T/64 wave-slice partials
+  extern __shared__ float sdyn[];
   float* sbuf = sdyn;
   float* s_dg = sdyn + T / kWave;
   const int ng = blockIdx.x;
@@ -305,18 +306,31 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
   const int g = ng - n * G;
   const int cpg = C / G;
   const int S = cpg * HW;
+  float* s_sl = s_dg + 2 * cpg;
   const int64_t base = ((int64_t)n * C + (int64_t)g * cpg) * HW;
   const int tid = threadIdx.x;
   const float mean = mean_in[ng];
   const float rstd = rstd_in[ng];
+  // gamma / beta partials per channel in a fixed order (the result must not depend on the
+  // order waves finish in): L = units of W elements per channel plane.  L % 64 == 0: every
+  // (k, wave) slice of 64 units lies in one channel -- butterfly sum per slice, then the
+  // slices of a channel in slice order; L < 64 dividing 64: a channel is one aligned lane
+  // segment of one slice -- a butterfly within the segment gives its sum.  Other planes
+  // (H W not a power-of-two multiple): LDS atomics, order-dependent in the last bits.
+  const int L = HW / W;
+  const bool slice_mode = L % kWave == 0;
+  const bool seg_mode = !slice_mode && L < kWave && kWave % L == 0;
   for (int i = tid; i < 2 * cpg; i += T) s_dg[i] = 0.f;
   __syncthreads();
 
   float xh[VPT][W], dxh[VPT][W];
   float la = 0.f, lb = 0.f;
+  const int lane = tid & (kWave - 1), wave = tid / kWave;
+  const bool ordered = (dgamma_nc || dbeta_nc) && (slice_mode || seg_mode);
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int e = (k * T + tid) * W;
+    float pg = 0.f, pb = 0.f;
     if (e < S) {
       const int cl = e / HW;
       const int c = g * cpg + cl;
@@ -326,7 +340,6 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
       float xv[W], gv[W];
       Vec<W>::load(x + base + e, xv);
       Vec<W>::load(dy + base + e, gv);
-      float pg = 0.f, pb = 0.f;
 #pragma unroll
       for (int q = 0; q < W; ++q) {
         const float xhat = (xv[q] + b - mean) * rstd;
@@ -338,9 +351,40 @@ __global__ __launch_bounds__(T) void gn_bwd_resident(
         la += dxh[k][q];
         lb += dxh[k][q] * xhat;
       }
-      if (dgamma_nc || dbeta_nc) {
+      if ((dgamma_nc || dbeta_nc) && !ordered) {
         atomicAdd(&s_dg[cl], pg);
         atomicAdd(&s_dg[cpg + cl], pb);
+      }
+    }
+    if (ordered) {  // every lane takes part (zeros past the slab)
+      const int span = slice_mode ? kWave : L;
+      for (int off = span >> 1; off > 0; off >>= 1) {
+        pg += __shfl_xor(pg, off, kWave);
+        pb += __shfl_xor(pb, off, kWave);
+      }
+      if (slice_mode) {
+        if (lane == 0) {
+          s_sl[2 * (k * (T / kWave) + wave)] = pg;
+          s_sl[2 * (k * (T / kWave) + wave) + 1] = pb;
+        }
+      } else if (lane % L == 0) {
+        const int cl = (k * T + tid) / L;  // the segment is channel cl's whole plane
+        if (cl < cpg) {
+          s_dg[cl] = pg;
+          s_dg[cpg + cl] = pb;
+        }
+      }
+    }
+  }
+  if (ordered) {
+    __syncthreads();
+    if (slice_mode) {  // channel c = slices [c L / 64, (c + 1) L / 64), summed in order
+      const int per = L / kWave;
+      for (int i = tid; i < 2 * cpg; i += T) {
+        const int c = i % cpg, which = i / cpg;
+        float acc = 0.f;
+        for (int j = c * per; j < (c + 1) * per; ++j) acc += s_sl[2 * j + which];
+        s_dg[i] = acc;
       }
     }
   }
@@ -654,7 +698,7 @@ int bwd_resident_dispatch(int64_t S, const float* dy, const float* x, const floa
   dim3 grid(N * G);
 #define GN_BWD(T_, V_)                                                                         \
   if (units <= (int64_t)(T_) * (V_)) {                                                         \
-    const size_t sh = sizeof(float) * ((T_) / kWave + 2 * cpg);                                \
+    const size_t sh = sizeof(float) * ((T_) / kWave + 2 * cpg + 2 * (V_) * ((T_) / kWave)); \
     hipLaunchKernelGGL((gn_bwd_resident<T_, V_, W>), grid, dim3(T_), sh, st, dy, x, bias,     \
                        gamma, beta, mean, rstd, dx, dg, db, C, HW, G, act, addend);            \
     BPK_LAUNCH_CHECK("group_norm_bwd_resident");                                              \
