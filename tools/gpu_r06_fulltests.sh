@@ -1,7 +1,7 @@
 #!/bin/bash
 # the driver's round-end GPU tier, rehearsed: pytest -m gpu, then smoke()
 set -o pipefail
-O=gpurun_out/r06full_s2c; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/r06full_s2d; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 1500 python3 -u -m pytest tests/ -x -q -m gpu --timeout 600 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/pytest.log | head -20; exit $rc; }
