@@ -326,12 +326,15 @@ def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
 # "auto" picks by the per-GPU batch, or a fixed 1 / 2 / 4 (1: the reference's seven passes).
 # Measured on configs[3]'s graph step (profiles/r06_pinn_copies.txt): B = 8 (a rank of the 8-GPU
 # point) 26.3 / 32.1 / 33.9 steps/s with 1 / 2 / 4 copies; B = 32 20.7 / 21.4 with 2 / 4;
-# B = 64 14.3 / 15.5 / 13.8 with 1 / 2 / 4 (profiles/r06_pinn_copies.txt).
+# B = 64 14.3 / 15.5 / 13.8 with 1 / 2 / 4 (profiles/r06_pinn_copies.txt).  Re-measured on the
+# final tree (deferred weight gradients, fan-outs; interleaved x3, one box,
+# profiles/r06_pinn_copies_s2/): B = 8 40.7-41.3 with 4 vs 39.1-39.8 with 2; B = 16 32.1-33.3 vs
+# 33.2-34.0; B = 32 23.6-23.8 vs 24.6-25.3 -- two copies from B = 16 on.
 _COPIES = os.environ.get("BPK_PINN_COPIES", "auto")
 # the PINN backward's weight gradients deferred and run two sources per launch
 # (op.conv.deferred_weight_grads); BPK_DEFER_WGRAD=0: autograd's per-node weight gradients
 _DEFER_WGRAD = os.environ.get("BPK_DEFER_WGRAD", "1") == "1"
-_COPIES_AUTO = ((32, 4), (64, 2))  # (largest per-GPU batch, copies); larger batches: 1
+_COPIES_AUTO = ((8, 4), (64, 2))  # (largest per-GPU batch, copies); larger batches: 1
 
 
 def residual_copies(batch, on_gpu=True):
