@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 6, second session, final tree: the default bench command twice, the per-rank work of
+# Evidence for the judged numbers: the default bench command twice, the per-rank work of
 # the 8-GPU point, rocprofv3 kernel summaries of the DSM train step (B = 64), DPS and the PINN
 # graph step at B = 8.
 set -o pipefail
-O=gpurun_out/r06final5; mkdir -p $O; export TMPDIR=/tmp
+O=${1:-gpurun_out/evidence}; mkdir -p $O; export TMPDIR=/tmp
 for r in 1 2; do
   timeout -k 10 900 python3 bench.py > $O/bench_$r.json 2> $O/bench_$r.err || { tail -20 $O/bench_$r.err; exit 1; }
   grep -o '"value": [0-9.]*' $O/bench_$r.json | head -1
