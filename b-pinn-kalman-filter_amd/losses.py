@@ -329,7 +329,8 @@ def get_prelim_step_fn(config, train, optimize_fn, is_bpinn=False, ctx=None):
 # B = 64 14.3 / 15.5 / 13.8 with 1 / 2 / 4 (profiles/r06_pinn_copies.txt).  Re-measured on the
 # final tree (deferred weight gradients, fan-outs; interleaved x3, one box,
 # profiles/r06_pinn_copies_s2/): B = 8 40.7-41.3 with 4 vs 39.1-39.8 with 2; B = 16 32.1-33.3 vs
-# 33.2-34.0; B = 32 23.6-23.8 vs 24.6-25.3 -- two copies from B = 16 on.
+# 33.2-34.0; B = 32 23.6-23.8 vs 24.6-25.3 -- two copies from B = 16 on; B = 64 15.4 / 17.2 /
+# 15.0 with 1 / 2 / 4 (b64.txt).
 _COPIES = os.environ.get("BPK_PINN_COPIES", "auto")
 # the PINN backward's weight gradients deferred and run two sources per launch
 # (op.conv.deferred_weight_grads); BPK_DEFER_WGRAD=0: autograd's per-node weight gradients
